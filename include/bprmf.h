@@ -1,0 +1,156 @@
+/*
+ * bprmf.h — C ABI of the MI355X-native BPR-MF training path (libbprmf_amd.so).
+ *
+ * Drop-in boundary for the reference's BPR-MF path (NotFoundGG/recommend-lib):
+ *   model      BPRMFRecommender.py:28-50   class BPR(nn.Module): two nn.Embedding tables, forward()
+ *   step       BPRMFRecommender.py:172-176 zero_grad / forward / -(x).sigmoid().log().sum() / SGD(wd)
+ *   sampler    util/data_loader.py:667-700 BPRData.ng_sample / __getitem__ -> (u, i, j)
+ *   surface    util/matrix_factorization.pyx:81-167 fit()/predict() convention (ValueError on bad ids)
+ * The reference has no FFI; a maintainer binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - every function returns 0 (BPRMF_OK) or a negative bprmf_status; bprmf_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - host buffers are caller-owned; the library owns device memory.  `_dev` functions take device
+ *     pointers (e.g. torch tensors' data_ptr()) and run on the handle's stream (bprmf_set_stream).
+ *   - a handle is not thread-safe: one host thread per handle.  One handle per GPU / process.
+ *   - tables are row-major fp32 [rows, factor_num] at the ABI (device rows are padded internally).
+ *   - weight decay is applied lazily: get_weights/score see the exact dense-decay values.
+ */
+#ifndef BPRMF_H
+#define BPRMF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  BPRMF_OK = 0,
+  BPRMF_E_INVALID = -1,     /* bad argument (ValueError in the reference surface) */
+  BPRMF_E_RANGE = -2,       /* user/item id out of range (IndexError / 'Invalid user code') */
+  BPRMF_E_HIP = -3,         /* HIP runtime error */
+  BPRMF_E_STATE = -4,       /* call order (e.g. train before set_train) */
+  BPRMF_E_NO_NEGATIVE = -5, /* a user has every item as positive: ng_sample would never end */
+  BPRMF_E_UNSUPPORTED = -6
+} bprmf_status;
+
+typedef struct {
+  int64_t user_num;     /* rows of embed_user  (BPRMFRecommender.py:36) — global count */
+  int64_t item_num;     /* rows of embed_item  (BPRMFRecommender.py:37) — global count */
+  int32_t factor_num;   /* --factor_num        (BPRMFRecommender.py:78-81) */
+  float lr;             /* --lr                (BPRMFRecommender.py:58-61) */
+  float weight_decay;   /* --wd                (BPRMFRecommender.py:62-65, SGD weight_decay :154) */
+  int32_t batch_size;   /* --batch_size        (BPRMFRecommender.py:66-69), per process */
+  int32_t num_ng;       /* --num_ng            (BPRMFRecommender.py:82-85) */
+  float init_std;       /* nn.init.normal_(std=0.01) (BPRMFRecommender.py:39-40) */
+  uint64_t seed;        /* seeds init, sampler and shuffle (the reference is unseeded) */
+  int32_t device;       /* HIP device ordinal */
+  int32_t rank;         /* shard of this handle: owns users u%world==rank, items i%world==rank */
+  int32_t world;        /* 1 for a single GPU */
+  int32_t reserved[4];
+} bprmf_config;
+
+typedef struct {
+  int64_t triplets;     /* triplets processed by the call */
+  int64_t steps;        /* optimizer steps taken by the call */
+  double loss;          /* sum over the call of -log(sigmoid(pred_i - pred_j)) (BPRMFRecommender.py:174) */
+  double seconds;       /* device wall time of the call (HIP events) */
+} bprmf_stats;
+
+/* live kernel timing (HIP events around every launch of each kind while enabled) */
+enum { BPRMF_KPROF_SAMPLE = 0, BPRMF_KPROF_FWD_SCATTER = 1, BPRMF_KPROF_APPLY = 2, BPRMF_KPROF_KINDS = 4 };
+typedef struct {
+  int64_t count[4];     /* launches recorded per kind */
+  double ms[4];         /* summed device time per kind (ms) */
+} bprmf_kprof;
+
+typedef struct bprmf_handle bprmf_handle;
+
+/* ---- lifecycle ---------------------------------------------------------------------------- */
+/* replaces BPR.__init__ + optim.SGD(...) (BPRMFRecommender.py:29-40,148-154) */
+int bprmf_create(const bprmf_config* cfg, bprmf_handle** out);
+int bprmf_destroy(bprmf_handle* h);
+const char* bprmf_last_error(void);
+int bprmf_version(void);
+/* Run on this hipStream_t (NULL = the handle's own stream). */
+int bprmf_set_stream(bprmf_handle* h, void* hip_stream);
+int bprmf_synchronize(bprmf_handle* h);
+
+/* ---- input -------------------------------------------------------------------------------- */
+/* Train positives in features order (load_mat train list + dok train_mat, util/data_loader.py:
+ * 538-545; BPRData.__init__ :668-678).  Global ids; a sharded handle keeps its own users' rows. */
+int bprmf_set_train(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz);
+/* Same, with extra (user, item) pairs that are never drawn as negatives: the keys of a train_mat
+ * that holds more than `features` (BPRData(features, num_item, train_mat), data_loader.py:668). */
+int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz,
+                       const int32_t* ex_users, const int32_t* ex_items, int64_t n_ex);
+/* Triplets and steps of one epoch of this handle (BPRData.__len__ :692-693, DataLoader len). */
+int bprmf_epoch_size(bprmf_handle* h, int64_t* n_triplets, int64_t* n_steps);
+
+/* ---- weights (checkpoint / parity) -------------------------------------------------------- */
+/* embed_user.weight / embed_item.weight (BPRMFRecommender.py:36-37); [rows, factor_num] fp32.
+ * Sharded handles: P holds local users (global id = local*world + rank), Q local items likewise. */
+int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q);
+int bprmf_get_weights(bprmf_handle* h, float* P, float* Q);
+int bprmf_local_rows(bprmf_handle* h, int64_t* users, int64_t* items);
+int bprmf_step_count(bprmf_handle* h, int64_t* steps);
+
+/* ---- training ----------------------------------------------------------------------------- */
+/* One epoch: ng_sample() on device + the shuffled DataLoader + steps
+ * (BPRMFRecommender.py:157-178, util/data_loader.py:680-690). */
+int bprmf_train_epoch(bprmf_handle* h, uint32_t epoch, bprmf_stats* stats);
+/* Steps [first_step, first_step+n_steps) of an epoch (bench / resumable training). */
+int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                      bprmf_stats* stats);
+/* Replay reference-format triplets in order, batch_size per step (last batch partial):
+ * the `for user, item_i, item_j in train_loader` body, BPRMFRecommender.py:162-176. */
+int bprmf_train_triplets(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                         int64_t n, bprmf_stats* stats);
+int bprmf_train_triplets_dev(bprmf_handle* h, const int32_t* u, const int32_t* i,
+                             const int32_t* j, int64_t n, bprmf_stats* stats);
+
+/* ---- sampler (exposed for bit-exact tests) ------------------------------------------------ */
+/* Triplet slots [first, first+n) of `epoch` in shuffled order -> (u, i, j), global ids. */
+int bprmf_sample(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t* u,
+                 int32_t* i, int32_t* j);
+
+/* ---- scoring ------------------------------------------------------------------------------ */
+/* pred = <P_u, Q_i> (BPR.forward, BPRMFRecommender.py:42-50; predict() convention
+ * util/matrix_factorization.pyx:157-167).  Single-GPU handles only. */
+int bprmf_score(bprmf_handle* h, const int32_t* u, const int32_t* i, int64_t n, float* out);
+/* forward(user, item_i, item_j) on device int64 ids -> pred_i, pred_j (device fp32). */
+int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const int64_t* j,
+                      int64_t n, float* pred_i, float* pred_j);
+
+/* ---- measurement -------------------------------------------------------------------------- */
+/* Enable (1) / disable (0) and reset per-kernel event timing; read the sums since enabling. */
+int bprmf_profile(bprmf_handle* h, int32_t enable);
+int bprmf_profile_read(bprmf_handle* h, bprmf_kprof* out);
+
+/* ---- sharded step phases (one process per GPU; exchanges done by the caller over RCCL) ---- */
+/* A step on a world>1 handle:  begin -> [caller: all-to-all requested item ids]
+ *   -> gather_items (owner side) -> [caller: all-to-all rows back]
+ *   -> fwd_scatter (local triplets vs received rows) -> apply_users
+ *   -> [caller: all-to-all item grads to owners] -> apply_items -> end.
+ * Ids passed here are LOCAL row indices of this handle (global id / world) unless noted. */
+int bprmf_dist_begin_step(bprmf_handle* h);
+int bprmf_dist_gather_items(bprmf_handle* h, const int32_t* rows, int64_t n, float* out);
+int bprmf_dist_fwd_scatter(bprmf_handle* h, const int32_t* u_local, const int32_t* slot_i,
+                           const int32_t* slot_j, int64_t n, const float* item_rows,
+                           float* item_grads, int64_t n_slots);
+int bprmf_dist_apply_users(bprmf_handle* h, const int32_t* u_local, int64_t n);
+int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n);
+int bprmf_dist_end_step(bprmf_handle* h, double* loss);
+/* Device triplets of a step of an epoch for this shard: writes global (u, i, j) of the slots
+ * [first, first+n) of the shard's epoch order into device buffers. */
+int bprmf_dist_sample_dev(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t* u,
+                          int32_t* i, int32_t* j);
+/* row stride (floats) of device row buffers used by the dist_* exchange functions */
+int bprmf_row_stride(bprmf_handle* h, int32_t* ld);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPRMF_H */

@@ -1,0 +1,235 @@
+"""ORACLE — CPU restatement of the reference BPR-MF training path, for TESTS ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker.  The product path (recommend-lib_amd) never calls it.
+
+Two parts:
+
+1. The reference training step, restated densely and literally (numpy float32):
+   BPRMFRecommender.py:42-50  forward   pred_i = <P_u,Q_i>, pred_j = <P_u,Q_j>
+   BPRMFRecommender.py:174    loss      L = -sum(log(sigmoid(pred_i - pred_j)))   (a SUM)
+   BPRMFRecommender.py:175    backward  dense embedding grads, duplicates summed
+   BPRMFRecommender.py:154,176 SGD      W <- W - lr*(G + wd*W) over EVERY row (weight decay is dense)
+   Pinned against tests/golden/bpr_step_tiny.npz (F1) and bpr_ml100k_replay.npz (F2), which were
+   produced by the reference itself (tests/golden/make_golden.py).
+
+2. The on-device sampler's specification (util/data_loader.py:680-700 semantics, our RNG):
+   the reference draws `num_ng` negatives per positive with MT19937 + rejection against the train
+   set (data_loader.py:684-689) and the DataLoader shuffles the triplets
+   (BPRMFRecommender.py:141-142).  A data-dependent MT19937 stream cannot be parallelised, so the
+   product uses a counter-based equivalent with the SAME distribution:
+     * triplet q = p*num_ng + r  <->  positive p = features[p], r-th negative   (data_loader.py:684-690)
+     * negative j = k-th item NOT in the user's train set, k ~ U[0, I - deg(u)) (exactly uniform over
+       non-positives, like rejection sampling, but one draw and one binary search)
+     * the epoch's triplet order is a keyed Feistel permutation of [0, N) (cycle-walking), standing in
+       for the DataLoader's torch.randperm shuffle
+     * randomness: Philox4x32-10 (Salmon et al., SC'11), key = 64-bit seed, counter = (q, epoch, tag)
+   This module restates that spec independently of the HIP code; GPU output must match it bit-for-bit.
+   Distributional parity with the reference sampler is pinned by tests/golden/ng_sample_ml100k.npz (F3).
+"""
+import numpy as np
+
+# ----------------------------------------------------------------------------------------------
+# 1. dense reference step
+# ----------------------------------------------------------------------------------------------
+
+
+def bpr_step_dense(P, Q, u, i, j, lr, wd):
+    """In-place reference step on float32 tables P [U,d], Q [I,d]; returns the loss (float64).
+
+    Follows BPRMFRecommender.py:172-176 with torch's single-tensor SGD (torch/optim/sgd.py):
+    d_p = grad + wd*p ; p = p - lr*d_p, applied to every row because nn.Embedding grads are dense.
+    """
+    f32 = np.float32
+    lr = f32(lr)
+    wd = f32(wd)
+    u = np.asarray(u, dtype=np.int64)
+    i = np.asarray(i, dtype=np.int64)
+    j = np.asarray(j, dtype=np.int64)
+    pu, qi, qj = P[u], Q[i], Q[j]
+    x = (pu * qi).sum(-1, dtype=f32) - (pu * qj).sum(-1, dtype=f32)
+    s = (f32(1) / (f32(1) + np.exp(-x, dtype=f32))).astype(f32)
+    with np.errstate(divide="ignore"):
+        loss = float(-np.log(s.astype(np.float64)).sum())
+    c = (f32(1) - s).astype(f32)  # -dL/dx
+    gP = np.zeros_like(P)
+    gQ = np.zeros_like(Q)
+    np.add.at(gP, u, (-c)[:, None] * qi + c[:, None] * qj)
+    np.add.at(gQ, i, (-c)[:, None] * pu)
+    np.add.at(gQ, j, c[:, None] * pu)
+    for W, G in ((P, gP), (Q, gQ)):
+        dp = G + wd * W
+        W -= lr * dp
+    return loss
+
+
+def train_replay(P, Q, triplets, bounds, lr, wd):
+    """Replay a sequence of reference batches (triplets [3,N], batch boundaries)."""
+    losses = []
+    for b in range(len(bounds) - 1):
+        s, e = bounds[b], bounds[b + 1]
+        losses.append(bpr_step_dense(P, Q, triplets[0, s:e], triplets[1, s:e], triplets[2, s:e], lr, wd))
+    return np.array(losses)
+
+
+# ----------------------------------------------------------------------------------------------
+# 2. sampler specification (bit-exact target for the HIP sampler)
+# ----------------------------------------------------------------------------------------------
+_M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_W0, _W1 = 0x9E3779B9, 0xBB67AE85
+_MASK32 = np.uint64(0xFFFFFFFF)
+TAG_NEG = 0x4E470000   # counter word 3 for negative draws ('NG'), low 16 bits = attempt
+TAG_PERM = 0x50520000  # counter word 3 for Feistel round keys ('PR'), low 16 bits = round
+FEISTEL_ROUNDS = 6
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Vectorised Philox4x32-10.  Counter words are uint32 arrays (or scalars); key two uint32."""
+    c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) & _MASK32 for c in (c0, c1, c2, c3))
+    k0 = int(k0) & 0xFFFFFFFF
+    k1 = int(k1) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = _M0 * c0
+        p1 = _M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _MASK32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ np.uint64(k0)), lo1, (hi0 ^ c3 ^ np.uint64(k1)), lo0
+        k0 = (k0 + _W0) & 0xFFFFFFFF
+        k1 = (k1 + _W1) & 0xFFFFFFFF
+    return c0, c1, c2, c3
+
+
+def _seed_key(seed):
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return seed & 0xFFFFFFFF, seed >> 32
+
+
+def feistel_bits(n):
+    """Half-width h of the balanced Feistel domain [0, 4^h) >= n (h >= 1)."""
+    h = 1
+    while (1 << (2 * h)) < n:
+        h += 1
+    return h
+
+
+def permute(q, n, seed, epoch):
+    """Keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle-walking."""
+    k0, k1 = _seed_key(seed)
+    h = feistel_bits(n)
+    mask = np.uint64((1 << h) - 1)
+    x = np.asarray(q, dtype=np.uint64).copy()
+    todo = np.ones(x.shape, dtype=bool)
+    while todo.any():
+        y = x[todo]
+        L = y >> np.uint64(h)
+        R = y & mask
+        for r in range(FEISTEL_ROUNDS):
+            f = philox4x32_10(R, np.uint64(r), np.uint64(epoch), np.uint64(TAG_PERM | r), k0, k1)[0]
+            L, R = R, (L ^ (f & mask))
+        y = (L << np.uint64(h)) | R
+        x[todo] = y
+        todo[todo] = y >= np.uint64(n)
+    return x.astype(np.int64)
+
+
+def _bounded(q, epoch, n, k0, k1):
+    """Unbiased Lemire reduction of Philox output into [0,n) for each triplet q (n>0 per element)."""
+    q = np.asarray(q, dtype=np.uint64)
+    n = np.asarray(n, dtype=np.uint64)
+    out = np.zeros(q.shape, dtype=np.uint64)
+    att = np.zeros(q.shape, dtype=np.uint64)
+    todo = np.ones(q.shape, dtype=bool)
+    thresh = ((np.uint64(1 << 32) - n) % n)  # (2^32 - n) mod n
+    while todo.any():
+        qq = q[todo]
+        r = philox4x32_10(qq & _MASK32, qq >> np.uint64(32), np.uint64(epoch),
+                          np.uint64(TAG_NEG) | att[todo], k0, k1)[0]
+        m = r * n[todo]
+        lo = m & _MASK32
+        ok = lo >= thresh[todo]
+        idx = np.flatnonzero(todo)
+        out[idx[ok]] = m[ok] >> np.uint64(32)
+        att[idx[~ok]] += np.uint64(1)
+        todo[idx[ok]] = False
+    return out.astype(np.int64)
+
+
+def build_csr(users, items, user_num):
+    """Per-user sorted, de-duplicated positive lists (the dok_matrix of data_loader.py:538-545)."""
+    users = np.asarray(users, dtype=np.int64)
+    items = np.asarray(items, dtype=np.int64)
+    key = np.unique(users * (1 << 32) + items)
+    uu = key >> 32
+    ii = key & 0xFFFFFFFF
+    indptr = np.zeros(user_num + 1, dtype=np.int64)
+    np.add.at(indptr, uu + 1, 1)
+    return np.cumsum(indptr), ii.astype(np.int32)
+
+
+def kth_nonmember(indptr, indices, u, k):
+    """j = the k-th (0-based) item id not in the sorted list of user u.  Vectorised binary search
+    for m = #{idx : a[idx] - idx <= k}; then j = k + m."""
+    u = np.asarray(u, dtype=np.int64)
+    k = np.asarray(k, dtype=np.int64)
+    lo = np.zeros(u.shape, dtype=np.int64)
+    hi = indptr[u + 1] - indptr[u]
+    base = indptr[u]
+    while True:
+        act = lo < hi
+        if not act.any():
+            break
+        mid = (lo + hi) >> 1
+        a = np.where(act, indices[np.where(act, base + mid, 0)].astype(np.int64) - mid, 0)
+        go_right = act & (a <= k)
+        lo = np.where(go_right, mid + 1, lo)
+        hi = np.where(act & ~go_right, mid, hi)
+    return k + lo
+
+
+def sample_triplets(pos_u, pos_i, indptr, indices, item_num, num_ng, seed, epoch, first, count):
+    """Triplet slots [first, first+count) of an epoch -> (u, i, j) int32 arrays.
+
+    slot s -> q = permute(s) -> positive p = q // num_ng -> (u,i) = pos[p]; j via kth_nonmember.
+    """
+    n = len(pos_u) * num_ng
+    s = np.arange(first, first + count, dtype=np.int64)
+    q = permute(s, n, seed, epoch)
+    p = q // num_ng
+    u = np.asarray(pos_u, dtype=np.int64)[p]
+    i = np.asarray(pos_i, dtype=np.int64)[p]
+    deg = indptr[u + 1] - indptr[u]
+    free = item_num - deg
+    if (free <= 0).any():
+        raise ValueError("user with no negative item (reference ng_sample would loop forever)")
+    k0, k1 = _seed_key(seed)
+    k = _bounded(q, epoch, free, k0, k1)
+    j = kth_nonmember(indptr, indices, u, k)
+    return u.astype(np.int32), i.astype(np.int32), j.astype(np.int32)
+
+
+# ----------------------------------------------------------------------------------------------
+# 3. metrics (restated from util/metrics.py:99-195 for host-only KAT cross-checks)
+# ----------------------------------------------------------------------------------------------
+def hr_ndcg_from_scores(test_users, test_items, scores, gt, k=10):
+    """Final KPI of BPRMFRecommender.py:196-229: per user rank candidates by score, take top-k,
+    HR = sum hits / sum |gt| (metrics.py:159-167), NDCG = mean DCG/IDCG (metrics.py:169-195)."""
+    order = np.lexsort((-scores, test_users))
+    tu = test_users[order]
+    ti = test_items[order]
+    starts = np.flatnonzero(np.r_[True, tu[1:] != tu[:-1]])
+    ends = np.r_[starts[1:], len(tu)]
+    hits = denom = 0
+    ndcgs = []
+    for s, e in zip(starts, ends):
+        u = int(tu[s])
+        top = ti[s:min(e, s + k)]
+        g = gt[u]
+        r = np.array([1.0 if int(x) in g else 0.0 for x in top])
+        hits += r.sum()
+        denom += len(g)
+        disc = 1.0 / np.log2(np.arange(2, len(r) + 2))
+        dcg = ((2 ** r - 1) * disc).sum()
+        rs = np.sort(r)[::-1]
+        idcg = ((2 ** rs - 1) * disc).sum()
+        ndcgs.append(dcg / idcg if idcg else 0.0)
+    return hits / denom, float(np.mean(ndcgs))

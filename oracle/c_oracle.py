@@ -1,0 +1,80 @@
+"""ORACLE (test infrastructure only) — ctypes binding of oracle/bpr_cpu.c (liboracle_bpr.so).
+
+Used by tests/ as a checker and by bench.py's cpu_baseline leg as the timed CPU port.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle_bpr.so")
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+
+
+def build():
+    src = os.path.join(HERE, "bpr_cpu.c")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        L.oracle_sample.argtypes = [_i32p, _i32p, ctypes.c_int64, _i64p, _i32p, ctypes.c_int64,
+                                    ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64,
+                                    ctypes.c_int64, _i32p, _i32p, _i32p]
+        L.oracle_sample.restype = ctypes.c_int
+        L.oracle_step_dense.argtypes = [_f32p, _f32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                        _i32p, _i32p, _i32p, ctypes.c_int64, ctypes.c_float,
+                                        ctypes.c_float, _f32p, _f32p]
+        L.oracle_step_dense.restype = ctypes.c_double
+        L.oracle_permute.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.oracle_permute.restype = ctypes.c_uint64
+        L.oracle_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def sample(pos_u, pos_i, indptr, indices, item_num, num_ng, seed, epoch, first, count):
+    L = lib()
+    pos_u = np.ascontiguousarray(pos_u, dtype=np.int32)
+    pos_i = np.ascontiguousarray(pos_i, dtype=np.int32)
+    out = [np.empty(count, dtype=np.int32) for _ in range(3)]
+    rc = L.oracle_sample(pos_u, pos_i, len(pos_u), np.ascontiguousarray(indptr, dtype=np.int64),
+                         np.ascontiguousarray(indices, dtype=np.int32), int(item_num), int(num_ng),
+                         int(seed) & (2**64 - 1), int(epoch), int(first), int(count), *out)
+    if rc != 0:
+        raise ValueError("user with no negative item")
+    return tuple(out)
+
+
+class DenseTrainer:
+    """The reference step on CPU (dense grads + dense weight decay), tables in float32."""
+
+    def __init__(self, P, Q, lr, wd):
+        self.P = np.ascontiguousarray(P, dtype=np.float32)
+        self.Q = np.ascontiguousarray(Q, dtype=np.float32)
+        self.gP = np.empty_like(self.P)
+        self.gQ = np.empty_like(self.Q)
+        self.lr, self.wd = float(lr), float(wd)
+
+    def step(self, u, i, j):
+        u = np.ascontiguousarray(u, dtype=np.int32)
+        i = np.ascontiguousarray(i, dtype=np.int32)
+        j = np.ascontiguousarray(j, dtype=np.int32)
+        U, d = self.P.shape
+        return lib().oracle_step_dense(self.P, self.Q, U, self.Q.shape[0], d, u, i, j, len(u),
+                                       self.lr, self.wd, self.gP, self.gQ)
+
+
+def threads():
+    return int(lib().oracle_threads())

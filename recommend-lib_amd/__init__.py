@@ -1,0 +1,19 @@
+"""recommend-lib_amd — MI355X-native BPR-MF training path (drop-in for the reference's
+BPRMFRecommender / util.data_loader.BPRData / util.metrics BPR parts).
+
+The directory name is not a Python identifier; import it with
+    importlib.import_module("recommend-lib_amd")
+(tests/conftest.py and __graft_entry__.py do exactly that).
+
+Compute lives in libbprmf_amd.so (hand-written HIP for gfx950, C ABI in include/bprmf.h).
+"""
+from . import _lib
+from ._lib import BprmfError
+from .build import build, LIB as LIB_PATH
+from .data import BPRData
+from .model import BPRMF
+from . import metrics
+
+BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
+
+__all__ = ["BPRMF", "BPR", "BPRData", "BprmfError", "metrics", "build", "LIB_PATH"]

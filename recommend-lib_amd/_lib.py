@@ -1,0 +1,117 @@
+"""ctypes binding of libbprmf_amd.so (include/bprmf.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is visible, handle creation
+raises — there is no CPU fallback in the product.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbprmf_amd.so")
+
+E_INVALID, E_RANGE, E_HIP, E_STATE, E_NO_NEGATIVE, E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
+
+
+class BprmfError(RuntimeError):
+    """A HIP / state failure inside libbprmf_amd."""
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("user_num", ctypes.c_int64), ("item_num", ctypes.c_int64),
+                ("factor_num", ctypes.c_int32), ("lr", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("batch_size", ctypes.c_int32),
+                ("num_ng", ctypes.c_int32), ("init_std", ctypes.c_float),
+                ("seed", ctypes.c_uint64), ("device", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("world", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("triplets", ctypes.c_int64), ("steps", ctypes.c_int64),
+                ("loss", ctypes.c_double), ("seconds", ctypes.c_double)]
+
+    def as_dict(self):
+        return dict(triplets=self.triplets, steps=self.steps, loss=self.loss, seconds=self.seconds)
+
+
+class KProf(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64 * 4), ("ms", ctypes.c_double * 4)]
+
+    KINDS = ("sample", "fwd_scatter", "apply")
+
+    def as_dict(self):
+        return {k: dict(count=int(self.count[n]), ms=float(self.ms[n])) for n, k in enumerate(self.KINDS)}
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+# name -> argtypes (restype int unless noted); mirrors include/bprmf.h
+SIGNATURES = {
+    "bprmf_create": [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)],
+    "bprmf_destroy": [_P],
+    "bprmf_last_error": [],
+    "bprmf_version": [],
+    "bprmf_set_stream": [_P, _P],
+    "bprmf_synchronize": [_P],
+    "bprmf_set_train": [_P, _P, _P, _I64],
+    "bprmf_set_train_ex": [_P, _P, _P, _I64, _P, _P, _I64],
+    "bprmf_epoch_size": [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+    "bprmf_set_weights": [_P, _P, _P],
+    "bprmf_get_weights": [_P, _P, _P],
+    "bprmf_local_rows": [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+    "bprmf_step_count": [_P, ctypes.POINTER(_I64)],
+    "bprmf_train_epoch": [_P, ctypes.c_uint32, ctypes.POINTER(Stats)],
+    "bprmf_train_steps": [_P, ctypes.c_uint32, _I64, _I64, ctypes.POINTER(Stats)],
+    "bprmf_train_triplets": [_P, _P, _P, _P, _I64, ctypes.POINTER(Stats)],
+    "bprmf_train_triplets_dev": [_P, _P, _P, _P, _I64, ctypes.POINTER(Stats)],
+    "bprmf_sample": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
+    "bprmf_score": [_P, _P, _P, _I64, _P],
+    "bprmf_forward_dev": [_P, _P, _P, _P, _I64, _P, _P],
+    "bprmf_dist_begin_step": [_P],
+    "bprmf_dist_gather_items": [_P, _P, _I64, _P],
+    "bprmf_dist_fwd_scatter": [_P, _P, _P, _P, _I64, _P, _P, _I64],
+    "bprmf_dist_apply_users": [_P, _P, _I64],
+    "bprmf_dist_apply_items": [_P, _P, _P, _I64],
+    "bprmf_dist_end_step": [_P, ctypes.POINTER(ctypes.c_double)],
+    "bprmf_dist_sample_dev": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
+    "bprmf_row_stride": [_P, ctypes.POINTER(ctypes.c_int32)],
+    "bprmf_profile": [_P, ctypes.c_int32],
+    "bprmf_profile_read": [_P, ctypes.POINTER(KProf)],
+}
+
+_lib = None
+
+
+def load():
+    """Load (never build) the in-tree library; raise ImportError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = ctypes.c_char_p if name == "bprmf_last_error" else ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc == 0:
+        return
+    msg = (load().bprmf_last_error() or b"").decode(errors="replace")
+    if rc in (E_INVALID, E_RANGE):
+        raise ValueError(msg)
+    if rc == E_NO_NEGATIVE:
+        raise ValueError(msg)
+    raise BprmfError(f"libbprmf_amd error {rc}: {msg}")
+
+
+def ptr(a):
+    """Raw address of a numpy array or torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data

@@ -1,0 +1,49 @@
+"""Build libbprmf_amd.so in-tree for gfx950 with hipcc (no torch JIT cache, no pip install).
+
+The shared library is the product: kernels.hip (device code) + capi.cpp (the C ABI of
+include/bprmf.h).  It is placed next to this file so it travels to the GPU box with the repo.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libbprmf_amd.so")
+SOURCES = [os.path.join(HERE, "csrc", "kernels.hip"), os.path.join(HERE, "csrc", "capi.cpp")]
+HEADERS = [os.path.join(HERE, "csrc", "kernels.h"), os.path.join(ROOT, "include", "bprmf.h")]
+ARCH = os.environ.get("BPRMF_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def is_stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False):
+    if not force and not is_stale():
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+           "-o", tmp] + SOURCES
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,674 @@
+// capi.cpp — C ABI (include/bprmf.h) over the gfx950 kernels of kernels.hip.
+//
+// One handle = one GPU = one shard (rank of world).  The handle owns, in HBM:
+//   P  [local users, ld] fp32 + grad accumulator + int32 stamp      (embed_user.weight)
+//   Q  [local items, ld] fp32 + grad accumulator + int32 stamp      (embed_item.weight)
+//   positives of its users (features order) and their sorted CSR     (BPRData.features / train_mat)
+//   a triplet chunk buffer [chunk, 3] int32 filled by the sampler    (BPRData.features_fill)
+// A training step is two launches: fwd_scatter (gather, dots, sigmoid, f32-atomic grad scatter)
+// then apply_refs (claim each referenced row once via its stamp, lazy decay + SGD update).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/bprmf.h"
+#include "kernels.h"
+
+using namespace bprmf;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+struct bprmf_handle {
+  bprmf_config cfg;
+  Geom geom;
+  Hyper hp;
+  int64_t U = 0, I = 0;  // local rows
+  Table P{}, Q{};
+  // training data
+  int64_t npos = 0;
+  int32_t* d_pos_u = nullptr;
+  int32_t* d_pos_i = nullptr;
+  int64_t* d_indptr = nullptr;
+  int32_t* d_indices = nullptr;
+  int feistel_h = 1;
+  uint32_t k0 = 0, k1 = 0;  // shard sampler key
+  // triplet chunk
+  int32_t* d_trip = nullptr;  // [3, cap]
+  int64_t trip_cap = 0;
+  // misc device scalars
+  double* d_loss = nullptr;
+  int32_t* d_err = nullptr;
+  int32_t t = 0;  // optimizer steps taken
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // live per-kernel timing (bprmf_profile): event pairs around each launch of each kind
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  size_t prof_used = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_rec[BPRMF_KPROF_KINDS];
+};
+
+static hipEvent_t prof_event(bprmf_handle* h) {
+  if (h->prof_used == h->prof_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->prof_pool.push_back(e);
+  }
+  return h->prof_pool[h->prof_used++];
+}
+
+// record an event before (begin) / after a launch of `kind` when profiling is on
+struct ProfScope {
+  bprmf_handle* h;
+  int kind;
+  hipEvent_t a = nullptr;
+  ProfScope(bprmf_handle* hh, int k) : h(hh), kind(k) {
+    if (h->prof_on && (a = prof_event(h))) hipEventRecord(a, h->stream);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = prof_event(h);
+    if (!b) return;
+    hipEventRecord(b, h->stream);
+    h->prof_rec[kind].push_back({a, b});
+  }
+};
+
+static int set_dev(bprmf_handle* h) {
+  HIPCHK(hipSetDevice(h->cfg.device));
+  return 0;
+}
+
+template <typename T>
+static int dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) return 0;
+  HIPCHK(hipMalloc((void**)p, sizeof(T) * (size_t)count));
+  return 0;
+}
+
+static int64_t chunk_triplets(const bprmf_handle* h) {
+  // sample up to ~4M triplets (48 MB of ids) per sampler launch, whole steps only
+  const int64_t B = h->cfg.batch_size;
+  int64_t steps = std::max<int64_t>(1, (int64_t(1) << 22) / B);
+  return steps * B;
+}
+
+static int ensure_trip(bprmf_handle* h, int64_t n) {
+  if (n <= h->trip_cap) return 0;
+  if (h->d_trip) HIPCHK(hipFree(h->d_trip));
+  h->d_trip = nullptr;
+  h->trip_cap = 0;
+  if (int r = dalloc(&h->d_trip, 3 * n)) return r;
+  h->trip_cap = n;
+  return 0;
+}
+
+static int check_err_flag(bprmf_handle* h) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, h->d_err, sizeof e, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (e) {
+    HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
+    if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
+    return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
+  }
+  return 0;
+}
+
+extern "C" {
+
+const char* bprmf_last_error(void) { return g_err.c_str(); }
+int bprmf_version(void) { return 1; }
+
+int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
+  if (!cfg || !out) return fail(BPRMF_E_INVALID, "null argument");
+  *out = nullptr;
+  if (cfg->user_num <= 0 || cfg->item_num <= 0)
+    return fail(BPRMF_E_INVALID, "user_num and item_num must be positive");
+  if (cfg->user_num > INT32_MAX || cfg->item_num > INT32_MAX)
+    return fail(BPRMF_E_INVALID, "ids are int32: user_num/item_num must be < 2^31");
+  if (cfg->batch_size <= 0 || cfg->num_ng <= 0)
+    return fail(BPRMF_E_INVALID, "batch_size and num_ng must be positive");
+  if (cfg->world <= 0 || cfg->rank < 0 || cfg->rank >= cfg->world)
+    return fail(BPRMF_E_INVALID, "need 0 <= rank < world");
+  if (!(cfg->lr >= 0.f) || !(cfg->weight_decay >= 0.f) || !(cfg->init_std >= 0.f))
+    return fail(BPRMF_E_INVALID, "lr, weight_decay and init_std must be >= 0");
+  Geom g;
+  if (!make_geom(cfg->factor_num, &g)) return fail(BPRMF_E_UNSUPPORTED, "factor_num must be in [1, 1024]");
+  auto* h = new bprmf_handle();
+  h->cfg = *cfg;
+  h->geom = g;
+  h->hp.lr = cfg->lr;
+  h->hp.wd = cfg->weight_decay;
+  h->hp.alpha = 1.0 - (double)cfg->lr * (double)cfg->weight_decay;
+  const int64_t W = cfg->world, R = cfg->rank;
+  h->U = (cfg->user_num - R + W - 1) / W;
+  h->I = (cfg->item_num - R + W - 1) / W;
+  const uint64_t shard_seed = cfg->seed + (uint64_t)cfg->rank * 0x9E3779B97F4A7C15ull;
+  h->k0 = (uint32_t)shard_seed;
+  h->k1 = (uint32_t)(shard_seed >> 32);
+  int rc = 0;
+#define TRY(x)            \
+  do {                    \
+    if ((rc = (x))) {     \
+      bprmf_destroy(h);   \
+      return rc;          \
+    }                     \
+  } while (0)
+  TRY(set_dev(h));
+  hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    bprmf_destroy(h);
+    return fail(BPRMF_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  h->stream = h->own_stream;
+  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+    bprmf_destroy(h);
+    return fail(BPRMF_E_HIP, "hipEventCreate failed");
+  }
+  const int64_t ld = g.ld;
+  TRY(dalloc(&h->P.W, h->U * ld));
+  TRY(dalloc(&h->P.G, h->U * ld));
+  TRY(dalloc(&h->P.stamp, h->U));
+  TRY(dalloc(&h->Q.W, h->I * ld));
+  TRY(dalloc(&h->Q.G, h->I * ld));
+  TRY(dalloc(&h->Q.stamp, h->I));
+  TRY(dalloc(&h->d_loss, 1));
+  TRY(dalloc(&h->d_err, 1));
+  h->P.rows = h->U;
+  h->Q.rows = h->I;
+  auto memz = [&](void* p, size_t bytes) -> int {
+    if (!p || !bytes) return 0;
+    HIPCHK(hipMemsetAsync(p, 0, bytes, h->stream));
+    return 0;
+  };
+  TRY(memz(h->P.G, sizeof(float) * h->U * ld));
+  TRY(memz(h->Q.G, sizeof(float) * h->I * ld));
+  TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
+  TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
+  TRY(memz(h->d_err, sizeof(int32_t)));
+  // init keyed by the global seed and GLOBAL row id: identical tables for any world size
+  const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
+  e = init_normal(g, h->P.W, h->U, cfg->init_std, s0, s1, 0u, (int)W, (int)R, h->stream);
+  if (e == hipSuccess) e = init_normal(g, h->Q.W, h->I, cfg->init_std, s0, s1, 1u, (int)W, (int)R, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {
+    bprmf_destroy(h);
+    return fail(BPRMF_E_HIP, "init: %s", hipGetErrorString(e));
+  }
+#undef TRY
+  *out = h;
+  return 0;
+}
+
+int bprmf_destroy(bprmf_handle* h) {
+  if (!h) return 0;
+  hipSetDevice(h->cfg.device);
+  if (h->own_stream) hipStreamSynchronize(h->own_stream);
+  void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
+                  h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
+  if (h->ev0) hipEventDestroy(h->ev0);
+  if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->own_stream) hipStreamDestroy(h->own_stream);
+  delete h;
+  return 0;
+}
+
+int bprmf_set_stream(bprmf_handle* h, void* s) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  h->stream = s ? (hipStream_t)s : h->own_stream;
+  return 0;
+}
+
+int bprmf_synchronize(bprmf_handle* h) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int bprmf_local_rows(bprmf_handle* h, int64_t* users, int64_t* items) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (users) *users = h->U;
+  if (items) *items = h->I;
+  return 0;
+}
+
+int bprmf_step_count(bprmf_handle* h, int64_t* steps) {
+  if (!h || !steps) return fail(BPRMF_E_INVALID, "null argument");
+  *steps = h->t;
+  return 0;
+}
+
+int bprmf_row_stride(bprmf_handle* h, int32_t* ld) {
+  if (!h || !ld) return fail(BPRMF_E_INVALID, "null argument");
+  *ld = h->geom.ld;
+  return 0;
+}
+
+int bprmf_set_train(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz) {
+  return bprmf_set_train_ex(h, users, items, nnz, nullptr, nullptr, 0);
+}
+
+int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz,
+                       const int32_t* ex_users, const int32_t* ex_items, int64_t n_ex) {
+  if (!h || (nnz > 0 && (!users || !items)) || nnz < 0) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (n_ex < 0 || (n_ex > 0 && (!ex_users || !ex_items))) return fail(BPRMF_E_INVALID, "bad exclusions");
+  if (int r = set_dev(h)) return r;
+  const int64_t W = h->cfg.world, R = h->cfg.rank;
+  std::vector<int32_t> pu, pi;
+  pu.reserve(nnz / W + 16);
+  pi.reserve(nnz / W + 16);
+  for (int64_t k = 0; k < nnz; ++k) {
+    const int32_t u = users[k], i = items[k];
+    if (u < 0 || u >= h->cfg.user_num || i < 0 || i >= h->cfg.item_num)
+      return fail(BPRMF_E_RANGE, "positive %lld = (%d, %d) out of range", (long long)k, u, i);
+    if (u % W == R) {
+      pu.push_back(u);
+      pi.push_back(i);
+    }
+  }
+  const int64_t n = (int64_t)pu.size();
+  // sorted, de-duplicated positive lists per local user (the dok train_mat): features + exclusions
+  std::vector<uint64_t> keys(n);
+  for (int64_t k = 0; k < n; ++k) keys[k] = ((uint64_t)(pu[k] / W) << 32) | (uint32_t)pi[k];
+  for (int64_t k = 0; k < n_ex; ++k) {
+    const int32_t u = ex_users[k], i = ex_items[k];
+    if (u < 0 || u >= h->cfg.user_num || i < 0 || i >= h->cfg.item_num)
+      return fail(BPRMF_E_RANGE, "train_mat entry (%d, %d) out of range", u, i);
+    if (u % W == R) keys.push_back(((uint64_t)(u / W) << 32) | (uint32_t)i);
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  std::vector<int64_t> indptr(h->U + 1, 0);
+  std::vector<int32_t> indices(keys.size());
+  for (size_t k = 0; k < keys.size(); ++k) {
+    indptr[(keys[k] >> 32) + 1]++;
+    indices[k] = (int32_t)(keys[k] & 0xFFFFFFFFu);
+  }
+  for (int64_t u = 0; u < h->U; ++u) indptr[u + 1] += indptr[u];
+  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices};
+  for (void* p : olds)
+    if (p) HIPCHK(hipFree(p));
+  h->d_pos_u = h->d_pos_i = h->d_indices = nullptr;
+  h->d_indptr = nullptr;
+  if (int r = dalloc(&h->d_pos_u, n)) return r;
+  if (int r = dalloc(&h->d_pos_i, n)) return r;
+  if (int r = dalloc(&h->d_indptr, h->U + 1)) return r;
+  if (int r = dalloc(&h->d_indices, (int64_t)indices.size())) return r;
+  if (n) {
+    HIPCHK(hipMemcpy(h->d_pos_u, pu.data(), 4 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_pos_i, pi.data(), 4 * n, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemcpy(h->d_indptr, indptr.data(), 8 * (h->U + 1), hipMemcpyHostToDevice));
+  if (!indices.empty())
+    HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
+  h->npos = n;
+  const uint64_t N = (uint64_t)n * (uint64_t)h->cfg.num_ng;
+  int hb = 1;
+  while (hb < 32 && (1ull << (2 * hb)) < N) ++hb;
+  h->feistel_h = hb;
+  return 0;
+}
+
+int bprmf_epoch_size(bprmf_handle* h, int64_t* n_triplets, int64_t* n_steps) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  const int64_t N = h->npos * h->cfg.num_ng;
+  if (n_triplets) *n_triplets = N;
+  if (n_steps) *n_steps = (N + h->cfg.batch_size - 1) / h->cfg.batch_size;
+  return 0;
+}
+
+static SamplerArgs sampler_args(bprmf_handle* h) {
+  SamplerArgs a;
+  a.pos_u = h->d_pos_u;
+  a.pos_i = h->d_pos_i;
+  a.indptr = h->d_indptr;
+  a.indices = h->d_indices;
+  a.npos = h->npos;
+  a.item_num = h->cfg.item_num;
+  a.num_ng = h->cfg.num_ng;
+  a.world = h->cfg.world;
+  a.feistel_h = h->feistel_h;
+  a.k0 = h->k0;
+  a.k1 = h->k1;
+  return a;
+}
+
+static int begin_call(bprmf_handle* h) {
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double), h->stream));
+  HIPCHK(hipEventRecord(h->ev0, h->stream));
+  return 0;
+}
+
+static int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
+  HIPCHK(hipEventRecord(h->ev1, h->stream));
+  double loss = 0;
+  HIPCHK(hipMemcpyAsync(&loss, h->d_loss, sizeof loss, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipEventSynchronize(h->ev1));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  if (int r = check_err_flag(h)) return r;
+  if (st) {
+    st->triplets = triplets;
+    st->steps = steps;
+    st->loss = loss;
+    st->seconds = ms * 1e-3;
+  }
+  return 0;
+}
+
+// run steps over device triplets tu/ti/tj[0..n) in batches of B
+static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                     int64_t n, int64_t* steps_done) {
+  const int64_t B = h->cfg.batch_size;
+  for (int64_t off = 0; off < n; off += B) {
+    const int64_t nb = std::min(B, n - off);
+    if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+    const int32_t t = h->t + 1;
+    {
+      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
+      HIPCHK(fwd_scatter(h->geom, tu + off, ti + off, tj + off, nb, h->P, h->Q, h->hp, t, h->d_loss,
+                         h->d_err, h->stream));
+    }
+    {
+      ProfScope ps(h, BPRMF_KPROF_APPLY);
+      HIPCHK(apply_refs(h->geom, tu + off, ti + off, tj + off, nb, h->P, h->Q, h->hp, t, h->stream));
+    }
+    h->t = t;
+    ++*steps_done;
+  }
+  return 0;
+}
+
+int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                      bprmf_stats* st) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (h->cfg.world != 1)
+    return fail(BPRMF_E_STATE, "sharded handle: drive steps with the bprmf_dist_* phases");
+  if (!h->d_pos_u || h->npos == 0) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
+  int64_t N, S;
+  bprmf_epoch_size(h, &N, &S);
+  if (first_step < 0 || n_steps < 0 || first_step + n_steps > S)
+    return fail(BPRMF_E_INVALID, "steps [%lld, %lld) outside the epoch's %lld steps",
+                (long long)first_step, (long long)(first_step + n_steps), (long long)S);
+  const int64_t B = h->cfg.batch_size;
+  const int64_t chunk = chunk_triplets(h);
+  const int64_t beg = first_step * B, end = std::min(N, (first_step + n_steps) * B);
+  if (int r = ensure_trip(h, std::min(chunk, std::max<int64_t>(end - beg, 1)))) return r;
+  if (int r = begin_call(h)) return r;
+  const SamplerArgs sa = sampler_args(h);
+  int64_t steps = 0;
+  for (int64_t off = beg; off < end; off += chunk) {
+    const int64_t n = std::min(chunk, end - off);
+    int32_t* tu = h->d_trip;
+    int32_t* ti = tu + h->trip_cap;
+    int32_t* tj = ti + h->trip_cap;
+    {
+      ProfScope ps(h, BPRMF_KPROF_SAMPLE);
+      HIPCHK(sample(sa, epoch, off, n, tu, ti, tj, h->d_err, h->stream));
+    }
+    if (int r = run_steps(h, tu, ti, tj, n, &steps)) return r;
+  }
+  return end_call(h, st, end - beg, steps);
+}
+
+int bprmf_train_epoch(bprmf_handle* h, uint32_t epoch, bprmf_stats* st) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  int64_t N, S;
+  bprmf_epoch_size(h, &N, &S);
+  return bprmf_train_steps(h, epoch, 0, S, st);
+}
+
+int bprmf_train_triplets_dev(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                             int64_t n, bprmf_stats* st) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_STATE, "sharded handle: use the bprmf_dist_* phases");
+  if (int r = begin_call(h)) return r;
+  int64_t steps = 0;
+  if (int r = run_steps(h, u, i, j, n, &steps)) return r;
+  return end_call(h, st, n, steps);
+}
+
+int bprmf_train_triplets(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                         int64_t n, bprmf_stats* st) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_STATE, "sharded handle: use the bprmf_dist_* phases");
+  for (int64_t k = 0; k < n; ++k) {
+    if (u[k] < 0 || u[k] >= h->cfg.user_num)
+      return fail(BPRMF_E_RANGE, "user id %d at %lld out of range [0, %lld)", u[k], (long long)k,
+                  (long long)h->cfg.user_num);
+    if (i[k] < 0 || i[k] >= h->cfg.item_num || j[k] < 0 || j[k] >= h->cfg.item_num)
+      return fail(BPRMF_E_RANGE, "item id at %lld out of range [0, %lld)", (long long)k,
+                  (long long)h->cfg.item_num);
+  }
+  if (int r = set_dev(h)) return r;
+  const int64_t B = h->cfg.batch_size;
+  const int64_t chunk = std::max<int64_t>(B, (chunk_triplets(h) / B) * B);
+  if (int r = ensure_trip(h, std::min(chunk, std::max<int64_t>(n, 1)))) return r;
+  if (int r = begin_call(h)) return r;
+  int64_t steps = 0;
+  for (int64_t off = 0; off < n; off += h->trip_cap) {
+    const int64_t m = std::min(h->trip_cap, n - off);
+    int32_t* tu = h->d_trip;
+    int32_t* ti = tu + h->trip_cap;
+    int32_t* tj = ti + h->trip_cap;
+    HIPCHK(hipMemcpyAsync(tu, u + off, 4 * m, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(ti, i + off, 4 * m, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(tj, j + off, 4 * m, hipMemcpyHostToDevice, h->stream));
+    if (int r = run_steps(h, tu, ti, tj, m, &steps)) return r;
+    HIPCHK(hipStreamSynchronize(h->stream));  // host buffers reused by the next chunk's copies
+  }
+  return end_call(h, st, n, steps);
+}
+
+int bprmf_sample(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t* u, int32_t* i,
+                 int32_t* j) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (!h->d_pos_u || h->npos == 0) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
+  int64_t N;
+  bprmf_epoch_size(h, &N, nullptr);
+  if (first < 0 || first + n > N) return fail(BPRMF_E_INVALID, "slots outside the epoch");
+  if (int r = set_dev(h)) return r;
+  if (n == 0) return 0;
+  int32_t* buf = nullptr;
+  if (int r = dalloc(&buf, 3 * n)) return r;
+  int rc = 0;
+  hipError_t e = sample(sampler_args(h), epoch, first, n, buf, buf + n, buf + 2 * n, h->d_err, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(u, buf, 4 * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(i, buf + n, 4 * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(j, buf + 2 * n, 4 * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "sample: %s", hipGetErrorString(e));
+  hipFree(buf);
+  if (rc) return rc;
+  return check_err_flag(h);
+}
+
+int bprmf_dist_sample_dev(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t* u,
+                          int32_t* i, int32_t* j) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (!h->d_pos_u || h->npos == 0) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
+  int64_t N;
+  bprmf_epoch_size(h, &N, nullptr);
+  if (first < 0 || first + n > N) return fail(BPRMF_E_INVALID, "slots outside the epoch");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(sample(sampler_args(h), epoch, first, n, u, i, j, h->d_err, h->stream));
+  return 0;
+}
+
+int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
+  if (!h || !P || !Q) return fail(BPRMF_E_INVALID, "null argument");
+  if (int r = set_dev(h)) return r;
+  const size_t D = h->geom.D, ld = h->geom.ld;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemset(h->P.W, 0, sizeof(float) * h->U * ld));
+  HIPCHK(hipMemset(h->Q.W, 0, sizeof(float) * h->I * ld));
+  if (h->U) HIPCHK(hipMemcpy2D(h->P.W, ld * 4, P, D * 4, D * 4, h->U, hipMemcpyHostToDevice));
+  if (h->I) HIPCHK(hipMemcpy2D(h->Q.W, ld * 4, Q, D * 4, D * 4, h->I, hipMemcpyHostToDevice));
+  // rows are now current at step t; grads are zero between steps
+  std::vector<int32_t> st(std::max(h->U, h->I), h->t);
+  if (h->U) HIPCHK(hipMemcpy(h->P.stamp, st.data(), 4 * h->U, hipMemcpyHostToDevice));
+  if (h->I) HIPCHK(hipMemcpy(h->Q.stamp, st.data(), 4 * h->I, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int bprmf_get_weights(bprmf_handle* h, float* P, float* Q) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(flush(h->geom, h->P, h->hp, h->t, h->stream));
+  HIPCHK(flush(h->geom, h->Q, h->hp, h->t, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const size_t D = h->geom.D, ld = h->geom.ld;
+  if (P && h->U) HIPCHK(hipMemcpy2D(P, D * 4, h->P.W, ld * 4, D * 4, h->U, hipMemcpyDeviceToHost));
+  if (Q && h->I) HIPCHK(hipMemcpy2D(Q, D * 4, h->Q.W, ld * 4, D * 4, h->I, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bprmf_score(bprmf_handle* h, const int32_t* u, const int32_t* i, int64_t n, float* out) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !out))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_UNSUPPORTED, "score needs an unsharded handle");
+  for (int64_t k = 0; k < n; ++k) {
+    if (u[k] < 0 || u[k] >= h->cfg.user_num) return fail(BPRMF_E_RANGE, "Invalid user code");
+    if (i[k] < 0 || i[k] >= h->cfg.item_num) return fail(BPRMF_E_RANGE, "Invalid item code");
+  }
+  if (n == 0) return 0;
+  if (int r = set_dev(h)) return r;
+  int32_t* buf = nullptr;
+  if (int r = dalloc(&buf, 3 * n)) return r;
+  float* o = (float*)(buf + 2 * n);
+  int rc = 0;
+  hipError_t e = hipMemcpyAsync(buf, u, 4 * n, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(buf + n, i, 4 * n, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = score(h->geom, buf, buf + n, n, h->P, h->Q, h->hp, h->t, o, h->d_err, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, o, 4 * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "score: %s", hipGetErrorString(e));
+  hipFree(buf);
+  if (rc) return rc;
+  return check_err_flag(h);
+}
+
+int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const int64_t* j,
+                      int64_t n, float* pred_i, float* pred_j) {
+  if (!h || n < 0 || (n > 0 && (!u || !i || !pred_i))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_UNSUPPORTED, "forward needs an unsharded handle");
+  if (n == 0) return 0;
+  if (int r = set_dev(h)) return r;
+  HIPCHK(forward64(h->geom, u, i, j, n, h->P, h->Q, h->hp, h->t, pred_i, j ? pred_j : nullptr,
+                   h->d_err, h->stream));
+  return check_err_flag(h);
+}
+
+int bprmf_profile(bprmf_handle* h, int32_t enable) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->prof_on = enable != 0;
+  h->prof_used = 0;
+  for (auto& v : h->prof_rec) v.clear();
+  return 0;
+}
+
+int bprmf_profile_read(bprmf_handle* h, bprmf_kprof* out) {
+  if (!h || !out) return fail(BPRMF_E_INVALID, "null argument");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  memset(out, 0, sizeof *out);
+  for (int k = 0; k < BPRMF_KPROF_KINDS; ++k) {
+    double total = 0;
+    for (auto& pr : h->prof_rec[k]) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+      total += ms;
+    }
+    out->count[k] = (int64_t)h->prof_rec[k].size();
+    out->ms[k] = total;
+  }
+  return 0;
+}
+
+// ---- sharded phases ------------------------------------------------------------------------
+int bprmf_dist_begin_step(bprmf_handle* h) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double), h->stream));
+  return 0;
+}
+
+int bprmf_dist_gather_items(bprmf_handle* h, const int32_t* rows, int64_t n, float* out) {
+  if (!h || n < 0 || (n > 0 && (!rows || !out))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(gather_rows(h->geom, h->Q, rows, n, h->hp, h->t + 1, out, h->d_err, h->stream));
+  return 0;
+}
+
+int bprmf_dist_fwd_scatter(bprmf_handle* h, const int32_t* u_local, const int32_t* slot_i,
+                           const int32_t* slot_j, int64_t n, const float* item_rows,
+                           float* item_grads, int64_t n_slots) {
+  if (!h || n < 0 || (n > 0 && (!u_local || !slot_i || !slot_j || !item_rows || !item_grads)))
+    return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(dist_fwd_scatter(h->geom, u_local, slot_i, slot_j, n, h->P, item_rows, item_grads, n_slots,
+                          h->hp, h->t + 1, h->d_loss, h->d_err, h->stream));
+  return 0;
+}
+
+int bprmf_dist_apply_users(bprmf_handle* h, const int32_t* u_local, int64_t n) {
+  if (!h || n < 0 || (n > 0 && !u_local)) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(apply_rows(h->geom, h->P, u_local, n, h->hp, h->t + 1, h->stream));
+  return 0;
+}
+
+int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n) {
+  if (!h || n < 0 || (n > 0 && (!rows || !grads))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(add_rows(h->geom, h->Q, rows, grads, n, h->d_err, h->stream));
+  HIPCHK(apply_rows(h->geom, h->Q, rows, n, h->hp, h->t + 1, h->stream));
+  return 0;
+}
+
+int bprmf_dist_end_step(bprmf_handle* h, double* loss) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (int r = set_dev(h)) return r;
+  h->t += 1;
+  if (loss) {
+    HIPCHK(hipMemcpyAsync(loss, h->d_loss, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return check_err_flag(h);
+  }
+  return 0;
+}
+
+}  // extern "C"

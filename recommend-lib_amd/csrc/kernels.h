@@ -1,0 +1,71 @@
+// kernels.h — host-side launchers of the gfx950 BPR-MF kernels (kernels.hip).
+// Internal to libbprmf_amd.so; the public ABI is include/bprmf.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bprmf {
+
+// Row geometry: a row of D floats is stored with stride ld = G*EPL (zero padded); a group of G
+// lanes owns one row, lane `sub` holds elements sub + G*k, k < EPL.  D <= 64: G = next_pow2(D),
+// EPL = 1 (64/G rows per wave); D > 64: G = 64 (one row per wave), EPL = ceil(D/64).
+struct Geom {
+  int D, G, EPL, ld;
+};
+bool make_geom(int D, Geom* g);
+
+// One factor table (user or item side) resident in HBM.
+struct Table {
+  float* W;        // [rows, ld] weights, value valid at step stamp[row]
+  float* G;        // [rows, ld] gradient accumulator, zero outside a step
+  int32_t* stamp;  // [rows] step at which W[row] is current (lazy dense weight decay)
+  int64_t rows;
+};
+
+struct Hyper {
+  float lr, wd;
+  double alpha;  // 1 - lr*wd in double: per-step decay factor of untouched rows
+};
+
+struct SamplerArgs {
+  const int32_t* pos_u;   // [npos] global user id, features order
+  const int32_t* pos_i;   // [npos] global item id
+  const int64_t* indptr;  // [local_users+1]
+  const int32_t* indices; // sorted positives per local user
+  int64_t npos, item_num;
+  int32_t num_ng, world, feistel_h;
+  uint32_t k0, k1;        // Philox key (shard seed)
+};
+
+// --- launches (all asynchronous on `s`) ---
+hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
+                       uint32_t table_tag, int world, int rank, hipStream_t s);
+hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,
+                  int32_t* oi, int32_t* oj, int32_t* err, hipStream_t s);
+// single-GPU step t (1-based): K1 forward + grad scatter, K2 claim + apply
+hipError_t fwd_scatter(const Geom& g, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                       int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, double* loss,
+                       int32_t* err, hipStream_t s);
+hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                      int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, hipStream_t s);
+// scoring of the current weights after T steps (reads apply the pending decay)
+hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
+                 const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);
+hipError_t forward64(const Geom& g, const int64_t* u, const int64_t* i, const int64_t* j,
+                     int64_t n, Table P, Table Q, const Hyper& hp, int32_t T, float* oi, float* oj,
+                     int32_t* err, hipStream_t s);
+// bring every row of a table to step T (before get_weights)
+hipError_t flush(const Geom& g, Table W, const Hyper& hp, int32_t T, hipStream_t s);
+// --- sharded step phases ---
+hipError_t gather_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
+                       int32_t t, float* out, int32_t* err, hipStream_t s);
+hipError_t dist_fwd_scatter(const Geom& g, const int32_t* ul, const int32_t* si, const int32_t* sj,
+                            int64_t n, Table P, const float* item_rows, float* item_grads,
+                            int64_t n_slots, const Hyper& hp, int32_t t, double* loss,
+                            int32_t* err, hipStream_t s);
+hipError_t add_rows(const Geom& g, Table W, const int32_t* rows, const float* grads, int64_t n,
+                    int32_t* err, hipStream_t s);
+hipError_t apply_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
+                      int32_t t, hipStream_t s);
+
+}  // namespace bprmf

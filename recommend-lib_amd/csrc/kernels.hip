@@ -1,0 +1,617 @@
+// kernels.hip — gfx950 (MI355X / CDNA4) kernels of the BPR-MF training path.
+//
+// What the reference computes per step (BPRMFRecommender.py:172-176), restated for the kernels:
+//   x_b  = <P_u,Q_i> - <P_u,Q_j>            (BPR.forward, :42-50)
+//   c_b  = sigmoid(-x_b) = -dL/dx_b          (loss = -sum log sigmoid(x), :174)
+//   G_P[u] += -c (Q_i - Q_j);  G_Q[i] += -c P_u;  G_Q[j] += c P_u   (embedding backward, duplicates summed)
+//   every row: W <- W - lr (G + wd W)        (SGD weight_decay over dense grads, :154,:176)
+// Rows not referenced in a step only decay; that decay is applied lazily (stamp per row, factor
+// (1-lr*wd)^k computed in double) so a step touches only its 3B rows, never the whole table.
+//
+// Memory-bound by design (≈0.66 flop/B): no MFMA.  A group of G lanes owns one row; lane `sub`
+// holds elements sub + G*k, so every global load / f32 atomic wave-instruction covers whole
+// contiguous 256 B (G=64) or 128 B (G=32) row segments — the shape the memory-side atomic unit
+// runs at full rate (MI355X_MICROARCH.md §Global float atomics).
+#include "kernels.h"
+
+#include <math.h>
+
+namespace bprmf {
+
+constexpr uint32_t TAG_NEG = 0x4E470000u;
+constexpr uint32_t TAG_PERM = 0x50520000u;
+constexpr uint32_t TAG_INIT = 0x494E0000u;
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = 256 * 8;  // 256 CUs x 8 resident 256-thread blocks, grid-stride beyond
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based; Salmon et al. SC'11).  Stateless: every triplet / element draws
+// from its own counter, so the sampler is embarrassingly parallel and bit-reproducible.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
+                                         uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// keyed bijection of [0, n): balanced Feistel on 2h bits, cycle-walking back into range.
+__device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int h, uint32_t k0, uint32_t k1,
+                                            uint32_t epoch) {
+  const uint64_t mask = (h >= 32) ? 0xFFFFFFFFull : ((1ull << h) - 1);
+  do {
+    uint64_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (uint32_t r = 0; r < 6; ++r) {
+      uint32_t c0 = (uint32_t)R, c1 = r, c2 = epoch, c3 = TAG_PERM | r;
+      philox10(c0, c1, c2, c3, k0, k1);
+      const uint64_t nl = R;
+      R = L ^ ((uint64_t)c0 & mask);
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
+// unbiased Lemire reduction into [0, n), n >= 1; retries draw fresh counters (attempt in tag).
+__device__ __forceinline__ uint32_t bounded(uint64_t q, uint32_t epoch, uint32_t n, uint32_t k0,
+                                            uint32_t k1) {
+  const uint32_t thresh = (uint32_t)((0x100000000ull - n) % n);
+  for (uint32_t a = 0;; ++a) {
+    uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = epoch, c3 = TAG_NEG | a;
+    philox10(c0, c1, c2, c3, k0, k1);
+    const uint64_t m = (uint64_t)c0 * n;
+    if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
+  }
+}
+
+// j = the k-th item id NOT in the sorted positive list a[0..n): m = #{x : a[x]-x <= k}, j = k+m.
+__device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restrict__ a, int64_t n, int64_t k) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)a[mid] - mid <= k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return k + lo;
+}
+
+// ng_sample + DataLoader shuffle of one epoch (util/data_loader.py:680-690,
+// BPRMFRecommender.py:141): slot s -> triplet q = perm(s) -> positive q / num_ng -> negative j
+// uniform over the user's non-positives.
+__global__ __launch_bounds__(kBlock) void k_sample(SamplerArgs a, uint32_t epoch, int64_t first,
+                                                   int64_t count, int32_t* __restrict__ ou,
+                                                   int32_t* __restrict__ oi,
+                                                   int32_t* __restrict__ oj,
+                                                   int32_t* __restrict__ err) {
+  const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = permute((uint64_t)(first + s), N, a.feistel_h, a.k0, a.k1, epoch);
+    const int64_t p = (int64_t)(q / (uint64_t)a.num_ng);
+    const int32_t u = a.pos_u[p];
+    const int32_t i = a.pos_i[p];
+    const int64_t ul = u / a.world;
+    const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
+    const int64_t free_items = a.item_num - deg;
+    int32_t j = -1;
+    if (free_items > 0) {
+      const uint32_t k = bounded(q, epoch, (uint32_t)free_items, a.k0, a.k1);
+      j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
+    } else {
+      atomicOr(err, 2);
+    }
+    ou[s] = u;
+    oi[s] = i;
+    oj[s] = j;
+  }
+}
+
+// N(0, std^2) init (nn.init.normal_, BPRMFRecommender.py:39-40): Box-Muller on Philox output,
+// one counter per element; padding columns are zero.
+__global__ __launch_bounds__(kBlock) void k_init_normal(float* __restrict__ W, int64_t rows, int ld,
+                                                        int D, float std, uint32_t k0, uint32_t k1,
+                                                        uint32_t tag, int world, int rank) {
+  const int64_t total = rows * (int64_t)ld;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / ld;
+    const int c = (int)(e - r * ld);
+    const int64_t rg = r * world + rank;  // global row: same init for every sharding
+    float v = 0.f;
+    if (c < D) {
+      uint32_t c0 = (uint32_t)rg, c1 = (uint32_t)(rg >> 32), c2 = (uint32_t)c, c3 = TAG_INIT | tag;
+      philox10(c0, c1, c2, c3, k0, k1);
+      const float u1 = ((float)c0 + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+      const float u2 = (float)c1 * 2.3283064365386963e-10f;
+      v = std * sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+    }
+    W[e] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Training step kernels
+// ------------------------------------------------------------------------------------------------
+// (1 - lr*wd)^k in double by squaring (deterministic IEEE order), rounded once to fp32.
+__device__ __forceinline__ float decay_pow(double alpha, int32_t k) {
+  if (k <= 0) return 1.0f;
+  double r = 1.0, b = alpha;
+  while (k) {
+    if (k & 1) r *= b;
+    b *= b;
+    k >>= 1;
+  }
+  return (float)r;
+}
+
+__device__ __forceinline__ float softplus(float z) {  // log(1 + e^z), overflow-free
+  return fmaxf(z, 0.f) + log1pf(expf(-fabsf(z)));
+}
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// sum over the wave of per-lane loss partials -> one f64 atomic per wave
+__device__ __forceinline__ void wave_add_loss(double* loss, float v) {
+  if (!loss) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(loss, (double)v);
+}
+
+struct RowPtrs {
+  const float* w;
+  float f;
+};
+
+// K1 — fused gather (with pending decay) + 2 dots + sigmoid + gradient scatter.
+//   reads  3 rows + 3 stamps + 3 ids per triplet;  writes 3 rows of f32 atomic adds into G.
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_fwd_scatter(const int32_t* __restrict__ tu,
+                                                        const int32_t* __restrict__ ti,
+                                                        const int32_t* __restrict__ tj, int64_t n,
+                                                        Table P, Table Q, Hyper hp, int ld,
+                                                        int32_t t, double* loss,
+                                                        int32_t* __restrict__ err) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  float lsum = 0.f;
+  for (int64_t b = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; b < n; b += ngroups) {
+    const int32_t u = tu[b], i = ti[b], j = tj[b];
+    if ((uint64_t)u >= (uint64_t)P.rows || (uint64_t)i >= (uint64_t)Q.rows ||
+        (uint64_t)j >= (uint64_t)Q.rows) {
+      if (sub == 0) atomicOr(err, 1);
+      continue;
+    }
+    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
+    const float fi = decay_pow(hp.alpha, t - 1 - Q.stamp[i]);
+    const float fj = decay_pow(hp.alpha, t - 1 - Q.stamp[j]);
+    const float* pu = P.W + (int64_t)u * ld + sub;
+    const float* qi = Q.W + (int64_t)i * ld + sub;
+    const float* qj = Q.W + (int64_t)j * ld + sub;
+    float vu[EPL], vi[EPL], vj[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      vu[k] = pu[G * k];
+      vi[k] = qi[G * k];
+      vj[k] = qj[G * k];
+    }
+    float di = 0.f, dj = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      vu[k] *= fu;
+      vi[k] *= fi;
+      vj[k] *= fj;
+      di = fmaf(vu[k], vi[k], di);
+      dj = fmaf(vu[k], vj[k], dj);
+    }
+    di = group_sum<G>(di);
+    dj = group_sum<G>(dj);
+    const float x = di - dj;
+    const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x)
+    if (sub == 0) lsum += softplus(-x);
+    float* gu = P.G + (int64_t)u * ld + sub;
+    float* gi = Q.G + (int64_t)i * ld + sub;
+    float* gj = Q.G + (int64_t)j * ld + sub;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const float cu = c * vu[k];
+      atomicAdd(gu + G * k, -c * (vi[k] - vj[k]));
+      atomicAdd(gi + G * k, -cu);
+      atomicAdd(gj + G * k, cu);
+    }
+  }
+  wave_add_loss(loss, lsum);
+}
+
+// apply one claimed row: V = W*alpha^(t-1-old); W = V - lr*(G + wd*V); G = 0
+template <int G, int EPL>
+__device__ __forceinline__ void apply_row(Table T, int64_t row, int32_t old, const Hyper& hp,
+                                          int ld, int32_t t, int sub) {
+  const float f = decay_pow(hp.alpha, t - 1 - old);
+  float* w = T.W + row * ld + sub;
+  float* g = T.G + row * ld + sub;
+  float wv[EPL], gv[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    wv[k] = w[G * k];
+    gv[k] = g[G * k];
+  }
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const float v = wv[k] * f;
+    const float dp = fmaf(hp.wd, v, gv[k]);  // grad.add(param, alpha=wd)
+    w[G * k] = fmaf(-hp.lr, dp, v);          // param.add_(grad, alpha=-lr)
+    g[G * k] = 0.f;
+  }
+}
+
+// claim row for step t: the first group to swap the stamp applies it, later duplicates skip.
+template <int G>
+__device__ __forceinline__ int32_t claim(int32_t* stamp, int64_t row, int32_t t, int sub) {
+  int32_t old = 0;
+  if (sub == 0) old = atomicExch(stamp + row, t);
+  return __shfl(old, (int)(threadIdx.x & 63) - sub);
+}
+
+// K2 — every row referenced by the step's 3n ids is claimed once and updated.
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_apply_refs(const int32_t* __restrict__ tu,
+                                                       const int32_t* __restrict__ ti,
+                                                       const int32_t* __restrict__ tj, int64_t n,
+                                                       Table P, Table Q, Hyper hp, int ld,
+                                                       int32_t t) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < 3 * n; r += ngroups) {
+    const int which = (int)(r / n);
+    const int64_t b = r - (int64_t)which * n;
+    const int32_t row = which == 0 ? tu[b] : (which == 1 ? ti[b] : tj[b]);
+    Table T = which == 0 ? P : Q;
+    if ((uint64_t)row >= (uint64_t)T.rows) continue;
+    const int32_t old = claim<G>(T.stamp, row, t, sub);
+    if (old == t) continue;
+    apply_row<G, EPL>(T, row, old, hp, ld, t, sub);
+  }
+}
+
+// rows referenced by a list (sharded path: local users of the batch, or received item ids)
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_apply_rows(const int32_t* __restrict__ rows, int64_t n,
+                                                       Table T, Hyper hp, int ld, int32_t t) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < n; r += ngroups) {
+    const int32_t row = rows[r];
+    if ((uint64_t)row >= (uint64_t)T.rows) continue;
+    const int32_t old = claim<G>(T.stamp, row, t, sub);
+    if (old == t) continue;
+    apply_row<G, EPL>(T, row, old, hp, ld, t, sub);
+  }
+}
+
+// scores <P_u, Q_i> of the weights after T steps
+template <int G, int EPL, typename Idx>
+__global__ __launch_bounds__(kBlock) void k_score(const Idx* __restrict__ us,
+                                                  const Idx* __restrict__ is,
+                                                  const Idx* __restrict__ js, int64_t n, Table P,
+                                                  Table Q, Hyper hp, int ld, int32_t T,
+                                                  float* __restrict__ oi, float* __restrict__ oj,
+                                                  int32_t* __restrict__ err) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t b = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; b < n; b += ngroups) {
+    const int64_t u = (int64_t)us[b], i = (int64_t)is[b];
+    const int64_t j = js ? (int64_t)js[b] : 0;
+    if ((uint64_t)u >= (uint64_t)P.rows || (uint64_t)i >= (uint64_t)Q.rows ||
+        (uint64_t)j >= (uint64_t)Q.rows) {
+      if (sub == 0) {
+        atomicOr(err, 1);
+        oi[b] = NAN;
+        if (oj) oj[b] = NAN;
+      }
+      continue;
+    }
+    const float fu = decay_pow(hp.alpha, T - P.stamp[u]);
+    const float fi = decay_pow(hp.alpha, T - Q.stamp[i]);
+    const float fj = js ? decay_pow(hp.alpha, T - Q.stamp[j]) : 0.f;
+    const float* pu = P.W + u * ld + sub;
+    const float* qi = Q.W + i * ld + sub;
+    const float* qj = Q.W + j * ld + sub;
+    float di = 0.f, dj = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const float vu = pu[G * k] * fu;
+      di = fmaf(vu, qi[G * k] * fi, di);
+      if (js) dj = fmaf(vu, qj[G * k] * fj, dj);
+    }
+    di = group_sum<G>(di);
+    dj = group_sum<G>(dj);
+    if (sub == 0) {
+      oi[b] = di;
+      if (oj) oj[b] = dj;
+    }
+  }
+}
+
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_flush(Table T, Hyper hp, int ld, int32_t Tstep) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < T.rows; r += ngroups) {
+    const int32_t s = T.stamp[r];
+    if (s == Tstep) continue;
+    const float f = decay_pow(hp.alpha, Tstep - s);
+    float* w = T.W + r * ld + sub;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) w[G * k] *= f;
+    __builtin_amdgcn_wave_barrier();
+    if (sub == 0) T.stamp[r] = Tstep;
+  }
+}
+
+// owner side of the item exchange: rows of the shard, brought to step t-1, packed [n, ld]
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_gather_rows(Table T, const int32_t* __restrict__ rows,
+                                                        int64_t n, Hyper hp, int ld, int32_t t,
+                                                        float* __restrict__ out,
+                                                        int32_t* __restrict__ err) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < n; r += ngroups) {
+    const int64_t row = rows[r];
+    float* o = out + r * ld + sub;
+    if ((uint64_t)row >= (uint64_t)T.rows) {
+      if (sub == 0) atomicOr(err, 1);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) o[G * k] = 0.f;
+      continue;
+    }
+    const float f = decay_pow(hp.alpha, t - 1 - T.stamp[row]);
+    const float* w = T.W + row * ld + sub;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) o[G * k] = w[G * k] * f;
+  }
+}
+
+// requester side: local users vs received item rows; item grads go to a slot buffer [n_slots, ld]
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_dist_fwd_scatter(
+    const int32_t* __restrict__ ul, const int32_t* __restrict__ si, const int32_t* __restrict__ sj,
+    int64_t n, Table P, const float* __restrict__ rows, float* __restrict__ grads, int64_t n_slots,
+    Hyper hp, int ld, int32_t t, double* loss, int32_t* __restrict__ err) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  float lsum = 0.f;
+  for (int64_t b = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; b < n; b += ngroups) {
+    const int32_t u = ul[b], a = si[b], c2 = sj[b];
+    if ((uint64_t)u >= (uint64_t)P.rows || (uint64_t)a >= (uint64_t)n_slots ||
+        (uint64_t)c2 >= (uint64_t)n_slots) {
+      if (sub == 0) atomicOr(err, 1);
+      continue;
+    }
+    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
+    const float* pu = P.W + (int64_t)u * ld + sub;
+    const float* qi = rows + (int64_t)a * ld + sub;
+    const float* qj = rows + (int64_t)c2 * ld + sub;
+    float vu[EPL], vi[EPL], vj[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      vu[k] = pu[G * k];
+      vi[k] = qi[G * k];
+      vj[k] = qj[G * k];
+    }
+    float di = 0.f, dj = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      vu[k] *= fu;
+      di = fmaf(vu[k], vi[k], di);
+      dj = fmaf(vu[k], vj[k], dj);
+    }
+    di = group_sum<G>(di);
+    dj = group_sum<G>(dj);
+    const float x = di - dj;
+    const float c = 1.0f / (1.0f + expf(x));
+    if (sub == 0) lsum += softplus(-x);
+    float* gu = P.G + (int64_t)u * ld + sub;
+    float* gi = grads + (int64_t)a * ld + sub;
+    float* gj = grads + (int64_t)c2 * ld + sub;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const float cu = c * vu[k];
+      atomicAdd(gu + G * k, -c * (vi[k] - vj[k]));
+      atomicAdd(gi + G * k, -cu);
+      atomicAdd(gj + G * k, cu);
+    }
+  }
+  wave_add_loss(loss, lsum);
+}
+
+// owner side: received item grads summed into the shard's accumulator
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_add_rows(Table T, const int32_t* __restrict__ rows,
+                                                     const float* __restrict__ grads, int64_t n,
+                                                     int ld, int32_t* __restrict__ err) {
+  const int sub = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
+  for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < n; r += ngroups) {
+    const int64_t row = rows[r];
+    if ((uint64_t)row >= (uint64_t)T.rows) {
+      if (sub == 0) atomicOr(err, 1);
+      continue;
+    }
+    const float* g = grads + r * ld + sub;
+    float* d = T.G + row * ld + sub;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) atomicAdd(d + G * k, g[G * k]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+bool make_geom(int D, Geom* g) {
+  if (D <= 0 || D > 1024) return false;
+  g->D = D;
+  if (D <= 64) {
+    int G = 4;
+    while (G < D) G <<= 1;
+    g->G = G;
+    g->EPL = 1;
+  } else {
+    int e = (D + 63) / 64;
+    static const int allowed[] = {2, 3, 4, 5, 6, 7, 8, 12, 16};
+    int pick = 16;
+    for (int a : allowed)
+      if (a >= e) {
+        pick = a;
+        break;
+      }
+    g->G = 64;
+    g->EPL = pick;
+  }
+  g->ld = g->G * g->EPL;
+  return true;
+}
+
+static inline unsigned grid_for(int64_t units, int G) {
+  const int64_t per_block = kBlock / G;
+  int64_t b = (units + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > kMaxBlocks) b = kMaxBlocks;
+  return (unsigned)b;
+}
+static inline unsigned grid_flat(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > 4 * kMaxBlocks) b = 4 * kMaxBlocks;
+  return (unsigned)b;
+}
+
+// Expand `BODY` for every instantiated (G, EPL) geometry.
+#define BPRMF_DISPATCH(geom, BODY)                                  \
+  switch ((geom).G * 100 + (geom).EPL) {                            \
+    case 401: { constexpr int G_ = 4, E_ = 1; BODY; } break;        \
+    case 801: { constexpr int G_ = 8, E_ = 1; BODY; } break;        \
+    case 1601: { constexpr int G_ = 16, E_ = 1; BODY; } break;      \
+    case 3201: { constexpr int G_ = 32, E_ = 1; BODY; } break;      \
+    case 6401: { constexpr int G_ = 64, E_ = 1; BODY; } break;      \
+    case 6402: { constexpr int G_ = 64, E_ = 2; BODY; } break;      \
+    case 6403: { constexpr int G_ = 64, E_ = 3; BODY; } break;      \
+    case 6404: { constexpr int G_ = 64, E_ = 4; BODY; } break;      \
+    case 6405: { constexpr int G_ = 64, E_ = 5; BODY; } break;      \
+    case 6406: { constexpr int G_ = 64, E_ = 6; BODY; } break;      \
+    case 6407: { constexpr int G_ = 64, E_ = 7; BODY; } break;      \
+    case 6408: { constexpr int G_ = 64, E_ = 8; BODY; } break;      \
+    case 6412: { constexpr int G_ = 64, E_ = 12; BODY; } break;     \
+    case 6416: { constexpr int G_ = 64, E_ = 16; BODY; } break;     \
+    default: return hipErrorInvalidValue;                           \
+  }
+
+hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
+                       uint32_t table_tag, int world, int rank, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  k_init_normal<<<grid_flat(rows * g.ld), kBlock, 0, s>>>(W, rows, g.ld, g.D, std, k0, k1, table_tag,
+                                                          world, rank);
+  return hipGetLastError();
+}
+
+hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,
+                  int32_t* oi, int32_t* oj, int32_t* err, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  k_sample<<<grid_flat(count), kBlock, 0, s>>>(a, epoch, first, count, ou, oi, oj, err);
+  return hipGetLastError();
+}
+
+hipError_t fwd_scatter(const Geom& g, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                       int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, double* loss,
+                       int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_fwd_scatter<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(
+                        tu, ti, tj, n, P, Q, hp, g.ld, t, loss, err)));
+  return hipGetLastError();
+}
+
+hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                      int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_apply_refs<G_, E_><<<grid_for(3 * n, G_), kBlock, 0, s>>>(
+                        tu, ti, tj, n, P, Q, hp, g.ld, t)));
+  return hipGetLastError();
+}
+
+hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
+                 const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_score<G_, E_, int32_t><<<grid_for(n, G_), kBlock, 0, s>>>(
+                        u, i, (const int32_t*)nullptr, n, P, Q, hp, g.ld, T, out, nullptr, err)));
+  return hipGetLastError();
+}
+
+hipError_t forward64(const Geom& g, const int64_t* u, const int64_t* i, const int64_t* j,
+                     int64_t n, Table P, Table Q, const Hyper& hp, int32_t T, float* oi, float* oj,
+                     int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_score<G_, E_, int64_t><<<grid_for(n, G_), kBlock, 0, s>>>(
+                        u, i, j, n, P, Q, hp, g.ld, T, oi, oj, err)));
+  return hipGetLastError();
+}
+
+hipError_t flush(const Geom& g, Table W, const Hyper& hp, int32_t T, hipStream_t s) {
+  if (W.rows <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_flush<G_, E_><<<grid_for(W.rows, G_), kBlock, 0, s>>>(W, hp, g.ld, T)));
+  return hipGetLastError();
+}
+
+hipError_t gather_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
+                       int32_t t, float* out, int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_gather_rows<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(
+                        W, rows, n, hp, g.ld, t, out, err)));
+  return hipGetLastError();
+}
+
+hipError_t dist_fwd_scatter(const Geom& g, const int32_t* ul, const int32_t* si, const int32_t* sj,
+                            int64_t n, Table P, const float* item_rows, float* item_grads,
+                            int64_t n_slots, const Hyper& hp, int32_t t, double* loss,
+                            int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_dist_fwd_scatter<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(
+                        ul, si, sj, n, P, item_rows, item_grads, n_slots, hp, g.ld, t, loss, err)));
+  return hipGetLastError();
+}
+
+hipError_t add_rows(const Geom& g, Table W, const int32_t* rows, const float* grads, int64_t n,
+                    int32_t* err, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_add_rows<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(W, rows, grads, n,
+                                                                           g.ld, err)));
+  return hipGetLastError();
+}
+
+hipError_t apply_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
+                      int32_t t, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  BPRMF_DISPATCH(g, (k_apply_rows<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(rows, n, W, hp,
+                                                                             g.ld, t)));
+  return hipGetLastError();
+}
+
+}  // namespace bprmf

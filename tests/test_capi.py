@@ -1,0 +1,48 @@
+"""CPU: the C-ABI library builds for gfx950, loads, and exports every symbol include/bprmf.h
+declares.  No compute call is made here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "bprmf.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(bprmf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol(rl):
+    lib = rl.build()
+    L = ctypes.CDLL(lib)
+    names = _declared()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # and the Python binding covers the same set
+    assert set(names) == set(rl._lib.SIGNATURES), set(names) ^ set(rl._lib.SIGNATURES)
+
+
+def test_library_is_gfx950_code_object(rl):
+    lib = rl.build()
+    with open(lib, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_no_gpu_fails_loudly(rl):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises((rl.BprmfError, ValueError, RuntimeError)):
+        rl.BPRMF(10, 10, 8)
+
+
+def test_config_layout_matches_header(rl):
+    # int64,int64,int32,float,float,int32,int32,float,uint64,int32,int32,int32,int32[4]
+    assert ctypes.sizeof(rl._lib.Config) == 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4 + 8 + 4 + 4 + 4 + 16 + 4
+    assert ctypes.sizeof(rl._lib.Stats) == 32

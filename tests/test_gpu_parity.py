@@ -1,0 +1,316 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference fixtures and the oracle.
+
+Tolerances (fp32 path; the integer/index path is bit-exact):
+  STEP_ATOL  per-element |HIP - reference| after replayed steps.  The reference (torch CPU) and the
+             HIP kernels differ only in summation order (wave-tree dots, f32 atomics) and in fused
+             multiply-adds, i.e. O(ulp) per step on values of magnitude ~1e-2.
+  LOSS_RTOL  relative difference of the per-call loss sum.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import bpr_oracle as O
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+
+STEP_ATOL = 1e-7
+LOSS_RTOL = 1e-5
+
+
+def _model(rl, U, I, d, B, lr=0.01, wd=0.001, **kw):
+    return rl.BPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, **kw)
+
+
+# ---------------------------------------------------------------------------------------------
+# training step parity (replay of reference triplets)
+# ---------------------------------------------------------------------------------------------
+def test_replay_tiny_steps_match_reference(rl, golden):
+    f = golden("bpr_step_tiny.npz")
+    m = _model(rl, int(f["U"]), int(f["I"]), int(f["d"]), int(f["B"]), float(f["lr"]), float(f["wd"]))
+    m.set_weights(f["P0"], f["Q0"])
+    for b in range(f["triplets"].shape[0]):
+        t = f["triplets"][b]
+        st = m.train_triplets(t[0], t[1], t[2])
+        assert st["steps"] == 1
+        P, Q = m.get_weights()
+        np.testing.assert_allclose(P, f["P"][b], rtol=0, atol=STEP_ATOL)
+        np.testing.assert_allclose(Q, f["Q"][b], rtol=0, atol=STEP_ATOL)
+        assert st["loss"] == pytest.approx(f["loss"][b], rel=LOSS_RTOL)
+
+
+def test_replay_ml100k_epoch_matches_reference(rl, golden):
+    """F2: one full reference epoch (72 batches of the reference's own triplets)."""
+    f = golden("bpr_ml100k_replay.npz")
+    tr = f["triplets"].astype(np.int32)
+    bd = f["batch_bounds"]
+    m = _model(rl, int(f["U"]), int(f["I"]), int(f["d"]), int(f["B"]), float(f["lr"]), float(f["wd"]))
+    m.set_weights(f["P0"], f["Q0"])
+    st = m.train_triplets(tr[0, :bd[10]], tr[1, :bd[10]], tr[2, :bd[10]])
+    assert st["steps"] == 10
+    P, Q = m.get_weights()
+    np.testing.assert_allclose(P, f["P10"], rtol=0, atol=STEP_ATOL)
+    np.testing.assert_allclose(Q, f["Q10"], rtol=0, atol=STEP_ATOL)
+    assert st["loss"] == pytest.approx(f["loss"][:10].sum(), rel=LOSS_RTOL)
+    st = m.train_triplets(tr[0, bd[10]:], tr[1, bd[10]:], tr[2, bd[10]:])
+    assert st["steps"] == len(bd) - 11  # last reference batch is partial, as in the DataLoader
+    P, Q = m.get_weights()
+    np.testing.assert_allclose(P, f["P_epoch"], rtol=0, atol=STEP_ATOL)
+    np.testing.assert_allclose(Q, f["Q_epoch"], rtol=0, atol=STEP_ATOL)
+
+
+def test_replay_from_device_tensors(rl, golden):
+    import torch
+    f = golden("bpr_step_tiny.npz")
+    m = _model(rl, int(f["U"]), int(f["I"]), int(f["d"]), int(f["B"]))
+    m.set_weights(f["P0"], f["Q0"])
+    t = torch.from_numpy(f["triplets"][0].astype(np.int64)).cuda()
+    m.train_triplets(t[0], t[1], t[2])
+    P, Q = m.get_weights()
+    np.testing.assert_allclose(P, f["P"][0], rtol=0, atol=STEP_ATOL)
+
+
+@pytest.mark.parametrize("d", [1, 3, 8, 32, 48, 64, 100, 128, 256, 384])
+def test_step_vs_oracle_all_geometries(rl, d):
+    """Every (G, EPL) row geometry, padded widths included, against the dense oracle."""
+    g = np.random.default_rng(d)
+    U, I, B = 37, 53, 96
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    m = _model(rl, U, I, d, B, lr=0.05, wd=0.01)
+    m.set_weights(P0, Q0)
+    P, Q = P0.copy(), Q0.copy()
+    for _ in range(4):
+        u, i, j = g.integers(0, U, B), g.integers(0, I, B), g.integers(0, I, B)
+        m.train_triplets(u, i, j)
+        O.bpr_step_dense(P, Q, u, i, j, 0.05, 0.01)
+    Pg, Qg = m.get_weights()
+    np.testing.assert_allclose(Pg, P, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Qg, Q, rtol=1e-5, atol=1e-6)
+
+
+def test_lazy_decay_equals_dense_decay(rl):
+    """Rows untouched for many steps carry (1-lr*wd)^k exactly as the dense SGD would."""
+    g = np.random.default_rng(0)
+    U, I, d = 64, 64, 16
+    P0 = g.standard_normal((U, d)).astype(np.float32)
+    Q0 = g.standard_normal((I, d)).astype(np.float32)
+    m = _model(rl, U, I, d, 8, lr=0.1, wd=0.05)
+    m.set_weights(P0, Q0)
+    P, Q = P0.copy(), Q0.copy()
+    for s in range(60):  # only rows 0..3 are ever touched
+        u = g.integers(0, 4, 8)
+        i = g.integers(0, 4, 8)
+        j = g.integers(0, 4, 8)
+        m.train_triplets(u, i, j)
+        O.bpr_step_dense(P, Q, u, i, j, 0.1, 0.05)
+    Pg, Qg = m.get_weights()
+    np.testing.assert_allclose(Pg[4:], P[4:], rtol=2e-6)  # pure decay rows
+    np.testing.assert_allclose(Qg[4:], Q[4:], rtol=2e-6)
+    np.testing.assert_allclose(Pg[:4], P[:4], rtol=1e-4, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+# sampler: bit-exact vs the oracle restatement
+# ---------------------------------------------------------------------------------------------
+def _ml100k_pos(golden):
+    f = golden("bpr_ml100k_replay.npz")
+    return f["positives"].astype(np.int64), int(f["U"]), int(f["I"])
+
+
+def test_sampler_bit_exact_ml100k(rl, golden):
+    pos, U, I = _ml100k_pos(golden)
+    m = _model(rl, U, I, 32, 4096, seed=0xDEADBEEF12345)
+    m.set_train(pos)
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    N = len(pos) * 4
+    for epoch in (0, 1, 17):
+        got = m.sample(epoch, 0, N)
+        want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 0xDEADBEEF12345, epoch, 0, N)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+    got = m.sample(3, N - 1000, 1000)
+    want = O.sample_triplets(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 0xDEADBEEF12345, 3, N - 1000, 1000)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)
+
+
+def test_sampler_bit_exact_sharded(rl, golden):
+    pos, U, I = _ml100k_pos(golden)
+    world, seed = 3, 77
+    for rank in range(world):
+        m = _model(rl, U, I, 8, 1024, seed=seed, rank=rank, world=world)
+        m.set_train(pos)
+        mine = pos[pos[:, 0] % world == rank]
+        indptr, indices = O.build_csr(mine[:, 0], mine[:, 1], U)
+        shard_seed = (seed + rank * 0x9E3779B97F4A7C15) & (2**64 - 1)
+        N = len(mine) * 4
+        got = m.sample(2, 0, N)
+        want = C.sample(mine[:, 0], mine[:, 1], indptr, indices, I, 4, shard_seed, 2, 0, N)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+
+
+def test_bprdata_dropin(rl, golden):
+    pos, U, I = _ml100k_pos(golden)
+    ds = rl.BPRData(pos.tolist(), I, None, 4, True, seed=5)
+    ds.ng_sample()
+    assert len(ds) == 4 * len(pos)
+    u, i, j = ds[0]
+    keys = set(map(tuple, pos.tolist()))
+    assert (u, i) in keys and (u, j) not in keys
+    test = rl.BPRData(pos[:10].tolist(), I, None, 0, False)
+    assert test[3] == (int(pos[3, 0]), int(pos[3, 1]), int(pos[3, 1]))
+    with pytest.raises(AssertionError):
+        test.ng_sample()
+
+
+def test_train_mat_exclusions(rl):
+    """Pairs only in train_mat (not in features) are never drawn as negatives."""
+    import scipy.sparse as sp
+    U, I = 4, 12
+    feats = [[0, 1], [1, 2], [2, 3], [3, 4]]
+    tm = sp.dok_matrix((U, I), dtype=np.float32)
+    for u, i in feats:
+        tm[u, i] = 1.0
+    for i in range(5, 11):
+        tm[0, i] = 1.0  # user 0 also excludes 5..10 -> only {0, 11} remain
+    ds = rl.BPRData(feats, I, tm, 50, True, seed=1, num_user=U)
+    ds.ng_sample()
+    f = ds.features_fill
+    assert set(f[f[:, 0] == 0][:, 2].tolist()) <= {0, 11}
+
+
+# ---------------------------------------------------------------------------------------------
+# scoring / drop-in forward
+# ---------------------------------------------------------------------------------------------
+def test_forward_and_predict(rl):
+    import torch
+    g = np.random.default_rng(1)
+    U, I, d = 20, 30, 32
+    P0 = g.standard_normal((U, d)).astype(np.float32)
+    Q0 = g.standard_normal((I, d)).astype(np.float32)
+    m = _model(rl, U, I, d, 16)
+    m.set_weights(P0, Q0)
+    u, i, j = g.integers(0, U, 100), g.integers(0, I, 100), g.integers(0, I, 100)
+    pi, pj = m(torch.from_numpy(u), torch.from_numpy(i), torch.from_numpy(j))
+    np.testing.assert_allclose(pi.numpy(), (P0[u] * Q0[i]).sum(1), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(pj.numpy(), (P0[u] * Q0[j]).sum(1), rtol=1e-5, atol=1e-5)
+    s0, _ = m(torch.tensor(3), torch.tensor(4), torch.tensor(4))  # 0-d, as the KPI loop calls it
+    assert s0.shape == () and float(s0) == pytest.approx(float(P0[3] @ Q0[4]), rel=1e-5)
+    pc, _ = m(torch.from_numpy(u).cuda(), torch.from_numpy(i).cuda(), torch.from_numpy(j).cuda())
+    assert pc.is_cuda
+    assert m.predict(3, 4) == pytest.approx(float(P0[3] @ Q0[4]), rel=1e-5)
+    with pytest.raises(ValueError, match="Invalid user code"):
+        m.predict(U, 0)
+    with pytest.raises(ValueError, match="Invalid item code"):
+        m.predict(0, I)
+
+
+def test_metric_eval_dropin_matches_reference_kat(rl):
+    """util/metrics.py _bpr_topk on the reference model's weights (F4) through our forward."""
+    import torch
+    with open(os.path.join(GOLDEN, "metrics_kat.json")) as fh:
+        kat = json.load(fh)["bpr_topk"]
+    P = np.array(kat["P"], dtype=np.float32)
+    Q = np.array(kat["Q"], dtype=np.float32)
+    m = _model(rl, P.shape[0], Q.shape[0], P.shape[1], 128)
+    m.set_weights(P, Q)
+    cand = np.array(kat["candidates"])
+    loader = [(torch.from_numpy(cand[s:s + 100, 0]), torch.from_numpy(cand[s:s + 100, 1]),
+               torch.from_numpy(cand[s:s + 100, 1])) for s in range(0, len(cand), 100)]
+    hr, ndcg = rl.metrics.metric_eval(m, loader, kat["k"])
+    assert hr == pytest.approx(kat["hr"], abs=1e-12)
+    assert ndcg == pytest.approx(kat["ndcg"], abs=1e-12)
+
+
+# ---------------------------------------------------------------------------------------------
+# edge cases
+# ---------------------------------------------------------------------------------------------
+def test_edge_cases(rl):
+    m = _model(rl, 5, 6, 8, 4)
+    P0, Q0 = m.get_weights()
+    st = m.train_triplets([], [], [])  # empty batch: no step
+    assert st["steps"] == 0 and m.steps_taken == 0
+    st = m.train_triplets([1, 2], [3, 3], [3, 4])  # smaller than batch_size: one partial step
+    assert st["steps"] == 1
+    with pytest.raises(ValueError):
+        m.train_triplets([5], [0], [1])  # user out of range
+    with pytest.raises(ValueError):
+        m.train_triplets([0], [0], [6])  # item out of range
+    with pytest.raises(ValueError):
+        m.fit(None)
+    full = rl.BPRMF(2, 3, 4)
+    with pytest.raises(ValueError):  # user 0 has every item: the reference would loop forever
+        full.fit([[0, 0], [0, 1], [0, 2], [1, 0]], epochs=1)
+
+
+def test_fit_and_epochs_reduce_loss(rl, golden):
+    pos, U, I = _ml100k_pos(golden)
+    m = _model(rl, U, I, 32, 4096, seed=3)
+    m.fit(pos, epochs=5)
+    losses = [h["loss"] for h in m.history]
+    n, s = m.epoch_size()
+    assert all(h["triplets"] == n and h["steps"] == s for h in m.history)
+    assert losses[-1] < losses[0]
+    P, Q = m.get_weights()
+    assert np.isfinite(P).all() and np.isfinite(Q).all()
+
+
+def test_hr_ndcg_parity_ml100k(rl):
+    """F5: HR@10 / NDCG@10 after the reference protocol (fo/tfo, d=32, B=4096, 20 epochs) with the
+    device sampler, on the reference's own split and candidates, within the reference's spread over
+    training seeds (mean +- 4 std)."""
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        ref = json.load(fh)
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    p = ref["protocol"]
+    gt = {int(u): set(f["gt_items"][f["gt_ptr"][k]:f["gt_ptr"][k + 1]].tolist())
+          for k, u in enumerate(f["gt_users"])}
+    m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
+                 batch_size=p["batch_size"], num_ng=p["num_ng"], seed=11)
+    m.fit(f["positives"].astype(np.int64), epochs=p["epochs"])
+    kpi = rl.metrics.evaluate_topk(m, f["test_data"], gt, p["topk"])
+    for k in ("hr", "ndcg"):
+        mu, sd = ref["summary"][k]["mean"], ref["summary"][k]["std"]
+        assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)
+
+
+# ---------------------------------------------------------------------------------------------
+# full-size properties (ml-20m shape)
+# ---------------------------------------------------------------------------------------------
+def _synthetic(U, I, npos, seed):
+    from importlib import import_module
+    syn = import_module("recommend-lib_amd.synthetic")
+    return syn.make_positives(U, I, npos, seed)
+
+
+def test_ml20m_shape_properties(rl):
+    U, I = 138493, 26744
+    pos = _synthetic(U, I, 10_000_000, 20261015)
+    m = rl.BPRMF(U, I, 128, batch_size=4096, seed=9)
+    m.set_train(pos)
+    N, S = m.epoch_size()
+    assert N == 4 * len(pos)
+    # sampler: bit-exact vs the C oracle on slices at both ends; never a positive
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    for first in (0, N - 200_000):
+        got = m.sample(0, first, 200_000)
+        want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 9, 0, first, 200_000)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+        u, j = got[0].astype(np.int64), got[2].astype(np.int64)
+        lo, hi = indptr[u], indptr[u + 1]
+        hit = np.array([j[t] in indices[lo[t]:hi[t]] for t in range(0, len(u), 97)])
+        assert not hit.any()
+    # 2000 steps of training: loss drops, weights stay finite
+    s1 = m.train_steps(0, 0, 1000)
+    s2 = m.train_steps(0, 1000, 1000)
+    assert s1["steps"] == 1000 and s2["triplets"] == 1000 * 4096
+    assert s2["loss"] < s1["loss"]
+    P, Q = m.get_weights()
+    assert np.isfinite(P).all() and np.isfinite(Q).all()

@@ -1,0 +1,164 @@
+"""CPU: the oracle is pinned against the reference's own outputs (tests/golden, made by importing
+the reference in the build container: tests/golden/make_golden.py) before anything trusts it."""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy import stats
+
+from conftest import GOLDEN
+from oracle import bpr_oracle as O
+from oracle import c_oracle as C
+
+# Tolerance of the fp32 restatement vs torch (different summation order / fused ops only).
+ORACLE_ATOL = 5e-8
+
+
+def test_dense_step_matches_reference_tiny(golden):
+    f = golden("bpr_step_tiny.npz")
+    P, Q = f["P0"].copy(), f["Q0"].copy()
+    for b in range(f["triplets"].shape[0]):
+        t = f["triplets"][b]
+        loss = O.bpr_step_dense(P, Q, t[0], t[1], t[2], float(f["lr"]), float(f["wd"]))
+        np.testing.assert_allclose(P, f["P"][b], rtol=0, atol=ORACLE_ATOL)
+        np.testing.assert_allclose(Q, f["Q"][b], rtol=0, atol=ORACLE_ATOL)
+        assert abs(loss - f["loss"][b]) <= 1e-5 * abs(f["loss"][b])
+
+
+def test_dense_step_matches_reference_ml100k_epoch(golden):
+    f = golden("bpr_ml100k_replay.npz")
+    tr = f["triplets"].astype(np.int64)
+    bd = f["batch_bounds"]
+    P, Q = f["P0"].copy(), f["Q0"].copy()
+    losses = O.train_replay(P, Q, tr, bd, float(f["lr"]), float(f["wd"]))
+    np.testing.assert_allclose(P, f["P_epoch"], rtol=0, atol=ORACLE_ATOL)
+    np.testing.assert_allclose(Q, f["Q_epoch"], rtol=0, atol=ORACLE_ATOL)
+    np.testing.assert_allclose(losses, f["loss"], rtol=1e-5)
+
+
+def test_c_dense_step_matches_reference(golden):
+    f = golden("bpr_ml100k_replay.npz")
+    tr = f["triplets"].astype(np.int32)
+    bd = f["batch_bounds"]
+    D = C.DenseTrainer(f["P0"], f["Q0"], f["lr"], f["wd"])
+    for b in range(10):
+        D.step(tr[0, bd[b]:bd[b + 1]], tr[1, bd[b]:bd[b + 1]], tr[2, bd[b]:bd[b + 1]])
+    np.testing.assert_allclose(D.P, f["P10"], rtol=0, atol=ORACLE_ATOL)
+    np.testing.assert_allclose(D.Q, f["Q10"], rtol=0, atol=ORACLE_ATOL)
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors, philox4x32 10 rounds
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = O.philox4x32_10(*ctr, *key)
+        assert tuple(int(x) for x in got) == want
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 16, 17, 63, 64, 65, 1000, 4097, 100003])
+def test_permutation_is_bijection(n):
+    q = O.permute(np.arange(n), n, 987654321, 7)
+    assert np.array_equal(np.sort(q), np.arange(n))
+    for s in (0, n // 2, n - 1):
+        assert C.lib().oracle_permute(s, n, 987654321, 7) == q[s]
+
+
+def test_kth_nonmember_bruteforce():
+    g = np.random.default_rng(3)
+    I = 50
+    users, items = [], []
+    for u in range(20):
+        deg = int(g.integers(0, 49))
+        for i in g.choice(I, deg, replace=False):
+            users.append(u)
+            items.append(int(i))
+    indptr, indices = O.build_csr(np.array(users), np.array(items), 20)
+    for u in range(20):
+        pos = set(indices[indptr[u]:indptr[u + 1]].tolist())
+        free = [x for x in range(I) if x not in pos]
+        ks = np.arange(len(free))
+        got = O.kth_nonmember(indptr, indices, np.full(len(ks), u), ks)
+        assert got.tolist() == free
+
+
+def test_sampler_numpy_and_c_restatements_agree(golden):
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    U, I = int(f["U"]), int(f["I"])
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    N = len(pos) * 4
+    for epoch, first, cnt in ((0, 0, N), (5, 1234, 5000), (2**31 + 3, N - 777, 777)):
+        a = O.sample_triplets(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 0xDEADBEEF12345, epoch, first, cnt)
+        b = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 0xDEADBEEF12345, epoch, first, cnt)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+def _expected_neg_hist(pos, U, I, num_ng):
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    npos_u = np.bincount(pos[:, 0], minlength=U).astype(np.float64)
+    deg = np.diff(indptr).astype(np.float64)
+    c = np.where(deg < I, num_ng * npos_u / np.maximum(I - deg, 1), 0.0)
+    E = np.full(I, c.sum())
+    np.subtract.at(E, indices, np.repeat(c, np.diff(indptr)))
+    return E
+
+
+def _chi2_p(obs, E):
+    m = E > 0
+    chi = ((obs[m] - E[m]) ** 2 / E[m]).sum()
+    return stats.chi2.sf(chi, m.sum() - 1)
+
+
+def test_sampler_distribution_matches_reference_ng_sample(golden):
+    """F3: the reference's ng_sample histogram and ours are both consistent with the exact
+    'uniform over non-positives' distribution (util/data_loader.py:684-689)."""
+    f3 = golden("ng_sample_ml100k.npz")
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    U, I, ng = int(f3["U"]), int(f3["I"]), int(f3["num_ng"])
+    E = _expected_neg_hist(pos, U, I, ng)
+    assert int(f3["negatives_in_train"]) == 0
+    p_ref = _chi2_p(f3["hist_j"].astype(np.float64), E)
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    u, i, j = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, ng, 42, 0, 0, len(pos) * ng)
+    p_ours = _chi2_p(np.bincount(j, minlength=I).astype(np.float64), E)
+    assert p_ref > 1e-4, p_ref
+    assert p_ours > 1e-4, p_ours
+    # per-user negative counts are exactly num_ng x positives, as in the reference
+    assert np.array_equal(np.bincount(u, minlength=U), f3["neg_per_user"])
+    keys = set(map(tuple, pos.tolist()))
+    assert not any((int(a), int(b)) in keys for a, b in zip(u, j))
+
+
+def test_metrics_known_answers(rl):
+    with open(os.path.join(GOLDEN, "metrics_kat.json")) as fh:
+        kat = json.load(fh)
+    M = rl.metrics
+    K = kat["k"]
+    for c in kat["cases"]:
+        r = c["r"]
+        assert M.precision_at_k(r, K) == pytest.approx(c["precision"], abs=1e-12)
+        assert M.recall_at_k(r, c["gt_len"], K) == pytest.approx(c["recall"], abs=1e-12)
+        assert M.ndcg_at_k(r, K) == pytest.approx(c["ndcg"], abs=1e-12)
+        assert M.average_precision(r[:K]) == pytest.approx(c["ap"], abs=1e-12)
+    rs = [c["r"][:K] for c in kat["cases"]]
+    us = list(range(len(rs)))
+    ur = {u: set(range(d)) for u, d in zip(us, kat["aggregate"]["hr_denoms"])}
+    assert M.map_at_k(rs) == pytest.approx(kat["aggregate"]["map"], abs=1e-12)
+    assert M.mrr_at_k(rs) == pytest.approx(kat["aggregate"]["mrr"], abs=1e-12)
+    assert M.hr_at_k(rs, us, ur) == pytest.approx(kat["aggregate"]["hr"], abs=1e-12)
+
+
+def test_hr_ndcg_fixture_is_consistent():
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        j = json.load(fh)
+    s = j["summary"]
+    assert len(j["runs"]) >= 3
+    assert 0 < s["hr"]["mean"] < 1 and s["hr"]["std"] < 0.2 * s["hr"]["mean"]
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    assert f["test_data"].shape[1] == 2 and len(f["gt_users"]) == len(f["gt_ptr"]) - 1

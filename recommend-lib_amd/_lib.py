@@ -88,6 +88,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    # torch links its bundled HIP runtime as "libamdhip64.so" (SONAME libamdhip64.so.7); loading
+    # torch first lets our NEEDED libamdhip64.so.7 resolve to that same copy.  Loading ours first
+    # would bring in a second HIP runtime and torch would then see no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
         f = getattr(L, name)

@@ -56,6 +56,11 @@ struct bprmf_handle {
   uint32_t k0 = 0, k1 = 0;  // shard sampler key
   // triplet chunk
   int32_t* d_trip = nullptr;  // [3, cap]
+  // segmented step (batch_size <= kMaxSegBatch): per-batch sorted layouts + per-triplet c*P_u
+  int32_t* d_batch = nullptr;  // batch_cap * BatchBuf::stride_for(B) int32
+  int64_t batch_cap = 0;
+  float* d_contrib = nullptr;  // [B, ld]
+  int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
   int64_t trip_cap = 0;
   // misc device scalars
   double* d_loss = nullptr;
@@ -197,7 +202,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.G, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
-  TRY(dalloc(&h->d_loss, 1));
+  TRY(dalloc(&h->d_loss, kLossSlots));
   TRY(dalloc(&h->d_err, 1));
   h->P.rows = h->U;
   h->Q.rows = h->I;
@@ -230,7 +235,8 @@ int bprmf_destroy(bprmf_handle* h) {
   hipSetDevice(h->cfg.device);
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
-                  h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err};
+                  h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err,
+                  h->d_batch, h->d_contrib, h->d_tbase};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
@@ -362,9 +368,21 @@ static SamplerArgs sampler_args(bprmf_handle* h) {
   return a;
 }
 
+// sum of the per-wave loss slots (copied back once per call)
+static int read_loss(bprmf_handle* h, double* loss) {
+  std::vector<double> slots(kLossSlots);
+  HIPCHK(hipMemcpyAsync(slots.data(), h->d_loss, sizeof(double) * kLossSlots, hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  double s = 0;
+  for (double v : slots) s += v;
+  *loss = s;
+  return 0;
+}
+
 static int begin_call(bprmf_handle* h) {
   if (int r = set_dev(h)) return r;
-  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double), h->stream));
+  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   return 0;
 }
@@ -372,9 +390,8 @@ static int begin_call(bprmf_handle* h) {
 static int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   double loss = 0;
-  HIPCHK(hipMemcpyAsync(&loss, h->d_loss, sizeof loss, hipMemcpyDeviceToHost, h->stream));
+  if (int r = read_loss(h, &loss)) return r;
   HIPCHK(hipEventSynchronize(h->ev1));
-  HIPCHK(hipStreamSynchronize(h->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
   if (int r = check_err_flag(h)) return r;
@@ -388,6 +405,74 @@ static int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
 }
 
 // run steps over device triplets tu/ti/tj[0..n) in batches of B
+static bool seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSegBatch; }
+
+static int ensure_seg(bprmf_handle* h, int64_t n_batches) {
+  const int64_t B = h->cfg.batch_size;
+  if (!h->d_contrib) {
+    if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
+    if (int r = dalloc(&h->d_tbase, 1)) return r;
+  }
+  if (n_batches <= h->batch_cap) return 0;
+  if (h->d_batch) HIPCHK(hipFree(h->d_batch));
+  h->d_batch = nullptr;
+  h->batch_cap = 0;
+  if (int r = dalloc(&h->d_batch, n_batches * BatchBuf::stride_for((int)B))) return r;
+  h->batch_cap = n_batches;
+  return 0;
+}
+
+static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
+                     int64_t n, int64_t* steps_done);
+
+// One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler
+// (ru == nullptr) or replayed device ids ru/ri/rj[0..n).  Segmented path for B <= kMaxSegBatch:
+// one build launch for the chunk, then two launches per step; otherwise the atomic path.
+static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_t n,
+                     const int32_t* ru, const int32_t* ri, const int32_t* rj, int64_t* steps_done) {
+  if (n <= 0) return 0;
+  const int64_t B = h->cfg.batch_size;
+  const int64_t nb = (n + B - 1) / B;
+  if ((int64_t)h->t + nb >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  if (!seg_mode(h)) {
+    if (!ru) {
+      if (int r = ensure_trip(h, n)) return r;
+      int32_t* tu = h->d_trip;
+      int32_t* ti = tu + h->trip_cap;
+      int32_t* tj = ti + h->trip_cap;
+      {
+        ProfScope ps(h, BPRMF_KPROF_SAMPLE);
+        HIPCHK(sample(sampler_args(h), epoch, first_slot, n, tu, ti, tj, h->d_err, h->stream));
+      }
+      return run_steps(h, tu, ti, tj, n, steps_done);
+    }
+    return run_steps(h, ru, ri, rj, n, steps_done);
+  }
+  if (int r = ensure_seg(h, nb)) return r;
+  BatchBuf bb{h->d_batch, (int)B};
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
+  {
+    ProfScope ps(h, BPRMF_KPROF_SAMPLE);
+    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U, h->I, bb,
+                         h->d_err, h->stream));
+  }
+  for (int64_t k = 0; k < nb; ++k) {
+    const BatchView v = bb.view(k);
+    {
+      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
+      HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
+                       h->d_contrib, h->stream));
+    }
+    {
+      ProfScope ps(h, BPRMF_KPROF_APPLY);
+      HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->stream));
+    }
+  }
+  h->t += (int32_t)nb;
+  *steps_done += nb;
+  return 0;
+}
+
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done) {
   const int64_t B = h->cfg.batch_size;
@@ -424,21 +509,11 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   const int64_t B = h->cfg.batch_size;
   const int64_t chunk = chunk_triplets(h);
   const int64_t beg = first_step * B, end = std::min(N, (first_step + n_steps) * B);
-  if (int r = ensure_trip(h, std::min(chunk, std::max<int64_t>(end - beg, 1)))) return r;
   if (int r = begin_call(h)) return r;
-  const SamplerArgs sa = sampler_args(h);
   int64_t steps = 0;
-  for (int64_t off = beg; off < end; off += chunk) {
-    const int64_t n = std::min(chunk, end - off);
-    int32_t* tu = h->d_trip;
-    int32_t* ti = tu + h->trip_cap;
-    int32_t* tj = ti + h->trip_cap;
-    {
-      ProfScope ps(h, BPRMF_KPROF_SAMPLE);
-      HIPCHK(sample(sa, epoch, off, n, tu, ti, tj, h->d_err, h->stream));
-    }
-    if (int r = run_steps(h, tu, ti, tj, n, &steps)) return r;
-  }
+  for (int64_t off = beg; off < end; off += chunk)
+    if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps))
+      return r;
   return end_call(h, st, end - beg, steps);
 }
 
@@ -454,8 +529,12 @@ int bprmf_train_triplets_dev(bprmf_handle* h, const int32_t* u, const int32_t* i
   if (!h || n < 0 || (n > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
   if (h->cfg.world != 1) return fail(BPRMF_E_STATE, "sharded handle: use the bprmf_dist_* phases");
   if (int r = begin_call(h)) return r;
+  const int64_t chunk = chunk_triplets(h);
   int64_t steps = 0;
-  if (int r = run_steps(h, u, i, j, n, &steps)) return r;
+  for (int64_t off = 0; off < n; off += chunk) {
+    const int64_t m = std::min(chunk, n - off);
+    if (int r = run_chunk(h, 0, 0, m, u + off, i + off, j + off, &steps)) return r;
+  }
   return end_call(h, st, n, steps);
 }
 
@@ -472,20 +551,19 @@ int bprmf_train_triplets(bprmf_handle* h, const int32_t* u, const int32_t* i, co
                   (long long)h->cfg.item_num);
   }
   if (int r = set_dev(h)) return r;
-  const int64_t B = h->cfg.batch_size;
-  const int64_t chunk = std::max<int64_t>(B, (chunk_triplets(h) / B) * B);
+  const int64_t chunk = chunk_triplets(h);  // whole batches
   if (int r = ensure_trip(h, std::min(chunk, std::max<int64_t>(n, 1)))) return r;
   if (int r = begin_call(h)) return r;
   int64_t steps = 0;
-  for (int64_t off = 0; off < n; off += h->trip_cap) {
-    const int64_t m = std::min(h->trip_cap, n - off);
+  for (int64_t off = 0; off < n; off += chunk) {
+    const int64_t m = std::min(chunk, n - off);
     int32_t* tu = h->d_trip;
     int32_t* ti = tu + h->trip_cap;
     int32_t* tj = ti + h->trip_cap;
     HIPCHK(hipMemcpyAsync(tu, u + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(ti, i + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(tj, j + off, 4 * m, hipMemcpyHostToDevice, h->stream));
-    if (int r = run_steps(h, tu, ti, tj, m, &steps)) return r;
+    if (int r = run_chunk(h, 0, 0, m, tu, ti, tj, &steps)) return r;
     HIPCHK(hipStreamSynchronize(h->stream));  // host buffers reused by the next chunk's copies
   }
   return end_call(h, st, n, steps);
@@ -622,7 +700,7 @@ int bprmf_dist_begin_step(bprmf_handle* h) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   if (int r = set_dev(h)) return r;
-  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double), h->stream));
+  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
   return 0;
 }
 
@@ -664,8 +742,7 @@ int bprmf_dist_end_step(bprmf_handle* h, double* loss) {
   if (int r = set_dev(h)) return r;
   h->t += 1;
   if (loss) {
-    HIPCHK(hipMemcpyAsync(loss, h->d_loss, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (int r = read_loss(h, loss)) return r;
     return check_err_flag(h);
   }
   return 0;

@@ -1,0 +1,148 @@
+// device_common.h — device helpers shared by kernels.hip and segment.hip (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace bprmf {
+
+constexpr uint32_t TAG_NEG = 0x4E470000u;
+constexpr uint32_t TAG_PERM = 0x50520000u;
+constexpr uint32_t TAG_INIT = 0x494E0000u;
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = kMaxGridBlocks;  // 256 CUs x 8 resident 256-thread blocks, grid-stride beyond
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based; Salmon et al. SC'11).  Stateless: every triplet / element draws
+// from its own counter, so the sampler is embarrassingly parallel and bit-reproducible.
+// ------------------------------------------------------------------------------------------------
+static __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
+                                         uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// keyed bijection of [0, n): balanced Feistel on 2h bits, cycle-walking back into range.
+static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int h, uint32_t k0, uint32_t k1,
+                                            uint32_t epoch) {
+  const uint64_t mask = (h >= 32) ? 0xFFFFFFFFull : ((1ull << h) - 1);
+  do {
+    uint64_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (uint32_t r = 0; r < 6; ++r) {
+      uint32_t c0 = (uint32_t)R, c1 = r, c2 = epoch, c3 = TAG_PERM | r;
+      philox10(c0, c1, c2, c3, k0, k1);
+      const uint64_t nl = R;
+      R = L ^ ((uint64_t)c0 & mask);
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
+// unbiased Lemire reduction into [0, n), n >= 1; retries draw fresh counters (attempt in tag).
+static __device__ __forceinline__ uint32_t bounded(uint64_t q, uint32_t epoch, uint32_t n, uint32_t k0,
+                                            uint32_t k1) {
+  const uint32_t thresh = (uint32_t)((0x100000000ull - n) % n);
+  for (uint32_t a = 0;; ++a) {
+    uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = epoch, c3 = TAG_NEG | a;
+    philox10(c0, c1, c2, c3, k0, k1);
+    const uint64_t m = (uint64_t)c0 * n;
+    if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
+  }
+}
+
+// j = the k-th item id NOT in the sorted positive list a[0..n): m = #{x : a[x]-x <= k}, j = k+m.
+static __device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restrict__ a, int64_t n, int64_t k) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)a[mid] - mid <= k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return k + lo;
+}
+
+// (1 - lr*wd)^k in double by squaring (deterministic IEEE order), rounded once to fp32.
+static __device__ __forceinline__ float decay_pow(double alpha, int32_t k) {
+  if (k <= 0) return 1.0f;
+  double r = 1.0, b = alpha;
+  while (k) {
+    if (k & 1) r *= b;
+    b *= b;
+    k >>= 1;
+  }
+  return (float)r;
+}
+
+static __device__ __forceinline__ float softplus(float z) {  // log(1 + e^z), overflow-free
+  return fmaxf(z, 0.f) + log1pf(expf(-fabsf(z)));
+}
+
+template <int G>
+static __device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// sum over the wave of per-lane loss partials into this wave's own f64 slot (plain RMW: a slot
+// belongs to one wave per launch and launches are stream-ordered).  No same-address atomics: one
+// f64 atomic per wave into a single word serialises at ~13 ns each (4096 waves = 53 us).
+static __device__ __forceinline__ void wave_add_loss(double* slots, float v) {
+  if (!slots) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) slots[blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)] += (double)v;
+}
+
+static inline unsigned grid_for(int64_t units, int G) {
+  const int64_t per_block = kBlock / G;
+  int64_t b = (units + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > kMaxBlocks) b = kMaxBlocks;
+  return (unsigned)b;
+}
+static inline unsigned grid_flat(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > 4 * kMaxBlocks) b = 4 * kMaxBlocks;
+  return (unsigned)b;
+}
+
+// Expand `BODY` for every instantiated (G, EPL) geometry.
+#define BPRMF_DISPATCH(geom, BODY)                                  \
+  switch ((geom).G * 100 + (geom).EPL) {                            \
+    case 401: { constexpr int G_ = 4, E_ = 1; BODY; } break;        \
+    case 801: { constexpr int G_ = 8, E_ = 1; BODY; } break;        \
+    case 1601: { constexpr int G_ = 16, E_ = 1; BODY; } break;      \
+    case 3201: { constexpr int G_ = 32, E_ = 1; BODY; } break;      \
+    case 6401: { constexpr int G_ = 64, E_ = 1; BODY; } break;      \
+    case 6402: { constexpr int G_ = 64, E_ = 2; BODY; } break;      \
+    case 6403: { constexpr int G_ = 64, E_ = 3; BODY; } break;      \
+    case 6404: { constexpr int G_ = 64, E_ = 4; BODY; } break;      \
+    case 6405: { constexpr int G_ = 64, E_ = 5; BODY; } break;      \
+    case 6406: { constexpr int G_ = 64, E_ = 6; BODY; } break;      \
+    case 6407: { constexpr int G_ = 64, E_ = 7; BODY; } break;      \
+    case 6408: { constexpr int G_ = 64, E_ = 8; BODY; } break;      \
+    case 6412: { constexpr int G_ = 64, E_ = 12; BODY; } break;     \
+    case 6416: { constexpr int G_ = 64, E_ = 16; BODY; } break;     \
+    default: return hipErrorInvalidValue;                           \
+  }
+
+}  // namespace bprmf

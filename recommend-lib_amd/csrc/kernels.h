@@ -9,6 +9,10 @@ namespace bprmf {
 // Row geometry: a row of D floats is stored with stride ld = G*EPL (zero padded); a group of G
 // lanes owns one row, lane `sub` holds elements sub + G*k, k < EPL.  D <= 64: G = next_pow2(D),
 // EPL = 1 (64/G rows per wave); D > 64: G = 64 (one row per wave), EPL = ceil(D/64).
+// per-wave loss partial slots of the step kernels: grid <= kMaxGridBlocks blocks of 4 waves
+constexpr int kMaxGridBlocks = 256 * 8;
+constexpr int kLossSlots = kMaxGridBlocks * 4;
+
 struct Geom {
   int D, G, EPL, ld;
 };
@@ -21,6 +25,41 @@ struct Table {
   int32_t* stamp;  // [rows] step at which W[row] is current (lazy dense weight decay)
   int64_t rows;
 };
+
+// One batch of a step, as laid out by k_build_batches (int32, positions within the batch).  Every
+// step kernel reaches its rows after ONE dependent load of a 32-byte record:
+//   ij    [B][2]    (i, j) item rows of the triplets, sorted by (local) user row
+//   urec  [B][8]    user segment s: {u, beg, end, i_beg, j_beg, 0, 0, 0}      (meta[1] of them)
+//   irec  [2B][8]   item segment s: {item, beg, end, ref0..ref3, long}        (meta[2] of them)
+//   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
+//                   sorted by item then position (fixed summation order)
+//   ilong [2B]      indices of item segments with > kLongSeg references      (meta[3] of them)
+//   useg  [B+1], ioff [2B+1]   builder scratch (segment starts)
+//   meta  [4]       {triplets, user segments, item segments, long item segments}
+constexpr int kRec = 8;
+constexpr int kLongSeg = 16;
+struct BatchView {
+  int32_t *ij, *urec, *irec, *refs, *ilong, *useg, *ioff, *meta;
+};
+struct BatchBuf {
+  int32_t* base;
+  int B;
+  __host__ __device__ static int64_t stride_for(int B) { return 33LL * B + 6; }
+  __host__ __device__ BatchView view(int64_t k) const {
+    int32_t* p = base + k * stride_for(B);
+    BatchView v;
+    v.ij = p;
+    v.urec = p + 2LL * B;
+    v.irec = p + 10LL * B;
+    v.refs = p + 26LL * B;
+    v.ilong = p + 28LL * B;
+    v.useg = p + 30LL * B;
+    v.ioff = p + 31LL * B + 1;
+    v.meta = p + 33LL * B + 2;
+    return v;
+  }
+};
+constexpr int kMaxSegBatch = 8192;  // largest batch the one-workgroup builder handles
 
 struct Hyper {
   float lr, wd;
@@ -48,6 +87,15 @@ hipError_t fwd_scatter(const Geom& g, const int32_t* tu, const int32_t* ti, cons
                        int32_t* err, hipStream_t s);
 hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                       int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, hipStream_t s);
+// segmented step: build `n_batches` batches of B (<= kMaxSegBatch) from the sampler (ru == null)
+// or from replayed ids; then per batch k: user_step (K1) and item_step (K2) with t = *tbase+k+1.
+hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
+                         int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
+                         int64_t u_rows, int64_t i_rows, BatchBuf bb, int32_t* err, hipStream_t s);
+hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s);
+hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, const float* contrib, hipStream_t s);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

@@ -1,0 +1,442 @@
+// segment.hip — the atomic-free, deterministic BPR-MF step for batches of <= kMaxSegBatch triplets.
+//
+// Per chunk of steps (off the per-step critical path, full-chip parallel):
+//   k_build_batches  one 1024-thread workgroup per batch: produce the batch's triplets (the device
+//                    sampler, bit-identical to k_sample, or replayed ids), sort them by user in LDS
+//                    (rocPRIM block radix sort), sort the batch's 2B item references by item, and
+//                    write 32-byte segment records so each step kernel needs ONE dependent load
+//                    before its row gathers.
+// Per step (two launches):
+//   k_user_step (K1) one lane group per user segment: gather P_u, Q_i, Q_j (pending decay applied),
+//                    x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x); accumulate the user's gradient in
+//                    registers; store c*P_u per triplet; write the updated user row and its stamp.
+//                    Every read of P_u in the step is inside the segment, so the in-place write is
+//                    race-free.
+//   k_item_step (K2) one lane group per distinct item (a whole workgroup for items with more than
+//                    kLongSeg references, reduced through LDS in a fixed order): sum -/+ c*P_u over
+//                    the item's references, W <- V - lr (g + wd V), V = W*(1-lr*wd)^pending.
+// No f32 atomics, results are bitwise reproducible run to run.
+// Reference semantics: BPRMFRecommender.py:172-176 (see kernels.hip header).
+#include <string.h>
+
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
+
+#include "device_common.h"
+
+namespace bprmf {
+
+constexpr int kBuildThreads = 1024;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+static __device__ __forceinline__ void store_rec(int32_t* rec, int a, int b, int c, int d, int e,
+                                                 int f, int g, int h) {
+  reinterpret_cast<int4*>(rec)[0] = make_int4(a, b, c, d);
+  reinterpret_cast<int4*>(rec)[1] = make_int4(e, f, g, h);
+}
+
+template <int IPT>
+__global__ __launch_bounds__(kBuildThreads) void k_build_batches(
+    SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
+    const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
+    int64_t u_rows, int64_t i_rows, int user_bits, int item_bits, BatchBuf bb,
+    int32_t* __restrict__ err) {
+  constexpr int T = kBuildThreads;
+  constexpr int IPT2 = 2 * IPT;
+  using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
+  using SortI = rocprim::block_radix_sort<uint32_t, T, IPT2, uint32_t>;
+  using Scan = rocprim::block_scan<int, T>;
+  union Smem {  // the sorted keys alias the sort storage (barrier after every sort)
+    typename SortU::storage_type su;
+    typename SortI::storage_type si;
+    uint32_t key[T * IPT2];
+  };
+  __shared__ Smem sm;
+  __shared__ typename Scan::storage_type sscan;
+  __shared__ int32_t s_i[T * IPT];
+  __shared__ int32_t s_j[T * IPT];
+  uint32_t* s_key = sm.key;
+
+  const int tid = threadIdx.x;
+  const int64_t batch = blockIdx.x;
+  const int64_t b0 = batch * (int64_t)B;
+  const int nb = (int)min<int64_t>(B, n_slots - b0);
+  const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
+  const BatchView v = bb.view(batch);
+
+  // 1. the batch's triplets in slot order, keyed by local user row
+  uint32_t key[IPT], val[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int p = tid * IPT + k;
+    key[k] = kNone;
+    val[k] = (uint32_t)p;
+    if (p < nb) {
+      int32_t u, i, j;
+      bool sampled_ok = true;
+      if (ru) {
+        u = ru[b0 + p];
+        i = ri[b0 + p];
+        j = rj[b0 + p];
+      } else {
+        const uint64_t q = permute((uint64_t)(first_slot + b0 + p), N, a.feistel_h, a.k0, a.k1, epoch);
+        const int64_t pp = (int64_t)(q / (uint64_t)a.num_ng);
+        const int64_t ul = a.pos_u[pp] / a.world;
+        i = a.pos_i[pp];
+        const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
+        const int64_t nfree = a.item_num - deg;
+        j = -1;
+        if (nfree > 0) {
+          const uint32_t kk = bounded(q, epoch, (uint32_t)nfree, a.k0, a.k1);
+          j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)kk);
+        } else {
+          sampled_ok = false;
+        }
+        u = (int32_t)ul;
+      }
+      if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
+          (uint64_t)j < (uint64_t)i_rows) {
+        key[k] = (uint32_t)u;
+        s_i[p] = i;
+        s_j[p] = j;
+      } else {
+        atomicOr(err, sampled_ok ? 1 : 2);
+      }
+    }
+  }
+  SortU().sort(key, val, sm.su, 0, user_bits);
+  __syncthreads();
+  // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
+  int32_t my_i[IPT], my_j[IPT];
+  int valid = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const bool ok = key[k] != kNone;
+    valid += ok;
+    my_i[k] = ok ? s_i[val[k]] : 0;
+    my_j[k] = ok ? s_j[val[k]] : 0;
+    s_key[tid * IPT + k] = key[k];
+  }
+  __syncthreads();  // slot-order reads of s_i/s_j done; s_key complete
+  int heads = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int p = tid * IPT + k;
+    s_i[p] = my_i[k];  // sorted order from here on
+    s_j[p] = my_j[k];
+    if (key[k] != kNone) {
+      heads += (p == 0 || s_key[p - 1] != key[k]);
+      reinterpret_cast<int2*>(v.ij)[p] = make_int2(my_i[k], my_j[k]);
+    }
+  }
+  int seg0 = 0, n_useg = 0, vpre = 0, nvalid = 0;
+  Scan().exclusive_scan(heads, seg0, 0, n_useg, sscan, rocprim::plus<int>());
+  __syncthreads();
+  Scan().exclusive_scan(valid, vpre, 0, nvalid, sscan, rocprim::plus<int>());
+  {
+    int s = seg0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
+      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) v.useg[s++] = p;
+    }
+  }
+  if (tid == 0) v.useg[n_useg] = nvalid;
+  __syncthreads();  // useg visible block-wide; s_i/s_j sorted; s_key free
+  {
+    int s = seg0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
+      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) {
+        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], s_i[p], s_j[p], 0, 0, 0);
+        ++s;
+      }
+    }
+  }
+  __syncthreads();  // s_key reads done before it is reused for the item keys
+
+  // 2. item references: r < nvalid -> i of sorted triplet r (sign -), else j of r - nvalid (sign +)
+  uint32_t ik[IPT2], iv[IPT2];
+#pragma unroll
+  for (int k = 0; k < IPT2; ++k) {
+    const int r = tid * IPT2 + k;
+    ik[k] = kNone;
+    iv[k] = 0;
+    if (r < 2 * nvalid) {
+      const int p = r < nvalid ? r : r - nvalid;
+      ik[k] = (uint32_t)(r < nvalid ? s_i[p] : s_j[p]);
+      iv[k] = ((uint32_t)p << 1) | (r < nvalid ? 0u : 1u);
+    }
+  }
+  SortI().sort(ik, iv, sm.si, 0, item_bits);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IPT2; ++k) s_key[tid * IPT2 + k] = ik[k];
+  __syncthreads();
+  int iheads = 0;
+#pragma unroll
+  for (int k = 0; k < IPT2; ++k) {
+    const int r = tid * IPT2 + k;
+    if (ik[k] != kNone) {
+      iheads += (r == 0 || s_key[r - 1] != ik[k]);
+      v.refs[r] = (int32_t)iv[k];
+    }
+  }
+  int iseg0 = 0, n_iseg = 0;
+  Scan().exclusive_scan(iheads, iseg0, 0, n_iseg, sscan, rocprim::plus<int>());
+  {
+    int s = iseg0;
+#pragma unroll
+    for (int k = 0; k < IPT2; ++k) {
+      const int r = tid * IPT2 + k;
+      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) v.ioff[s++] = r;
+    }
+  }
+  if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
+  __syncthreads();  // ioff and refs visible block-wide
+  int nlong_mine = 0;
+  {
+    int s = iseg0;
+#pragma unroll
+    for (int k = 0; k < IPT2; ++k) {
+      const int r = tid * IPT2 + k;
+      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
+        const int end = v.ioff[s + 1];
+        const int len = end - r;
+        const int lng = len > kLongSeg;
+        nlong_mine += lng;
+        store_rec(v.irec + (int64_t)s * kRec, (int)ik[k], r, end, v.refs[r],
+                  len > 1 ? v.refs[r + 1] : 0, len > 2 ? v.refs[r + 2] : 0,
+                  len > 3 ? v.refs[r + 3] : 0, lng);
+        ++s;
+      }
+    }
+  }
+  __syncthreads();
+  int lpre = 0, n_long = 0;
+  Scan().exclusive_scan(nlong_mine, lpre, 0, n_long, sscan, rocprim::plus<int>());
+  if (nlong_mine) {
+    int s = iseg0;
+#pragma unroll
+    for (int k = 0; k < IPT2; ++k) {
+      const int r = tid * IPT2 + k;
+      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
+        if (v.ioff[s + 1] - r > kLongSeg) v.ilong[lpre++] = s;
+        ++s;
+      }
+    }
+  }
+  if (tid == 0) {
+    v.meta[0] = nvalid;
+    v.meta[1] = n_useg;
+    v.meta[2] = n_iseg;
+    v.meta[3] = n_long;
+  }
+}
+
+// K1: user segments, one lane group each.  t = *tbase + step + 1.
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
+                                                      int ld, const int32_t* __restrict__ tbase,
+                                                      int step, double* loss,
+                                                      float* __restrict__ contrib) {
+  const int sub = threadIdx.x & (G - 1);
+  const int s = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  // independent loads: the record (allocated for every s < B), the segment count and the step
+  const int4 r0 = reinterpret_cast<const int4*>(bv.urec + (int64_t)s * kRec)[0];
+  const int r1x = bv.urec[(int64_t)s * kRec + 4];
+  const int n_useg = bv.meta[1];
+  const int32_t t = *tbase + step + 1;
+  float lsum = 0.f;
+  if (s < n_useg) {
+    const int32_t u = r0.x;
+    const int beg = r0.y, end = r0.z;
+    int32_t i = r0.w, j = r1x;
+    float* pw = P.W + (int64_t)u * ld + sub;
+    float pu[EPL], g[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      pu[k] = pw[G * k];
+      g[k] = 0.f;
+    }
+    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) pu[k] *= fu;
+    for (int p = beg; p < end; ++p) {
+      int2 nxt = make_int2(0, 0);
+      if (p + 1 < end) nxt = reinterpret_cast<const int2*>(bv.ij)[p + 1];
+      const float* qi = Q.W + (int64_t)i * ld + sub;
+      const float* qj = Q.W + (int64_t)j * ld + sub;
+      float vi[EPL], vj[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        vi[k] = qi[G * k];
+        vj[k] = qj[G * k];
+      }
+      const float fi = decay_pow(hp.alpha, t - 1 - Q.stamp[i]);
+      const float fj = decay_pow(hp.alpha, t - 1 - Q.stamp[j]);
+      float di = 0.f, dj = 0.f;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        vi[k] *= fi;
+        vj[k] *= fj;
+        di = fmaf(pu[k], vi[k], di);
+        dj = fmaf(pu[k], vj[k], dj);
+      }
+      di = group_sum<G>(di);
+      dj = group_sum<G>(dj);
+      const float x = di - dj;
+      const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
+      if (sub == 0) lsum += softplus(-x);
+      float* cb = contrib + (int64_t)p * ld + sub;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        g[k] = fmaf(-c, vi[k] - vj[k], g[k]);
+        cb[G * k] = c * pu[k];
+      }
+      i = nxt.x;
+      j = nxt.y;
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) pw[G * k] = fmaf(-hp.lr, fmaf(hp.wd, pu[k], g[k]), pu[k]);
+    if (sub == 0) P.stamp[u] = t;
+  }
+  wave_add_loss(loss, lsum);
+}
+
+template <int G, int EPL>
+static __device__ __forceinline__ void add_ref(float (&g)[EPL], const float* __restrict__ contrib,
+                                               int32_t ref, int ld, int sub) {
+  const float sgn = (ref & 1) ? 1.f : -1.f;
+  const float* cb = contrib + (int64_t)(ref >> 1) * ld + sub;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) g[k] = fmaf(sgn, cb[G * k], g[k]);
+}
+
+template <int G, int EPL>
+static __device__ __forceinline__ void apply_item(Table Q, int32_t item, const float (&g)[EPL],
+                                                  const Hyper& hp, int ld, int32_t t, int sub) {
+  float* w = Q.W + (int64_t)item * ld + sub;
+  float x[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) x[k] = w[G * k];
+  const float f = decay_pow(hp.alpha, t - 1 - Q.stamp[item]);
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const float vv = x[k] * f;
+    w[G * k] = fmaf(-hp.lr, fmaf(hp.wd, vv, g[k]), vv);
+  }
+  if (sub == 0) Q.stamp[item] = t;
+}
+
+// K2: blocks [0, long_blocks) take one long item segment each (all groups, LDS reduction in group
+// order); the rest take short segments, one lane group each.
+template <int G, int EPL>
+__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyper hp, int ld,
+                                                      const int32_t* __restrict__ tbase, int step,
+                                                      const float* __restrict__ contrib,
+                                                      int long_blocks) {
+  constexpr int NG = kBlock / G;
+  const int sub = threadIdx.x & (G - 1);
+  const int grp = threadIdx.x / G;
+  const int32_t t = *tbase + step + 1;
+  if ((int)blockIdx.x < long_blocks) {
+    __shared__ float part[NG][G * EPL];
+    const int n_long = bv.meta[3];
+    if ((int)blockIdx.x >= n_long) return;  // uniform over the block
+    const int s = bv.ilong[blockIdx.x];
+    const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
+    const int32_t item = r0.x;
+    const int beg = r0.y, end = r0.z;
+    float g[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) g[k] = 0.f;
+    int r = beg + grp;
+    for (; r + 3 * NG < end; r += 4 * NG) {  // 4 independent row loads in flight per group
+      const int32_t a0 = bv.refs[r], a1 = bv.refs[r + NG], a2 = bv.refs[r + 2 * NG],
+                    a3 = bv.refs[r + 3 * NG];
+      add_ref<G, EPL>(g, contrib, a0, ld, sub);
+      add_ref<G, EPL>(g, contrib, a1, ld, sub);
+      add_ref<G, EPL>(g, contrib, a2, ld, sub);
+      add_ref<G, EPL>(g, contrib, a3, ld, sub);
+    }
+    for (; r < end; r += NG) add_ref<G, EPL>(g, contrib, bv.refs[r], ld, sub);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) part[grp][sub + G * k] = g[k];
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        float acc = part[0][sub + G * k];
+#pragma unroll
+        for (int q = 1; q < NG; ++q) acc += part[q][sub + G * k];
+        g[k] = acc;
+      }
+      apply_item<G, EPL>(Q, item, g, hp, ld, t, sub);
+    }
+    return;
+  }
+  const int s = (blockIdx.x - long_blocks) * NG + grp;
+  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
+  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
+  const int n_iseg = bv.meta[2];
+  if (s >= n_iseg || r1.w) return;  // past the batch's items, or a long segment
+  const int32_t item = r0.x;
+  const int beg = r0.y, end = r0.z, len = end - beg;
+  float g[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) g[k] = 0.f;
+  add_ref<G, EPL>(g, contrib, r0.w, ld, sub);
+  if (len > 1) add_ref<G, EPL>(g, contrib, r1.x, ld, sub);
+  if (len > 2) add_ref<G, EPL>(g, contrib, r1.y, ld, sub);
+  if (len > 3) add_ref<G, EPL>(g, contrib, r1.z, ld, sub);
+  for (int r = beg + 4; r < end; ++r) add_ref<G, EPL>(g, contrib, bv.refs[r], ld, sub);
+  apply_item<G, EPL>(Q, item, g, hp, ld, t, sub);
+}
+
+// ------------------------------------------------------------------------------------------------
+static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
+  int b = 1;
+  while (b < 32 && (1LL << b) < n) ++b;
+  return b;
+}
+
+hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
+                         int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
+                         int64_t u_rows, int64_t i_rows, BatchBuf bb, int32_t* err, hipStream_t s) {
+  if (n_slots <= 0) return hipSuccess;
+  if (B <= 0 || B > kMaxSegBatch) return hipErrorInvalidValue;
+  const unsigned nb = (unsigned)((n_slots + B - 1) / B);
+  const int ub = bits_for(u_rows), ib = bits_for(i_rows);
+  if (B <= kBuildThreads * 4)
+    k_build_batches<4><<<nb, kBuildThreads, 0, s>>>(a, epoch, first_slot, n_slots, B, ru, ri, rj,
+                                                     u_rows, i_rows, ub, ib, bb, err);
+  else
+    k_build_batches<8><<<nb, kBuildThreads, 0, s>>>(a, epoch, first_slot, n_slots, B, ru, ri, rj,
+                                                     u_rows, i_rows, ub, ib, bb, err);
+  return hipGetLastError();
+}
+
+hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s) {
+  BPRMF_DISPATCH(g, ({
+    const unsigned blocks = (unsigned)((B + kBlock / G_ - 1) / (kBlock / G_));
+    k_user_step<G_, E_><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss, contrib);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, const float* contrib, hipStream_t s) {
+  const int long_blocks = (2 * B) / (kLongSeg + 1);
+  BPRMF_DISPATCH(g, ({
+    const unsigned blocks =
+        (unsigned)(long_blocks + (2LL * B + kBlock / G_ - 1) / (kBlock / G_));
+    k_item_step<G_, E_><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
+                                                  long_blocks);
+  }));
+  return hipGetLastError();
+}
+
+}  // namespace bprmf

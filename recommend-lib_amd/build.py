@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libbprmf_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "capi.cpp")]
+SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "capi.cpp")]
 HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h")] + [os.path.join(ROOT, "include", "bprmf.h")]
 ARCH = os.environ.get("BPRMF_OFFLOAD_ARCH", "gfx950")
 

@@ -170,6 +170,11 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   h->hp.lr = cfg->lr;
   h->hp.wd = cfg->weight_decay;
   h->hp.alpha = 1.0 - (double)cfg->lr * (double)cfg->weight_decay;
+  if (!(h->hp.alpha > 0.0)) {
+    delete h;
+    return fail(BPRMF_E_INVALID, "lr * weight_decay must be < 1 (weight decay would flip signs)");
+  }
+  h->hp.log2a = std::log2(h->hp.alpha);
   const int64_t W = cfg->world, R = cfg->rank;
   h->U = (cfg->user_num - R + W - 1) / W;
   h->I = (cfg->item_num - R + W - 1) / W;

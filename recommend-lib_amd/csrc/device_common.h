@@ -79,15 +79,12 @@ static __device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restric
 }
 
 // (1 - lr*wd)^k in double by squaring (deterministic IEEE order), rounded once to fp32.
-static __device__ __forceinline__ float decay_pow(double alpha, int32_t k) {
+// (1 - lr*wd)^k for a row whose last k steps were pure weight decay.  log2a = log2(1 - lr*wd) is
+// formed in double on the host; k*log2a in double, one v_exp_f32 (relative error ~1e-7, far below
+// the ~sqrt(k) ulp drift of the reference's own k repeated fp32 decays).  k == 0: exactly 1.
+static __device__ __forceinline__ float decay_pow(double log2a, int32_t k) {
   if (k <= 0) return 1.0f;
-  double r = 1.0, b = alpha;
-  while (k) {
-    if (k & 1) r *= b;
-    b *= b;
-    k >>= 1;
-  }
-  return (float)r;
+  return exp2f((float)((double)k * log2a));
 }
 
 static __device__ __forceinline__ float softplus(float z) {  // log(1 + e^z), overflow-free
@@ -101,14 +98,14 @@ static __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// sum over the wave of per-lane loss partials into this wave's own f64 slot (plain RMW: a slot
-// belongs to one wave per launch and launches are stream-ordered).  No same-address atomics: one
-// f64 atomic per wave into a single word serialises at ~13 ns each (4096 waves = 53 us).
+// sum over the wave of per-lane loss partials into this wave's own f64 slot.  Never one shared
+// word: same-address atomics serialise at ~13 ns each (4096 waves = 53 us).
 static __device__ __forceinline__ void wave_add_loss(double* slots, float v) {
   if (!slots) return;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  if ((threadIdx.x & 63) == 0) slots[blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)] += (double)v;
+  // no-return atomic into the wave's own slot: no contention, and the wave does not wait on it
+  if ((threadIdx.x & 63) == 0) atomicAdd(&slots[blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)], (double)v);
 }
 
 static inline unsigned grid_for(int64_t units, int G) {

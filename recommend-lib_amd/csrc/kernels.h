@@ -15,6 +15,7 @@ constexpr int kLossSlots = kMaxGridBlocks * 4;
 
 struct Geom {
   int D, G, EPL, ld;
+  int G4, S;  // float4 layout: G4 lanes per row, lane `sub` holds floats 4*sub + 4*G4*s, s < S
 };
 bool make_geom(int D, Geom* g);
 
@@ -33,18 +34,20 @@ struct Table {
 //   irec  [2B][8]   item segment s: {item, beg, end, ref0..ref3, long}        (meta[2] of them)
 //   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
 //                   sorted by item then position (fixed summation order)
-//   ilong [2B]      indices of item segments with > kLongSeg references      (meta[3] of them)
+//   lrec  [B/8][8]  copies of the records of item segments with > kLongSeg references (meta[3];
+//                   at most 2B/(kLongSeg+1) < B/8 of them)
 //   useg  [B+1], ioff [2B+1]   builder scratch (segment starts)
 //   meta  [4]       {triplets, user segments, item segments, long item segments}
 constexpr int kRec = 8;
 constexpr int kLongSeg = 16;
+constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
 struct BatchView {
-  int32_t *ij, *urec, *irec, *refs, *ilong, *useg, *ioff, *meta;
+  int32_t *ij, *urec, *irec, *refs, *lrec, *useg, *ioff, *meta;
 };
 struct BatchBuf {
   int32_t* base;
   int B;
-  __host__ __device__ static int64_t stride_for(int B) { return 33LL * B + 6; }
+  __host__ __device__ static int64_t stride_for(int B) { return 32LL * B + 6; }
   __host__ __device__ BatchView view(int64_t k) const {
     int32_t* p = base + k * stride_for(B);
     BatchView v;
@@ -52,10 +55,10 @@ struct BatchBuf {
     v.urec = p + 2LL * B;
     v.irec = p + 10LL * B;
     v.refs = p + 26LL * B;
-    v.ilong = p + 28LL * B;
-    v.useg = p + 30LL * B;
-    v.ioff = p + 31LL * B + 1;
-    v.meta = p + 33LL * B + 2;
+    v.lrec = p + 28LL * B;
+    v.useg = p + 29LL * B;
+    v.ioff = p + 30LL * B + 1;
+    v.meta = p + 32LL * B + 2;
     return v;
   }
 };
@@ -64,6 +67,7 @@ constexpr int kMaxSegBatch = 8192;  // largest batch the one-workgroup builder h
 struct Hyper {
   float lr, wd;
   double alpha;  // 1 - lr*wd in double: per-step decay factor of untouched rows
+  double log2a;  // log2(alpha): decay over k steps = exp2(k * log2a)
 };
 
 struct SamplerArgs {

@@ -101,9 +101,9 @@ __global__ __launch_bounds__(kBlock) void k_fwd_scatter(const int32_t* __restric
       if (sub == 0) atomicOr(err, 1);
       continue;
     }
-    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
-    const float fi = decay_pow(hp.alpha, t - 1 - Q.stamp[i]);
-    const float fj = decay_pow(hp.alpha, t - 1 - Q.stamp[j]);
+    const float fu = decay_pow(hp.log2a, t - 1 - P.stamp[u]);
+    const float fi = decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
+    const float fj = decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
     const float* pu = P.W + (int64_t)u * ld + sub;
     const float* qi = Q.W + (int64_t)i * ld + sub;
     const float* qj = Q.W + (int64_t)j * ld + sub;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_scatter(const int32_t* __restric
 template <int G, int EPL>
 __device__ __forceinline__ void apply_row(Table T, int64_t row, int32_t old, const Hyper& hp,
                                           int ld, int32_t t, int sub) {
-  const float f = decay_pow(hp.alpha, t - 1 - old);
+  const float f = decay_pow(hp.log2a, t - 1 - old);
   float* w = T.W + row * ld + sub;
   float* g = T.G + row * ld + sub;
   float wv[EPL], gv[EPL];
@@ -230,9 +230,9 @@ __global__ __launch_bounds__(kBlock) void k_score(const Idx* __restrict__ us,
       }
       continue;
     }
-    const float fu = decay_pow(hp.alpha, T - P.stamp[u]);
-    const float fi = decay_pow(hp.alpha, T - Q.stamp[i]);
-    const float fj = js ? decay_pow(hp.alpha, T - Q.stamp[j]) : 0.f;
+    const float fu = decay_pow(hp.log2a, T - P.stamp[u]);
+    const float fi = decay_pow(hp.log2a, T - Q.stamp[i]);
+    const float fj = js ? decay_pow(hp.log2a, T - Q.stamp[j]) : 0.f;
     const float* pu = P.W + u * ld + sub;
     const float* qi = Q.W + i * ld + sub;
     const float* qj = Q.W + j * ld + sub;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_flush(Table T, Hyper hp, int ld, int
   for (int64_t r = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; r < T.rows; r += ngroups) {
     const int32_t s = T.stamp[r];
     if (s == Tstep) continue;
-    const float f = decay_pow(hp.alpha, Tstep - s);
+    const float f = decay_pow(hp.log2a, Tstep - s);
     float* w = T.W + r * ld + sub;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) w[G * k] *= f;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(Table T, const int32_t* 
       for (int k = 0; k < EPL; ++k) o[G * k] = 0.f;
       continue;
     }
-    const float f = decay_pow(hp.alpha, t - 1 - T.stamp[row]);
+    const float f = decay_pow(hp.log2a, t - 1 - T.stamp[row]);
     const float* w = T.W + row * ld + sub;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) o[G * k] = w[G * k] * f;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_dist_fwd_scatter(
       if (sub == 0) atomicOr(err, 1);
       continue;
     }
-    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
+    const float fu = decay_pow(hp.log2a, t - 1 - P.stamp[u]);
     const float* pu = P.W + (int64_t)u * ld + sub;
     const float* qi = rows + (int64_t)a * ld + sub;
     const float* qj = rows + (int64_t)c2 * ld + sub;
@@ -371,24 +371,26 @@ __global__ __launch_bounds__(kBlock) void k_add_rows(Table T, const int32_t* __r
 bool make_geom(int D, Geom* g) {
   if (D <= 0 || D > 1024) return false;
   g->D = D;
-  if (D <= 64) {
-    int G = 4;
-    while (G < D) G <<= 1;
-    g->G = G;
+  // float4 layout (segmented kernels): G4 lanes x S stripes of float4 per row
+  const int q = (D + 3) / 4;
+  if (q <= 64) {
+    int G4 = 1;
+    while (G4 < q) G4 <<= 1;
+    g->G4 = G4;
+    g->S = 1;
+  } else {
+    g->G4 = 64;
+    g->S = (q + 63) / 64;
+  }
+  g->ld = 4 * g->G4 * g->S;
+  // dword layout (atomic / sharded kernels) over the same padded stride
+  if (g->ld < 64) {
+    g->G = g->ld;
     g->EPL = 1;
   } else {
-    int e = (D + 63) / 64;
-    static const int allowed[] = {2, 3, 4, 5, 6, 7, 8, 12, 16};
-    int pick = 16;
-    for (int a : allowed)
-      if (a >= e) {
-        pick = a;
-        break;
-      }
     g->G = 64;
-    g->EPL = pick;
+    g->EPL = g->ld / 64;
   }
-  g->ld = g->G * g->EPL;
   return true;
 }
 

@@ -28,6 +28,7 @@ namespace bprmf {
 
 constexpr int kBuildThreads = 1024;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kMaxLong = kMaxLongItems;  // hot items per batch given a whole workgroup in K2
 
 static __device__ __forceinline__ void store_rec(int32_t* rec, int a, int b, int c, int d, int e,
                                                  int f, int g, int h) {
@@ -222,7 +223,14 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
-        if (v.ioff[s + 1] - r > kLongSeg) v.ilong[lpre++] = s;
+        const int end = v.ioff[s + 1];
+        if (end - r > kLongSeg) {
+          if (lpre < kMaxLong)
+            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, 0, 0, 0, 0, 1);
+          else
+            v.irec[(int64_t)s * kRec + 7] = 0;  // over the cap: served by the short path
+          ++lpre;
+        }
         ++s;
       }
     }
@@ -231,171 +239,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     v.meta[0] = nvalid;
     v.meta[1] = n_useg;
     v.meta[2] = n_iseg;
-    v.meta[3] = n_long;
+    v.meta[3] = min(n_long, kMaxLong);
   }
 }
 
-// K1: user segments, one lane group each.  t = *tbase + step + 1.
-template <int G, int EPL>
-__global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
-                                                      int ld, const int32_t* __restrict__ tbase,
-                                                      int step, double* loss,
-                                                      float* __restrict__ contrib) {
-  const int sub = threadIdx.x & (G - 1);
-  const int s = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-  // independent loads: the record (allocated for every s < B), the segment count and the step
-  const int4 r0 = reinterpret_cast<const int4*>(bv.urec + (int64_t)s * kRec)[0];
-  const int r1x = bv.urec[(int64_t)s * kRec + 4];
-  const int n_useg = bv.meta[1];
-  const int32_t t = *tbase + step + 1;
-  float lsum = 0.f;
-  if (s < n_useg) {
-    const int32_t u = r0.x;
-    const int beg = r0.y, end = r0.z;
-    int32_t i = r0.w, j = r1x;
-    float* pw = P.W + (int64_t)u * ld + sub;
-    float pu[EPL], g[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      pu[k] = pw[G * k];
-      g[k] = 0.f;
-    }
-    const float fu = decay_pow(hp.alpha, t - 1 - P.stamp[u]);
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) pu[k] *= fu;
-    for (int p = beg; p < end; ++p) {
-      int2 nxt = make_int2(0, 0);
-      if (p + 1 < end) nxt = reinterpret_cast<const int2*>(bv.ij)[p + 1];
-      const float* qi = Q.W + (int64_t)i * ld + sub;
-      const float* qj = Q.W + (int64_t)j * ld + sub;
-      float vi[EPL], vj[EPL];
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        vi[k] = qi[G * k];
-        vj[k] = qj[G * k];
-      }
-      const float fi = decay_pow(hp.alpha, t - 1 - Q.stamp[i]);
-      const float fj = decay_pow(hp.alpha, t - 1 - Q.stamp[j]);
-      float di = 0.f, dj = 0.f;
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        vi[k] *= fi;
-        vj[k] *= fj;
-        di = fmaf(pu[k], vi[k], di);
-        dj = fmaf(pu[k], vj[k], dj);
-      }
-      di = group_sum<G>(di);
-      dj = group_sum<G>(dj);
-      const float x = di - dj;
-      const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
-      if (sub == 0) lsum += softplus(-x);
-      float* cb = contrib + (int64_t)p * ld + sub;
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        g[k] = fmaf(-c, vi[k] - vj[k], g[k]);
-        cb[G * k] = c * pu[k];
-      }
-      i = nxt.x;
-      j = nxt.y;
-    }
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) pw[G * k] = fmaf(-hp.lr, fmaf(hp.wd, pu[k], g[k]), pu[k]);
-    if (sub == 0) P.stamp[u] = t;
-  }
-  wave_add_loss(loss, lsum);
-}
-
-template <int G, int EPL>
-static __device__ __forceinline__ void add_ref(float (&g)[EPL], const float* __restrict__ contrib,
-                                               int32_t ref, int ld, int sub) {
-  const float sgn = (ref & 1) ? 1.f : -1.f;
-  const float* cb = contrib + (int64_t)(ref >> 1) * ld + sub;
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) g[k] = fmaf(sgn, cb[G * k], g[k]);
-}
-
-template <int G, int EPL>
-static __device__ __forceinline__ void apply_item(Table Q, int32_t item, const float (&g)[EPL],
-                                                  const Hyper& hp, int ld, int32_t t, int sub) {
-  float* w = Q.W + (int64_t)item * ld + sub;
-  float x[EPL];
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) x[k] = w[G * k];
-  const float f = decay_pow(hp.alpha, t - 1 - Q.stamp[item]);
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) {
-    const float vv = x[k] * f;
-    w[G * k] = fmaf(-hp.lr, fmaf(hp.wd, vv, g[k]), vv);
-  }
-  if (sub == 0) Q.stamp[item] = t;
-}
-
-// K2: blocks [0, long_blocks) take one long item segment each (all groups, LDS reduction in group
-// order); the rest take short segments, one lane group each.
-template <int G, int EPL>
-__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyper hp, int ld,
-                                                      const int32_t* __restrict__ tbase, int step,
-                                                      const float* __restrict__ contrib,
-                                                      int long_blocks) {
-  constexpr int NG = kBlock / G;
-  const int sub = threadIdx.x & (G - 1);
-  const int grp = threadIdx.x / G;
-  const int32_t t = *tbase + step + 1;
-  if ((int)blockIdx.x < long_blocks) {
-    __shared__ float part[NG][G * EPL];
-    const int n_long = bv.meta[3];
-    if ((int)blockIdx.x >= n_long) return;  // uniform over the block
-    const int s = bv.ilong[blockIdx.x];
-    const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
-    const int32_t item = r0.x;
-    const int beg = r0.y, end = r0.z;
-    float g[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) g[k] = 0.f;
-    int r = beg + grp;
-    for (; r + 3 * NG < end; r += 4 * NG) {  // 4 independent row loads in flight per group
-      const int32_t a0 = bv.refs[r], a1 = bv.refs[r + NG], a2 = bv.refs[r + 2 * NG],
-                    a3 = bv.refs[r + 3 * NG];
-      add_ref<G, EPL>(g, contrib, a0, ld, sub);
-      add_ref<G, EPL>(g, contrib, a1, ld, sub);
-      add_ref<G, EPL>(g, contrib, a2, ld, sub);
-      add_ref<G, EPL>(g, contrib, a3, ld, sub);
-    }
-    for (; r < end; r += NG) add_ref<G, EPL>(g, contrib, bv.refs[r], ld, sub);
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) part[grp][sub + G * k] = g[k];
-    __syncthreads();
-    if (grp == 0) {
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        float acc = part[0][sub + G * k];
-#pragma unroll
-        for (int q = 1; q < NG; ++q) acc += part[q][sub + G * k];
-        g[k] = acc;
-      }
-      apply_item<G, EPL>(Q, item, g, hp, ld, t, sub);
-    }
-    return;
-  }
-  const int s = (blockIdx.x - long_blocks) * NG + grp;
-  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
-  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
-  const int n_iseg = bv.meta[2];
-  if (s >= n_iseg || r1.w) return;  // past the batch's items, or a long segment
-  const int32_t item = r0.x;
-  const int beg = r0.y, end = r0.z, len = end - beg;
-  float g[EPL];
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) g[k] = 0.f;
-  add_ref<G, EPL>(g, contrib, r0.w, ld, sub);
-  if (len > 1) add_ref<G, EPL>(g, contrib, r1.x, ld, sub);
-  if (len > 2) add_ref<G, EPL>(g, contrib, r1.y, ld, sub);
-  if (len > 3) add_ref<G, EPL>(g, contrib, r1.z, ld, sub);
-  for (int r = beg + 4; r < end; ++r) add_ref<G, EPL>(g, contrib, bv.refs[r], ld, sub);
-  apply_item<G, EPL>(Q, item, g, hp, ld, t, sub);
-}
-
-// ------------------------------------------------------------------------------------------------
 static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
   int b = 1;
   while (b < 32 && (1LL << b) < n) ++b;
@@ -418,25 +265,5 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   return hipGetLastError();
 }
 
-hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s) {
-  BPRMF_DISPATCH(g, ({
-    const unsigned blocks = (unsigned)((B + kBlock / G_ - 1) / (kBlock / G_));
-    k_user_step<G_, E_><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss, contrib);
-  }));
-  return hipGetLastError();
-}
-
-hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, const float* contrib, hipStream_t s) {
-  const int long_blocks = (2 * B) / (kLongSeg + 1);
-  BPRMF_DISPATCH(g, ({
-    const unsigned blocks =
-        (unsigned)(long_blocks + (2LL * B + kBlock / G_ - 1) / (kBlock / G_));
-    k_item_step<G_, E_><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
-                                                  long_blocks);
-  }));
-  return hipGetLastError();
-}
-
 }  // namespace bprmf
+

@@ -1,0 +1,282 @@
+// step.hip — the two per-step kernels of the segmented (atomic-free, deterministic) BPR-MF step,
+// over the batch layout built by k_build_batches (segment.hip).
+//
+//   k_user_step (K1) one lane group per user segment: gather P_u, Q_i, Q_j with their pending
+//     weight decay, x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x) = -dL/dx; the user's gradient
+//     -c (Q_i - Q_j) is summed in registers over the segment; c*P_u is stored per triplet for K2;
+//     the updated user row W = V - lr (g + wd V) is written in place (every read of P_u in the
+//     step belongs to this segment).
+//   k_item_step (K2) one lane group per distinct item; items with more than kLongSeg references
+//     get a whole workgroup and an LDS reduction in group order.  g = sum of -/+ c*P_u over the
+//     item's references in a fixed order, then the same SGD + weight decay update.
+// Reference semantics: BPRMFRecommender.py:172-176 (forward :42-50, loss :174, SGD(wd) :154).
+//
+// Row layout: G4 lanes per row, each lane one float4 per stripe (16 B/lane, whole 64..1024 B rows
+// per wave instruction); 64/G4 rows per wave.  Nothing here is an atomic: every output row has
+// exactly one writer, so the result does not depend on scheduling.
+#include <algorithm>
+
+#include "device_common.h"
+
+namespace bprmf {
+
+static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+static __device__ __forceinline__ float4 scale4(float4 a, float s) {
+  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+}
+static __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
+  acc = fmaf(a.x, b.x, acc);
+  acc = fmaf(a.y, b.y, acc);
+  acc = fmaf(a.z, b.z, acc);
+  return fmaf(a.w, b.w, acc);
+}
+// a + s*b, per component, fused
+static __device__ __forceinline__ float4 fma4(float s, float4 b, float4 a) {
+  return make_float4(fmaf(s, b.x, a.x), fmaf(s, b.y, a.y), fmaf(s, b.z, a.z), fmaf(s, b.w, a.w));
+}
+static __device__ __forceinline__ float4 sub4(float4 a, float4 b) {
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+// W <- V - lr (g + wd V): torch SGD  d_p = grad.add(param, alpha=wd); param.add_(d_p, alpha=-lr)
+static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, float wd) {
+  return make_float4(fmaf(-lr, fmaf(wd, v.x, g.x), v.x), fmaf(-lr, fmaf(wd, v.y, g.y), v.y),
+                     fmaf(-lr, fmaf(wd, v.z, g.z), v.z), fmaf(-lr, fmaf(wd, v.w, g.w), v.w));
+}
+
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
+                                                      int ld, const int32_t* __restrict__ tbase,
+                                                      int step, double* loss,
+                                                      float* __restrict__ contrib) {
+  const int sub = threadIdx.x & (G4 - 1);
+  const int s = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
+  // independent loads: the record (allocated for every s < B), the segment count, the step base
+  const int4 r0 = reinterpret_cast<const int4*>(bv.urec + (int64_t)s * kRec)[0];
+  const int r1x = bv.urec[(int64_t)s * kRec + 4];
+  const int n_useg = bv.meta[1];
+  const int32_t t = *tbase + step + 1;
+  float lsum = 0.f;
+  if (s < n_useg) {
+    const int32_t u = r0.x;
+    const int beg = r0.y, end = r0.z;
+    int32_t i = r0.w, j = r1x;
+    float* pw = P.W + (int64_t)u * ld + 4 * sub;
+    float4 pu[S], g[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      pu[k] = ld4(pw + 4 * G4 * k);
+      g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float fu = decay_pow(hp.log2a, t - 1 - P.stamp[u]);
+#pragma unroll
+    for (int k = 0; k < S; ++k) pu[k] = scale4(pu[k], fu);
+    for (int p = beg; p < end; ++p) {
+      int2 nxt = make_int2(0, 0);
+      if (p + 1 < end) nxt = reinterpret_cast<const int2*>(bv.ij)[p + 1];
+      const float* qi = Q.W + (int64_t)i * ld + 4 * sub;
+      const float* qj = Q.W + (int64_t)j * ld + 4 * sub;
+      float4 vi[S], vj[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        vi[k] = ld4(qi + 4 * G4 * k);
+        vj[k] = ld4(qj + 4 * G4 * k);
+      }
+      const float fi = decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
+      const float fj = decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
+      float di = 0.f, dj = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        vi[k] = scale4(vi[k], fi);
+        vj[k] = scale4(vj[k], fj);
+        di = dot4(pu[k], vi[k], di);
+        dj = dot4(pu[k], vj[k], dj);
+      }
+      di = group_sum<G4>(di);
+      dj = group_sum<G4>(dj);
+      const float x = di - dj;
+      const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
+      if (sub == 0 && loss) lsum += softplus(-x);
+      float* cb = contrib + (int64_t)p * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        g[k] = fma4(-c, sub4(vi[k], vj[k]), g[k]);
+        st4(cb + 4 * G4 * k, scale4(pu[k], c));
+      }
+      i = nxt.x;
+      j = nxt.y;
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) st4(pw + 4 * G4 * k, sgd4(pu[k], g[k], hp.lr, hp.wd));
+    if (sub == 0) P.stamp[u] = t;
+  }
+  if (loss) wave_add_loss(loss, lsum);
+}
+
+template <int G4, int S>
+static __device__ __forceinline__ void apply_item(Table Q, int32_t item, const float4 (&g)[S],
+                                                  const Hyper& hp, int ld, int32_t t, int sub) {
+  float* w = Q.W + (int64_t)item * ld + 4 * sub;
+  float4 x[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) x[k] = ld4(w + 4 * G4 * k);
+  const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[item]);
+#pragma unroll
+  for (int k = 0; k < S; ++k) st4(w + 4 * G4 * k, sgd4(scale4(x[k], f), g[k], hp.lr, hp.wd));
+  if (sub == 0) Q.stamp[item] = t;
+}
+
+template <int G4, int S>
+static __device__ __forceinline__ void load_ref(float4 (&row)[S], const float* __restrict__ contrib,
+                                                int32_t ref, int ld, int sub) {
+  const float* cb = contrib + (int64_t)(ref >> 1) * ld + 4 * sub;
+#pragma unroll
+  for (int k = 0; k < S; ++k) row[k] = ld4(cb + 4 * G4 * k);
+}
+
+template <int S>
+static __device__ __forceinline__ void acc_ref(float4 (&g)[S], const float4 (&row)[S], int32_t ref) {
+  const float sgn = (ref & 1) ? 1.f : -1.f;  // j: +c P_u, i: -c P_u
+#pragma unroll
+  for (int k = 0; k < S; ++k) g[k] = fma4(sgn, row[k], g[k]);
+}
+
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyper hp, int ld,
+                                                      const int32_t* __restrict__ tbase, int step,
+                                                      const float* __restrict__ contrib,
+                                                      int long_blocks) {
+  constexpr int NG = kBlock / G4;
+  const int sub = threadIdx.x & (G4 - 1);
+  const int grp = threadIdx.x / G4;
+  const int32_t t = *tbase + step + 1;
+  if ((int)blockIdx.x < long_blocks) {
+    __shared__ float4 part[NG][G4 * S];
+    const int4 r0 = reinterpret_cast<const int4*>(bv.lrec + (int64_t)blockIdx.x * kRec)[0];
+    const int n_long = bv.meta[3];
+    if ((int)blockIdx.x >= n_long) return;  // uniform over the block
+    const int32_t item = r0.x;
+    const int beg = r0.y, end = r0.z;
+    float4 g[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // group q owns refs beg + q + NG*m.  Its lanes fetch G4 of those refs at once; every row of a
+    // chunk of 8 is requested before any is accumulated (accumulation order fixed: m ascending).
+    const int lane0 = (threadIdx.x & 63) - sub;
+    for (int base = beg + grp; base < end; base += NG * G4) {
+      const int ridx = base + NG * sub;
+      const int32_t myref = ridx < end ? bv.refs[ridx] : 0;
+      const int cnt = min(G4, (end - base + NG - 1) / NG);
+      for (int m0 = 0; m0 < cnt; m0 += 8) {
+        float4 rows[8][S];
+        int32_t rf[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
+          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) part[grp][sub + G4 * k] = g[k];
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        float4 acc = part[0][sub + G4 * k];
+#pragma unroll 4
+        for (int q = 1; q < NG; ++q) {
+          const float4 o = part[q][sub + G4 * k];
+          acc = make_float4(acc.x + o.x, acc.y + o.y, acc.z + o.z, acc.w + o.w);
+        }
+        g[k] = acc;
+      }
+      apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+    }
+    return;
+  }
+  const int s = (blockIdx.x - long_blocks) * NG + grp;
+  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
+  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
+  const int n_iseg = bv.meta[2];
+  if (s >= n_iseg || r1.w) return;  // past the batch's items, or a workgroup-served hot item
+  const int32_t item = r0.x;
+  const int beg = r0.y, end = r0.z, len = end - beg;
+  float4 g[S], row[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (len <= 4) {  // the common case: every ref inline, all rows requested before accumulating
+    float4 rows[4][S];
+    const int32_t rf[4] = {r0.w, r1.x, r1.y, r1.z};
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (m < len) acc_ref<S>(g, rows[m], rf[m]);
+  } else {  // lanes fetch G4 refs at once; rows requested 8 at a time before accumulating
+    const int lane0 = (threadIdx.x & 63) - sub;
+    for (int base = beg; base < end; base += G4) {
+      const int32_t myref = base + sub < end ? bv.refs[base + sub] : 0;
+      const int cnt = min(G4, end - base);
+      for (int m0 = 0; m0 < cnt; m0 += 8) {
+        float4 rows[8][S];
+        int32_t rf[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
+          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
+      }
+    }
+  }
+  (void)row;
+  apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+}
+
+// Expand BODY for every instantiated float4 geometry (G4_, S_).
+#define BPRMF_DISPATCH4(geom, BODY)                                \
+  switch ((geom).G4 * 10 + (geom).S) {                             \
+    case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
+    case 21: { constexpr int G4_ = 2, S_ = 1; BODY; } break;       \
+    case 41: { constexpr int G4_ = 4, S_ = 1; BODY; } break;       \
+    case 81: { constexpr int G4_ = 8, S_ = 1; BODY; } break;       \
+    case 161: { constexpr int G4_ = 16, S_ = 1; BODY; } break;     \
+    case 321: { constexpr int G4_ = 32, S_ = 1; BODY; } break;     \
+    case 641: { constexpr int G4_ = 64, S_ = 1; BODY; } break;     \
+    case 642: { constexpr int G4_ = 64, S_ = 2; BODY; } break;     \
+    case 643: { constexpr int G4_ = 64, S_ = 3; BODY; } break;     \
+    case 644: { constexpr int G4_ = 64, S_ = 4; BODY; } break;     \
+    default: return hipErrorInvalidValue;                          \
+  }
+
+hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s) {
+  BPRMF_DISPATCH4(g, ({
+    const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
+    k_user_step<G4_, S_><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss, contrib);
+  }));
+  return hipGetLastError();
+}
+
+int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg + 1)); }
+
+hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, const float* contrib, hipStream_t s) {
+  const int long_blocks = item_long_blocks(B);
+  BPRMF_DISPATCH4(g, ({
+    const unsigned blocks =
+        (unsigned)(long_blocks + (2LL * B + kBlock / G4_ - 1) / (kBlock / G4_));
+    k_item_step<G4_, S_><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
+                                                   long_blocks);
+  }));
+  return hipGetLastError();
+}
+
+}  // namespace bprmf

@@ -60,7 +60,8 @@ typedef struct {
 } bprmf_stats;
 
 /* live kernel timing (HIP events around every launch of each kind while enabled) */
-enum { BPRMF_KPROF_SAMPLE = 0, BPRMF_KPROF_FWD_SCATTER = 1, BPRMF_KPROF_APPLY = 2, BPRMF_KPROF_KINDS = 4 };
+/* kinds: sample/build, step kernel 1 (users), step kernel 2 (items), owner-side item update */
+enum { BPRMF_KPROF_SAMPLE = 0, BPRMF_KPROF_FWD_SCATTER = 1, BPRMF_KPROF_APPLY = 2, BPRMF_KPROF_OWNER = 3, BPRMF_KPROF_KINDS = 4 };
 typedef struct {
   int64_t count[4];     /* launches recorded per kind */
   double ms[4];         /* summed device time per kind (ms) */
@@ -129,22 +130,30 @@ int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const
 int bprmf_profile(bprmf_handle* h, int32_t enable);
 int bprmf_profile_read(bprmf_handle* h, bprmf_kprof* out);
 
-/* ---- sharded step phases (one process per GPU; exchanges done by the caller over RCCL) ---- */
-/* A step on a world>1 handle:  begin -> [caller: all-to-all requested item ids]
- *   -> gather_items (owner side) -> [caller: all-to-all rows back]
- *   -> fwd_scatter (local triplets vs received rows) -> apply_users
- *   -> [caller: all-to-all item grads to owners] -> apply_items -> end.
- * Ids passed here are LOCAL row indices of this handle (global id / world) unless noted. */
-int bprmf_dist_begin_step(bprmf_handle* h);
+/* ---- sharded steps (one process per GPU; the caller moves the buffers over RCCL) ---------- */
+/* Users u live on rank u % world, items i on rank i % world (strided row sharding).  A step:
+ *   request_ids -> [all-to-all ids] -> gather_items (owner) -> [all-to-all rows back]
+ *   -> user_step (local users vs the received rows) -> item_grads (one row per requested item)
+ *   -> [all-to-all grads to the owners] -> apply_items (owner) -> end_step.
+ * Requests are owner-major: the first owner_counts[k][0] ids go to rank 0, and so on; ids are the
+ * owner's LOCAL rows (item / world).  Device buffers have row stride bprmf_row_stride floats. */
+/* Build steps [first_step, first_step+n_steps) of `epoch` for this shard (device sampler over its
+ * own users; steps past the shard's epoch are empty) and copy the per-owner request counts
+ * owner_counts[n_steps][world] to the host (the exchange sizes).  Replaces the previous plan. */
+int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                    int32_t* owner_counts);
+/* Same from host triplets u/i/j[n_steps * batch_size] (global ids, this shard's users only;
+ * u < 0 marks an empty slot): the replay form of BPRData batches. */
+int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                           int64_t n_steps, int32_t* owner_counts);
+int bprmf_dist_request_ids(bprmf_handle* h, int64_t step, int32_t* ids, int64_t n);
 int bprmf_dist_gather_items(bprmf_handle* h, const int32_t* rows, int64_t n, float* out);
-int bprmf_dist_fwd_scatter(bprmf_handle* h, const int32_t* u_local, const int32_t* slot_i,
-                           const int32_t* slot_j, int64_t n, const float* item_rows,
-                           float* item_grads, int64_t n_slots);
-int bprmf_dist_apply_users(bprmf_handle* h, const int32_t* u_local, int64_t n);
+int bprmf_dist_user_step(bprmf_handle* h, int64_t step, const float* item_rows);
+int bprmf_dist_item_grads(bprmf_handle* h, int64_t step, float* grads);
 int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n);
+/* Advance the step counter; loss != NULL: loss since the last read (synchronises). */
 int bprmf_dist_end_step(bprmf_handle* h, double* loss);
-/* Device triplets of a step of an epoch for this shard: writes global (u, i, j) of the slots
- * [first, first+n) of the shard's epoch order into device buffers. */
+/* Device triplets (global ids) of slots [first, first+n) of the shard's epoch order. */
 int bprmf_dist_sample_dev(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t* u,
                           int32_t* i, int32_t* j);
 /* row stride (floats) of device row buffers used by the dist_* exchange functions */

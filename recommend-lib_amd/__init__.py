@@ -13,6 +13,8 @@ from .build import build, LIB as LIB_PATH
 from .data import BPRData
 from .model import BPRMF
 from . import metrics
+from . import sharded
+from .sharded import ShardedBPRMF
 
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 

@@ -36,7 +36,7 @@ class Stats(ctypes.Structure):
 class KProf(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int64 * 4), ("ms", ctypes.c_double * 4)]
 
-    KINDS = ("sample", "fwd_scatter", "apply")
+    KINDS = ("sample", "user_step", "item_step", "owner_apply")
 
     def as_dict(self):
         return {k: dict(count=int(self.count[n]), ms=float(self.ms[n])) for n, k in enumerate(self.KINDS)}
@@ -66,10 +66,12 @@ SIGNATURES = {
     "bprmf_sample": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
     "bprmf_score": [_P, _P, _P, _I64, _P],
     "bprmf_forward_dev": [_P, _P, _P, _P, _I64, _P, _P],
-    "bprmf_dist_begin_step": [_P],
+    "bprmf_dist_plan": [_P, ctypes.c_uint32, _I64, _I64, _P],
+    "bprmf_dist_plan_replay": [_P, _P, _P, _P, _I64, _P],
+    "bprmf_dist_request_ids": [_P, _I64, _P, _I64],
     "bprmf_dist_gather_items": [_P, _P, _I64, _P],
-    "bprmf_dist_fwd_scatter": [_P, _P, _P, _P, _I64, _P, _P, _I64],
-    "bprmf_dist_apply_users": [_P, _P, _I64],
+    "bprmf_dist_user_step": [_P, _I64, _P],
+    "bprmf_dist_item_grads": [_P, _I64, _P],
     "bprmf_dist_apply_items": [_P, _P, _P, _I64],
     "bprmf_dist_end_step": [_P, ctypes.POINTER(ctypes.c_double)],
     "bprmf_dist_sample_dev": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],

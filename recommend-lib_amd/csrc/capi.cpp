@@ -61,6 +61,7 @@ struct bprmf_handle {
   int64_t batch_cap = 0;
   float* d_contrib = nullptr;  // [B, ld]
   int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
+  int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;
   // misc device scalars
   double* d_loss = nullptr;
@@ -221,6 +222,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
   TRY(memz(h->d_err, sizeof(int32_t)));
+  TRY(memz(h->d_loss, sizeof(double) * kLossSlots));
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size
   const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
   e = init_normal(g, h->P.W, h->U, cfg->init_std, s0, s1, 0u, (int)W, (int)R, h->stream);
@@ -458,19 +460,20 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
-    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U, h->I, bb,
-                         h->d_err, h->stream));
+    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
+                         h->cfg.item_num, 1, false, nb, bb, h->d_err, h->stream));
   }
   for (int64_t k = 0; k < nb; ++k) {
     const BatchView v = bb.view(k);
     {
       ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
       HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                       h->d_contrib, h->stream));
+                       h->d_contrib, nullptr, h->stream));
     }
     {
       ProfScope ps(h, BPRMF_KPROF_APPLY);
-      HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->stream));
+      HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
+                       h->stream));
     }
   }
   h->t += (int32_t)nb;
@@ -700,12 +703,82 @@ int bprmf_profile_read(bprmf_handle* h, bprmf_kprof* out) {
   return 0;
 }
 
-// ---- sharded phases ------------------------------------------------------------------------
-int bprmf_dist_begin_step(bprmf_handle* h) {
-  if (!h) return fail(BPRMF_E_INVALID, "null handle");
-  if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+// ---- sharded steps (one process per GPU; the caller moves the buffers over RCCL) ------------
+// Users u live on rank u % world, items i on rank i % world.  A step of this shard:
+//   request_ids -> [all-to-all ids] -> gather_items (owner) -> [all-to-all rows back]
+//   -> user_step (K1: local users vs received rows) -> item_grads (K2: per requested item)
+//   -> [all-to-all grads to owners] -> apply_items (owner) -> end_step.
+static int dist_counts(bprmf_handle* h, int64_t n_steps, int32_t* owner_counts) {
+  const int64_t stride = BatchBuf::stride_for(h->cfg.batch_size);
+  const BatchBuf bb{h->d_batch, h->cfg.batch_size};
+  HIPCHK(hipMemcpy2DAsync(owner_counts, sizeof(int32_t) * h->cfg.world, bb.view(0).own,
+                          sizeof(int32_t) * stride, sizeof(int32_t) * h->cfg.world, n_steps,
+                          hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->plan_steps = n_steps;
+  return check_err_flag(h);
+}
+
+int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                    int32_t* owner_counts) {
+  if (!h || first_step < 0 || n_steps <= 0 || !owner_counts) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (!seg_mode(h)) return fail(BPRMF_E_UNSUPPORTED, "sharded steps need batch_size <= %d", kMaxSegBatch);
+  if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
   if (int r = set_dev(h)) return r;
-  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
+  if (int r = ensure_seg(h, n_steps)) return r;
+  int64_t N;
+  bprmf_epoch_size(h, &N, nullptr);
+  const int64_t B = h->cfg.batch_size;
+  const int64_t first_slot = first_step * B;
+  const int64_t n_slots = std::max<int64_t>(0, std::min(N - first_slot, n_steps * B));
+  const BatchBuf bb{h->d_batch, (int)B};
+  {
+    ProfScope ps(h, BPRMF_KPROF_SAMPLE);
+    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, (int)B, nullptr, nullptr,
+                         nullptr, h->U, h->cfg.item_num, h->cfg.world, true, n_steps, bb, h->d_err,
+                         h->stream));
+  }
+  return dist_counts(h, n_steps, owner_counts);
+}
+
+int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                           int64_t n_steps, int32_t* owner_counts) {
+  if (!h || n_steps <= 0 || !u || !i || !j || !owner_counts) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (!seg_mode(h)) return fail(BPRMF_E_UNSUPPORTED, "sharded steps need batch_size <= %d", kMaxSegBatch);
+  const int64_t B = h->cfg.batch_size, n = n_steps * B, W = h->cfg.world, R = h->cfg.rank;
+  for (int64_t k = 0; k < n; ++k) {
+    if (u[k] < 0) continue;  // padding slot
+    if (u[k] >= h->cfg.user_num || u[k] % W != R)
+      return fail(BPRMF_E_RANGE, "user %d at %lld is not a user of shard %lld", u[k], (long long)k, (long long)R);
+    if (i[k] < 0 || i[k] >= h->cfg.item_num || j[k] < 0 || j[k] >= h->cfg.item_num)
+      return fail(BPRMF_E_RANGE, "item id at %lld out of range", (long long)k);
+  }
+  if (int r = set_dev(h)) return r;
+  if (int r = ensure_seg(h, n_steps)) return r;
+  if (int r = ensure_trip(h, n)) return r;
+  int32_t* tu = h->d_trip;
+  int32_t* ti = tu + h->trip_cap;
+  int32_t* tj = ti + h->trip_cap;
+  HIPCHK(hipMemcpyAsync(tu, u, 4 * n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(ti, i, 4 * n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(tj, j, 4 * n, hipMemcpyHostToDevice, h->stream));
+  const BatchBuf bb{h->d_batch, (int)B};
+  HIPCHK(build_batches(sampler_args(h), 0, 0, n, (int)B, tu, ti, tj, h->U, h->cfg.item_num,
+                       h->cfg.world, true, n_steps, bb, h->d_err, h->stream));
+  return dist_counts(h, n_steps, owner_counts);
+}
+
+static int dist_step_ok(bprmf_handle* h, int64_t k) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (k < 0 || k >= h->plan_steps) return fail(BPRMF_E_STATE, "step %lld is not in the current plan", (long long)k);
+  return set_dev(h);
+}
+
+int bprmf_dist_request_ids(bprmf_handle* h, int64_t k, int32_t* ids, int64_t n) {
+  if (int r = dist_step_ok(h, k)) return r;
+  if (n < 0 || (n > 0 && !ids) || n > 2LL * h->cfg.batch_size) return fail(BPRMF_E_INVALID, "bad arguments");
+  const BatchBuf bb{h->d_batch, h->cfg.batch_size};
+  if (n) HIPCHK(hipMemcpyAsync(ids, bb.view(k).ukey, 4 * n, hipMemcpyDeviceToDevice, h->stream));
   return 0;
 }
 
@@ -716,27 +789,31 @@ int bprmf_dist_gather_items(bprmf_handle* h, const int32_t* rows, int64_t n, flo
   return 0;
 }
 
-int bprmf_dist_fwd_scatter(bprmf_handle* h, const int32_t* u_local, const int32_t* slot_i,
-                           const int32_t* slot_j, int64_t n, const float* item_rows,
-                           float* item_grads, int64_t n_slots) {
-  if (!h || n < 0 || (n > 0 && (!u_local || !slot_i || !slot_j || !item_rows || !item_grads)))
-    return fail(BPRMF_E_INVALID, "bad arguments");
-  if (int r = set_dev(h)) return r;
-  HIPCHK(dist_fwd_scatter(h->geom, u_local, slot_i, slot_j, n, h->P, item_rows, item_grads, n_slots,
-                          h->hp, h->t + 1, h->d_loss, h->d_err, h->stream));
+int bprmf_dist_user_step(bprmf_handle* h, int64_t k, const float* item_rows) {
+  if (int r = dist_step_ok(h, k)) return r;
+  if (!item_rows) return fail(BPRMF_E_INVALID, "null item_rows");
+  const BatchBuf bb{h->d_batch, h->cfg.batch_size};
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
+  ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
+  HIPCHK(user_step(h->geom, bb.view(k), h->cfg.batch_size, h->P, h->Q, h->hp, h->d_tbase, 0,
+                   h->d_loss, h->d_contrib, item_rows, h->stream));
   return 0;
 }
 
-int bprmf_dist_apply_users(bprmf_handle* h, const int32_t* u_local, int64_t n) {
-  if (!h || n < 0 || (n > 0 && !u_local)) return fail(BPRMF_E_INVALID, "bad arguments");
-  if (int r = set_dev(h)) return r;
-  HIPCHK(apply_rows(h->geom, h->P, u_local, n, h->hp, h->t + 1, h->stream));
+int bprmf_dist_item_grads(bprmf_handle* h, int64_t k, float* grads) {
+  if (int r = dist_step_ok(h, k)) return r;
+  if (!grads) return fail(BPRMF_E_INVALID, "null grads");
+  const BatchBuf bb{h->d_batch, h->cfg.batch_size};
+  ProfScope ps(h, BPRMF_KPROF_APPLY);
+  HIPCHK(item_step(h->geom, bb.view(k), h->cfg.batch_size, h->Q, h->hp, h->d_tbase, 0,
+                   h->d_contrib, grads, h->stream));
   return 0;
 }
 
 int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n) {
   if (!h || n < 0 || (n > 0 && (!rows || !grads))) return fail(BPRMF_E_INVALID, "bad arguments");
   if (int r = set_dev(h)) return r;
+  ProfScope ps(h, BPRMF_KPROF_OWNER);
   HIPCHK(add_rows(h->geom, h->Q, rows, grads, n, h->d_err, h->stream));
   HIPCHK(apply_rows(h->geom, h->Q, rows, n, h->hp, h->t + 1, h->stream));
   return 0;
@@ -745,9 +822,11 @@ int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* gr
 int bprmf_dist_end_step(bprmf_handle* h, double* loss) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (int r = set_dev(h)) return r;
+  if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   h->t += 1;
-  if (loss) {
+  if (loss) {  // loss since the last read; resets the accumulator
     if (int r = read_loss(h, loss)) return r;
+    HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
     return check_err_flag(h);
   }
   return 0;

@@ -37,17 +37,22 @@ struct Table {
 //   lrec  [B/8][8]  copies of the records of item segments with > kLongSeg references (meta[3];
 //                   at most 2B/(kLongSeg+1) < B/8 of them)
 //   useg  [B+1], ioff [2B+1]   builder scratch (segment starts)
+//   ukey  [2B]      sharded mode: the distinct items as the owner's local row, segment order
 //   meta  [4]       {triplets, user segments, item segments, long item segments}
+//   own   [64]      sharded mode: item segments per owner rank (segments are owner-major)
+// Item segments are ordered by key = (item % world) * iloc + item / world (= item when world 1).
+// In sharded mode ij / urec hold item SLOTS (segment indices: rows of the exchange buffers).
 constexpr int kRec = 8;
 constexpr int kLongSeg = 16;
 constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
+constexpr int kMaxWorld = 64;
 struct BatchView {
-  int32_t *ij, *urec, *irec, *refs, *lrec, *useg, *ioff, *meta;
+  int32_t *ij, *urec, *irec, *refs, *lrec, *useg, *ioff, *ukey, *meta, *own;
 };
 struct BatchBuf {
   int32_t* base;
   int B;
-  __host__ __device__ static int64_t stride_for(int B) { return 32LL * B + 6; }
+  __host__ __device__ static int64_t stride_for(int B) { return 34LL * B + 6 + kMaxWorld; }
   __host__ __device__ BatchView view(int64_t k) const {
     int32_t* p = base + k * stride_for(B);
     BatchView v;
@@ -58,7 +63,9 @@ struct BatchBuf {
     v.lrec = p + 28LL * B;
     v.useg = p + 29LL * B;
     v.ioff = p + 30LL * B + 1;
-    v.meta = p + 32LL * B + 2;
+    v.ukey = p + 32LL * B + 2;
+    v.meta = p + 34LL * B + 2;
+    v.own = p + 34LL * B + 6;
     return v;
   }
 };
@@ -93,13 +100,21 @@ hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const
                       int64_t n, Table P, Table Q, const Hyper& hp, int32_t t, hipStream_t s);
 // segmented step: build `n_batches` batches of B (<= kMaxSegBatch) from the sampler (ru == null)
 // or from replayed ids; then per batch k: user_step (K1) and item_step (K2) with t = *tbase+k+1.
+// ru/ri/rj are GLOBAL ids (users are mapped to local rows u / world).  i_rows = global item count.
+// slots: write item slots (sharded exchange) instead of item rows into ij/urec.
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
-                         int64_t u_rows, int64_t i_rows, BatchBuf bb, int32_t* err, hipStream_t s);
+                         int64_t u_rows, int64_t i_rows, int world, bool slots, int64_t n_batches,
+                         BatchBuf bb, int32_t* err, hipStream_t s);
+// item_rows != null: sharded K1 (item rows by slot from the exchange buffer)
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s);
+                     const int32_t* tbase, int step, double* loss, float* contrib,
+                     const float* item_rows, hipStream_t s);
+// grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying)
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, const float* contrib, hipStream_t s);
+                     const int32_t* tbase, int step, const float* contrib, float* grads,
+                     hipStream_t s);
+int item_long_blocks(int B);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

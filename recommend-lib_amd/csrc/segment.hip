@@ -1,22 +1,15 @@
-// segment.hip — the atomic-free, deterministic BPR-MF step for batches of <= kMaxSegBatch triplets.
+// segment.hip — batch builder of the segmented (atomic-free, deterministic) BPR-MF step.
 //
-// Per chunk of steps (off the per-step critical path, full-chip parallel):
-//   k_build_batches  one 1024-thread workgroup per batch: produce the batch's triplets (the device
-//                    sampler, bit-identical to k_sample, or replayed ids), sort them by user in LDS
-//                    (rocPRIM block radix sort), sort the batch's 2B item references by item, and
-//                    write 32-byte segment records so each step kernel needs ONE dependent load
-//                    before its row gathers.
-// Per step (two launches):
-//   k_user_step (K1) one lane group per user segment: gather P_u, Q_i, Q_j (pending decay applied),
-//                    x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x); accumulate the user's gradient in
-//                    registers; store c*P_u per triplet; write the updated user row and its stamp.
-//                    Every read of P_u in the step is inside the segment, so the in-place write is
-//                    race-free.
-//   k_item_step (K2) one lane group per distinct item (a whole workgroup for items with more than
-//                    kLongSeg references, reduced through LDS in a fixed order): sum -/+ c*P_u over
-//                    the item's references, W <- V - lr (g + wd V), V = W*(1-lr*wd)^pending.
-// No f32 atomics, results are bitwise reproducible run to run.
-// Reference semantics: BPRMFRecommender.py:172-176 (see kernels.hip header).
+// k_build_batches: one 1024-thread workgroup per batch of B <= kMaxSegBatch triplets, run once per
+// chunk of steps at full-chip parallelism (off the per-step critical path):
+//   1. the batch's triplets: the device sampler (bit-identical to k_sample: Feistel shuffle of the
+//      epoch, negative = k-th non-positive item; util/data_loader.py:680-690 semantics) or
+//      replayed ids;
+//   2. sort by (local) user row in LDS (rocPRIM block radix sort) -> user segments;
+//   3. sort the 2B item references (i: -, j: +) by item key = (owner, owner's row) -> item
+//      segments, their references in a fixed order, hot-item records, per-owner counts;
+//   4. 32-byte segment records so each step kernel needs ONE dependent load before its gathers.
+// Layout: kernels.h (BatchBuf).  Step kernels: step.hip.
 #include <string.h>
 
 #include <rocprim/block/block_radix_sort.hpp>
@@ -28,7 +21,6 @@ namespace bprmf {
 
 constexpr int kBuildThreads = 1024;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kMaxLong = kMaxLongItems;  // hot items per batch given a whole workgroup in K2
 
 static __device__ __forceinline__ void store_rec(int32_t* rec, int a, int b, int c, int d, int e,
                                                  int f, int g, int h) {
@@ -40,8 +32,8 @@ template <int IPT>
 __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
-    int64_t u_rows, int64_t i_rows, int user_bits, int item_bits, BatchBuf bb,
-    int32_t* __restrict__ err) {
+    int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int user_bits,
+    int item_bits, BatchBuf bb, int32_t* __restrict__ err) {
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -54,16 +46,18 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   };
   __shared__ Smem sm;
   __shared__ typename Scan::storage_type sscan;
-  __shared__ int32_t s_i[T * IPT];
+  __shared__ int32_t s_i[T * IPT];  // per sorted position: item row (world 1) or item slot
   __shared__ int32_t s_j[T * IPT];
+  __shared__ int s_own[kMaxWorld];
   uint32_t* s_key = sm.key;
 
   const int tid = threadIdx.x;
   const int64_t batch = blockIdx.x;
   const int64_t b0 = batch * (int64_t)B;
-  const int nb = (int)min<int64_t>(B, n_slots - b0);
+  const int nb = (int)max<int64_t>(0, min<int64_t>(B, n_slots - b0));
   const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
   const BatchView v = bb.view(batch);
+  if (tid < kMaxWorld) s_own[tid] = 0;
 
   // 1. the batch's triplets in slot order, keyed by local user row
   uint32_t key[IPT], val[IPT];
@@ -76,7 +70,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       int32_t u, i, j;
       bool sampled_ok = true;
       if (ru) {
-        u = ru[b0 + p];
+        u = ru[b0 + p] / world;
         i = ri[b0 + p];
         j = rj[b0 + p];
       } else {
@@ -125,37 +119,24 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     const int p = tid * IPT + k;
     s_i[p] = my_i[k];  // sorted order from here on
     s_j[p] = my_j[k];
-    if (key[k] != kNone) {
-      heads += (p == 0 || s_key[p - 1] != key[k]);
-      reinterpret_cast<int2*>(v.ij)[p] = make_int2(my_i[k], my_j[k]);
-    }
+    if (key[k] != kNone) heads += (p == 0 || s_key[p - 1] != key[k]);
   }
   int seg0 = 0, n_useg = 0, vpre = 0, nvalid = 0;
   Scan().exclusive_scan(heads, seg0, 0, n_useg, sscan, rocprim::plus<int>());
   __syncthreads();
   Scan().exclusive_scan(valid, vpre, 0, nvalid, sscan, rocprim::plus<int>());
+  bool uhead[IPT];
   {
     int s = seg0;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
-      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) v.useg[s++] = p;
+      uhead[k] = key[k] != kNone && (p == 0 || s_key[p - 1] != key[k]);
+      if (uhead[k]) v.useg[s++] = p;
     }
   }
   if (tid == 0) v.useg[n_useg] = nvalid;
-  __syncthreads();  // useg visible block-wide; s_i/s_j sorted; s_key free
-  {
-    int s = seg0;
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int p = tid * IPT + k;
-      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) {
-        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], s_i[p], s_j[p], 0, 0, 0);
-        ++s;
-      }
-    }
-  }
-  __syncthreads();  // s_key reads done before it is reused for the item keys
+  __syncthreads();  // useg visible block-wide; s_i/s_j sorted; s_key free for the item keys
 
   // 2. item references: r < nvalid -> i of sorted triplet r (sign -), else j of r - nvalid (sign +)
   uint32_t ik[IPT2], iv[IPT2];
@@ -166,12 +147,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     iv[k] = 0;
     if (r < 2 * nvalid) {
       const int p = r < nvalid ? r : r - nvalid;
-      ik[k] = (uint32_t)(r < nvalid ? s_i[p] : s_j[p]);
+      const uint32_t item = (uint32_t)(r < nvalid ? s_i[p] : s_j[p]);
+      ik[k] = (uint32_t)(item % (uint32_t)world) * (uint32_t)iloc + item / (uint32_t)world;
       iv[k] = ((uint32_t)p << 1) | (r < nvalid ? 0u : 1u);
     }
   }
   SortI().sort(ik, iv, sm.si, 0, item_bits);
-  __syncthreads();
+  __syncthreads();  // also: every read of s_i/s_j above is done
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) s_key[tid * IPT2 + k] = ik[k];
   __syncthreads();
@@ -187,15 +169,24 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   int iseg0 = 0, n_iseg = 0;
   Scan().exclusive_scan(iheads, iseg0, 0, n_iseg, sscan, rocprim::plus<int>());
   {
-    int s = iseg0;
+    int s = iseg0 - 1;  // segment of this thread's first ref if it is not a head
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
-      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) v.ioff[s++] = r;
+      if (ik[k] == kNone) continue;
+      if (r == 0 || s_key[r - 1] != ik[k]) {
+        ++s;
+        v.ioff[s] = r;
+        if (slots) {
+          v.ukey[s] = (int32_t)(ik[k] % (uint32_t)iloc);
+          atomicAdd(&s_own[ik[k] / (uint32_t)iloc], 1);
+        }
+      }
+      if (slots) (iv[k] & 1 ? s_j : s_i)[iv[k] >> 1] = s;  // triplet side -> its item slot
     }
   }
   if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
-  __syncthreads();  // ioff and refs visible block-wide
+  __syncthreads();  // ioff, refs, slots visible block-wide
   int nlong_mine = 0;
   {
     int s = iseg0;
@@ -225,8 +216,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
         const int end = v.ioff[s + 1];
         if (end - r > kLongSeg) {
-          if (lpre < kMaxLong)
-            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, 0, 0, 0, 0, 1);
+          if (lpre < kMaxLongItems)
+            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, s, 0, 0, 0, 1);
           else
             v.irec[(int64_t)s * kRec + 7] = 0;  // over the cap: served by the short path
           ++lpre;
@@ -235,11 +226,27 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       }
     }
   }
+
+  // 3. triplet records, now that s_i/s_j hold the final item rows (world 1) or slots
+  {
+    int s = seg0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
+      if (key[k] == kNone) continue;
+      reinterpret_cast<int2*>(v.ij)[p] = make_int2(s_i[p], s_j[p]);
+      if (uhead[k]) {
+        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], s_i[p], s_j[p], 0, 0, 0);
+        ++s;
+      }
+    }
+  }
+  if (tid < world && slots) v.own[tid] = s_own[tid];
   if (tid == 0) {
     v.meta[0] = nvalid;
     v.meta[1] = n_useg;
     v.meta[2] = n_iseg;
-    v.meta[3] = min(n_long, kMaxLong);
+    v.meta[3] = min(n_long, kMaxLongItems);
   }
 }
 
@@ -251,19 +258,22 @@ static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
 
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
-                         int64_t u_rows, int64_t i_rows, BatchBuf bb, int32_t* err, hipStream_t s) {
-  if (n_slots <= 0) return hipSuccess;
-  if (B <= 0 || B > kMaxSegBatch) return hipErrorInvalidValue;
-  const unsigned nb = (unsigned)((n_slots + B - 1) / B);
-  const int ub = bits_for(u_rows), ib = bits_for(i_rows);
+                         int64_t u_rows, int64_t i_rows, int world, bool slots, int64_t n_batches,
+                         BatchBuf bb, int32_t* err, hipStream_t s) {
+  if (n_batches <= 0) return hipSuccess;
+  if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
+  const int64_t iloc = (i_rows + world - 1) / world;
+  if ((uint64_t)iloc * (uint64_t)world >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const int ub = bits_for(u_rows), ib = bits_for(iloc * world);
   if (B <= kBuildThreads * 4)
-    k_build_batches<4><<<nb, kBuildThreads, 0, s>>>(a, epoch, first_slot, n_slots, B, ru, ri, rj,
-                                                     u_rows, i_rows, ub, ib, bb, err);
+    k_build_batches<4><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
+        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0, ub,
+        ib, bb, err);
   else
-    k_build_batches<8><<<nb, kBuildThreads, 0, s>>>(a, epoch, first_slot, n_slots, B, ru, ri, rj,
-                                                     u_rows, i_rows, ub, ib, bb, err);
+    k_build_batches<8><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
+        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0, ub,
+        ib, bb, err);
   return hipGetLastError();
 }
 
 }  // namespace bprmf
-

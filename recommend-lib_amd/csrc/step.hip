@@ -44,11 +44,14 @@ static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, floa
                      fmaf(-lr, fmaf(wd, v.z, g.z), v.z), fmaf(-lr, fmaf(wd, v.w, g.w), v.w));
 }
 
-template <int G4, int S>
+// SH (sharded): i/j are slots of item_rows, the rows the owners sent for this step, already
+// brought to step t-1 by the owner (no stamps here).
+template <int G4, int S, bool SH>
 __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
                                                       int ld, const int32_t* __restrict__ tbase,
                                                       int step, double* loss,
-                                                      float* __restrict__ contrib) {
+                                                      float* __restrict__ contrib,
+                                                      const float* __restrict__ item_rows) {
   const int sub = threadIdx.x & (G4 - 1);
   const int s = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
   // independent loads: the record (allocated for every s < B), the segment count, the step base
@@ -74,16 +77,17 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
     for (int p = beg; p < end; ++p) {
       int2 nxt = make_int2(0, 0);
       if (p + 1 < end) nxt = reinterpret_cast<const int2*>(bv.ij)[p + 1];
-      const float* qi = Q.W + (int64_t)i * ld + 4 * sub;
-      const float* qj = Q.W + (int64_t)j * ld + 4 * sub;
+      const float* qbase = SH ? item_rows : Q.W;
+      const float* qi = qbase + (int64_t)i * ld + 4 * sub;
+      const float* qj = qbase + (int64_t)j * ld + 4 * sub;
       float4 vi[S], vj[S];
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         vi[k] = ld4(qi + 4 * G4 * k);
         vj[k] = ld4(qj + 4 * G4 * k);
       }
-      const float fi = decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
-      const float fj = decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
+      const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
+      const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
       float di = 0.f, dj = 0.f;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
@@ -141,11 +145,25 @@ static __device__ __forceinline__ void acc_ref(float4 (&g)[S], const float4 (&ro
   for (int k = 0; k < S; ++k) g[k] = fma4(sgn, row[k], g[k]);
 }
 
-template <int G4, int S>
+// finish one item segment: apply (single GPU) or hand the gradient to the exchange (sharded)
+template <int G4, int S, bool SH>
+static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int slot,
+                                                   const float4 (&g)[S], const Hyper& hp, int ld,
+                                                   int32_t t, int sub, float* __restrict__ grads) {
+  if (SH) {
+    float* o = grads + (int64_t)slot * ld + 4 * sub;
+#pragma unroll
+    for (int k = 0; k < S; ++k) st4(o + 4 * G4 * k, g[k]);
+  } else {
+    apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+  }
+}
+
+template <int G4, int S, bool SH>
 __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyper hp, int ld,
                                                       const int32_t* __restrict__ tbase, int step,
                                                       const float* __restrict__ contrib,
-                                                      int long_blocks) {
+                                                      int long_blocks, float* __restrict__ grads) {
   constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
@@ -194,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyp
         }
         g[k] = acc;
       }
-      apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+      finish_item<G4, S, SH>(Q, item, r0.w, g, hp, ld, t, sub, grads);
     }
     return;
   }
@@ -237,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyp
     }
   }
   (void)row;
-  apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+  finish_item<G4, S, SH>(Q, item, s, g, hp, ld, t, sub, grads);
 }
 
 // Expand BODY for every instantiated float4 geometry (G4_, S_).
@@ -257,10 +275,16 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyp
   }
 
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib, hipStream_t s) {
+                     const int32_t* tbase, int step, double* loss, float* contrib,
+                     const float* item_rows, hipStream_t s) {
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
-    k_user_step<G4_, S_><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss, contrib);
+    if (item_rows)
+      k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
+                                                           contrib, item_rows);
+    else
+      k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
+                                                            contrib, nullptr);
   }));
   return hipGetLastError();
 }
@@ -268,13 +292,18 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg + 1)); }
 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, const float* contrib, hipStream_t s) {
+                     const int32_t* tbase, int step, const float* contrib, float* grads,
+                     hipStream_t s) {
   const int long_blocks = item_long_blocks(B);
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks =
         (unsigned)(long_blocks + (2LL * B + kBlock / G4_ - 1) / (kBlock / G4_));
-    k_item_step<G4_, S_><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
-                                                   long_blocks);
+    if (grads)
+      k_item_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
+                                                           long_blocks, grads);
+    else
+      k_item_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
+                                                            long_blocks, nullptr);
   }));
   return hipGetLastError();
 }

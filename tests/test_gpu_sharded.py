@@ -1,0 +1,103 @@
+"""GPU: the sharded step kernels (bprmf_dist_*) through the real orchestrator, several shards on
+the one GPU of the box stepped by threads (ThreadComm in place of RCCL).  G shards stepping their
+users' share of each global batch == one single-GPU step on the whole global batch."""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import bpr_oracle as O
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+
+U, I, D = 301, 157, 128
+
+
+def _run_threads(rl, world, fn):
+    grp = rl.sharded.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            out[r] = fn(rl.sharded.ThreadComm(grp, r), r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_replay_equals_single_gpu_global_batch(rl, world):
+    g = np.random.default_rng(world)
+    P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, D))).astype(np.float32)
+    GB, steps = 512, 6
+    batches = []
+    for k in range(steps):
+        u, i, j = g.integers(0, U, GB), g.integers(0, I, GB), g.integers(0, I, GB)
+        i[:40] = 7  # hot item (> kLongSeg references)
+        batches.append((u, i, j))
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=GB, device=0, comm=comm)
+        m.set_weights(sh.shard_rows(P0, r, world), sh.shard_rows(Q0, r, world))
+        m.plan_replay(batches)
+        for k in range(steps):
+            m.step_replay(k)
+        return m.get_weights()
+
+    parts = _run_threads(rl, world, fn)
+    P = sh.unshard_rows([p[0] for p in parts], U)
+    Q = sh.unshard_rows([p[1] for p in parts], I)
+    Pr, Qr = P0.copy(), Q0.copy()
+    for u, i, j in batches:
+        O.bpr_step_dense(Pr, Qr, u, i, j, 0.05, 0.01)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+
+
+def test_sharded_sampler_training(rl, golden):
+    """Sampler mode over 2 shards: each shard's batches are its own users' triplets, bit-exact with
+    the oracle sampler for that shard; training reduces the loss."""
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    Uu, Ii = int(f["U"]), int(f["I"])
+    world, B, seed = 2, 2048, 31
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(Uu, Ii, 32, batch_size=B, seed=seed, device=0, comm=comm)
+        S = m.set_train(pos)
+        losses = []
+        for e in range(3):
+            tot = 0.0
+            for s in range(S):
+                tot += m.step(e, s, want_loss=True)
+            losses.append(tot)
+        return S, losses
+
+    out = _run_threads(rl, world, fn)
+    S = out[0][0]
+    for r in range(world):
+        mine = pos[pos[:, 0] % world == r]
+        assert S >= (len(mine) * 4 + B - 1) // B
+        l = out[r][1]
+        assert l[-1] < l[0], l
+    # shard 1's sampler == the oracle's (shard seed = seed + rank * 0x9E3779B97F4A7C15)
+    m1 = rl.BPRMF(Uu, Ii, 8, batch_size=B, seed=seed, rank=1, world=world)
+    m1.set_train(pos)
+    mine = pos[pos[:, 0] % world == 1]
+    indptr, indices = O.build_csr(mine[:, 0], mine[:, 1], Uu)
+    got = m1.sample(0, 0, 1000)
+    want = C.sample(mine[:, 0], mine[:, 1], indptr, indices, Ii, 4,
+                    (seed + 0x9E3779B97F4A7C15) & (2**64 - 1), 0, 0, 1000)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)

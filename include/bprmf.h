@@ -60,11 +60,19 @@ typedef struct {
 } bprmf_stats;
 
 /* live kernel timing (HIP events around every launch of each kind while enabled) */
-/* kinds: sample/build, step kernel 1 (users), step kernel 2 (items), owner-side item update */
-enum { BPRMF_KPROF_SAMPLE = 0, BPRMF_KPROF_FWD_SCATTER = 1, BPRMF_KPROF_APPLY = 2, BPRMF_KPROF_OWNER = 3, BPRMF_KPROF_KINDS = 4 };
+/* kinds: sample/build, step kernel 1 (users), step kernel 2 (items), owner-side item update, and
+ * whole steps replayed from a captured graph (count = steps, ms = their summed device time) */
+enum {
+  BPRMF_KPROF_SAMPLE = 0,
+  BPRMF_KPROF_FWD_SCATTER = 1,
+  BPRMF_KPROF_APPLY = 2,
+  BPRMF_KPROF_OWNER = 3,
+  BPRMF_KPROF_STEPS = 4,
+  BPRMF_KPROF_KINDS = 5
+};
 typedef struct {
-  int64_t count[4];     /* launches recorded per kind */
-  double ms[4];         /* summed device time per kind (ms) */
+  int64_t count[8];     /* launches (steps for BPRMF_KPROF_STEPS) recorded per kind */
+  double ms[8];         /* summed device time per kind (ms) */
 } bprmf_kprof;
 
 typedef struct bprmf_handle bprmf_handle;

@@ -34,9 +34,9 @@ class Stats(ctypes.Structure):
 
 
 class KProf(ctypes.Structure):
-    _fields_ = [("count", ctypes.c_int64 * 4), ("ms", ctypes.c_double * 4)]
+    _fields_ = [("count", ctypes.c_int64 * 8), ("ms", ctypes.c_double * 8)]
 
-    KINDS = ("sample", "user_step", "item_step", "owner_apply")
+    KINDS = ("sample", "user_step", "item_step", "owner_apply", "step_graph")
 
     def as_dict(self):
         return {k: dict(count=int(self.count[n]), ms=float(self.ms[n])) for n, k in enumerate(self.KINDS)}

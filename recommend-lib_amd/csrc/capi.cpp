@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -39,6 +40,12 @@ static int fail(int code, const char* fmt, ...) {
     hipError_t e_ = (x);                                                             \
     if (e_ != hipSuccess) return fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
+
+struct StepGraph {  // a captured chunk of step launches (launch_step_graph)
+  int64_t nb = 0;
+  hipGraphExec_t exec = nullptr;
+};
+constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step
 
 struct bprmf_handle {
   bprmf_config cfg;
@@ -75,12 +82,20 @@ struct bprmf_handle {
   std::vector<hipEvent_t> prof_pool;
   size_t prof_used = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_rec[BPRMF_KPROF_KINDS];
+  int64_t prof_weight[BPRMF_KPROF_KINDS] = {};  // extra units per pair (a step-graph pair = nb steps)
+  // captured step sequences (BPRMF_NO_GRAPH=1 disables: eager launches)
+  bool use_graphs = true;
+  std::vector<StepGraph> graphs;
 };
 
+static void drop_graphs(bprmf_handle* h);
+
+// Profiling events skip the system-scope fence a default event record performs (an L2 write-back
+// that would otherwise land inside the measured interval: +2 us per kernel measured on gfx950).
 static hipEvent_t prof_event(bprmf_handle* h) {
   if (h->prof_used == h->prof_pool.size()) {
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     h->prof_pool.push_back(e);
   }
   return h->prof_pool[h->prof_used++];
@@ -91,8 +106,8 @@ struct ProfScope {
   bprmf_handle* h;
   int kind;
   hipEvent_t a = nullptr;
-  ProfScope(bprmf_handle* hh, int k) : h(hh), kind(k) {
-    if (h->prof_on && (a = prof_event(h))) hipEventRecord(a, h->stream);
+  ProfScope(bprmf_handle* hh, int k, bool sampled = true) : h(hh), kind(k) {
+    if (h->prof_on && sampled && (a = prof_event(h))) hipEventRecord(a, h->stream);
   }
   ~ProfScope() {
     if (!a) return;
@@ -197,6 +212,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   h->stream = h->own_stream;
+  h->use_graphs = getenv("BPRMF_NO_GRAPH") == nullptr;
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
     bprmf_destroy(h);
     return fail(BPRMF_E_HIP, "hipEventCreate failed");
@@ -246,6 +262,7 @@ int bprmf_destroy(bprmf_handle* h) {
                   h->d_batch, h->d_contrib, h->d_tbase};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  drop_graphs(h);
   for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
@@ -421,6 +438,7 @@ static int ensure_seg(bprmf_handle* h, int64_t n_batches) {
     if (int r = dalloc(&h->d_tbase, 1)) return r;
   }
   if (n_batches <= h->batch_cap) return 0;
+  drop_graphs(h);  // captured graphs point into the old batch buffer
   if (h->d_batch) HIPCHK(hipFree(h->d_batch));
   h->d_batch = nullptr;
   h->batch_cap = 0;
@@ -431,6 +449,51 @@ static int ensure_seg(bprmf_handle* h, int64_t n_batches) {
 
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done);
+
+// The 2*nb step launches of a chunk (user_step k, item_step k; k < nb) captured once into a
+// hipGraph and replayed: every argument is fixed (batch k's records at a fixed offset, t read from
+// d_tbase), so a replay costs one host call instead of 2*nb launches.
+static void drop_graphs(bprmf_handle* h) {
+  for (auto& ge : h->graphs)
+    if (ge.exec) hipGraphExecDestroy(ge.exec);
+  h->graphs.clear();
+}
+
+static int launch_step_graph(bprmf_handle* h, int64_t nb) {
+  StepGraph* ge = nullptr;
+  for (auto& g : h->graphs)
+    if (g.nb == nb) ge = &g;
+  if (!ge) {
+    if (h->graphs.size() >= 8) drop_graphs(h);
+    StepGraph ng;
+    ng.nb = nb;
+    const int B = h->cfg.batch_size;
+    const BatchBuf bb{h->d_batch, B};
+    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipSuccess;
+    for (int64_t k = 0; k < nb && e == hipSuccess; ++k) {
+      const BatchView v = bb.view(k);
+      e = user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss, h->d_contrib,
+                    nullptr, h->stream);
+      if (e == hipSuccess)
+        e = item_step(h->geom, v, B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
+                      h->stream);
+    }
+    hipGraph_t graph = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+    if (e != hipSuccess || e2 != hipSuccess) {
+      if (graph) hipGraphDestroy(graph);
+      return fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e != hipSuccess ? e : e2));
+    }
+    e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    if (e != hipSuccess) return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
+    h->graphs.push_back(ng);
+    ge = &h->graphs.back();
+  }
+  HIPCHK(hipGraphLaunch(ge->exec, h->stream));
+  return 0;
+}
 
 // One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler
 // (ru == nullptr) or replayed device ids ru/ri/rj[0..n).  Segmented path for B <= kMaxSegBatch:
@@ -463,17 +526,36 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
                          h->cfg.item_num, 1, false, nb, bb, h->d_err, h->stream));
   }
-  for (int64_t k = 0; k < nb; ++k) {
-    const BatchView v = bb.view(k);
-    {
-      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
-      HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                       h->d_contrib, nullptr, h->stream));
+  if (h->use_graphs) {
+    // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
+    // the step kernels and their gaps; per-kernel splits come from rocprofv3)
+    hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
+    if (ea) HIPCHK(hipEventRecord(ea, h->stream));
+    if (int r = launch_step_graph(h, nb)) return r;
+    if (ea) {
+      hipEvent_t eb = prof_event(h);
+      if (eb) {
+        HIPCHK(hipEventRecord(eb, h->stream));
+        h->prof_rec[BPRMF_KPROF_STEPS].push_back({ea, eb});
+        h->prof_weight[BPRMF_KPROF_STEPS] += nb - 1;  // one pair covers nb steps
+      }
     }
-    {
-      ProfScope ps(h, BPRMF_KPROF_APPLY);
-      HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
-                       h->stream));
+  } else {
+    // eager; while profiling, an event pair brackets the kernels of every kProfStride-th step only,
+    // so the host stays ahead of the GPU and the events time the kernels, not launch latency
+    for (int64_t k = 0; k < nb; ++k) {
+      const BatchView v = bb.view(k);
+      const bool sampled = ((h->t + k) % kProfStride) == 0;
+      {
+        ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
+        HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
+                         h->d_contrib, nullptr, h->stream));
+      }
+      {
+        ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
+        HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
+                         h->stream));
+      }
     }
   }
   h->t += (int32_t)nb;
@@ -681,6 +763,7 @@ int bprmf_profile(bprmf_handle* h, int32_t enable) {
   HIPCHK(hipStreamSynchronize(h->stream));
   h->prof_on = enable != 0;
   h->prof_used = 0;
+  for (auto& w : h->prof_weight) w = 0;
   for (auto& v : h->prof_rec) v.clear();
   return 0;
 }
@@ -697,7 +780,7 @@ int bprmf_profile_read(bprmf_handle* h, bprmf_kprof* out) {
       HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
       total += ms;
     }
-    out->count[k] = (int64_t)h->prof_rec[k].size();
+    out->count[k] = (int64_t)h->prof_rec[k].size() + h->prof_weight[k];
     out->ms[k] = total;
   }
   return 0;

@@ -6,9 +6,10 @@
 
 namespace bprmf {
 
-// Row geometry: a row of D floats is stored with stride ld = G*EPL (zero padded); a group of G
-// lanes owns one row, lane `sub` holds elements sub + G*k, k < EPL.  D <= 64: G = next_pow2(D),
-// EPL = 1 (64/G rows per wave); D > 64: G = 64 (one row per wave), EPL = ceil(D/64).
+// Row geometry: a row of D floats is stored with stride ld (zero padded).  Two lane layouts share
+// that stride: float4 (segmented step, step.hip): G4 = next_pow2(ceil(D/4)) <= 64 lanes per row,
+// S stripes, ld = 4*G4*S; dword (atomic path, owner-side kernels, kernels.hip): G lanes per row,
+// lane `sub` holds elements sub + G*k, k < EPL, with G*EPL = ld.
 // per-wave loss partial slots of the step kernels: grid <= kMaxGridBlocks blocks of 4 waves
 constexpr int kMaxGridBlocks = 256 * 8;
 constexpr int kLossSlots = kMaxGridBlocks * 4;
@@ -126,10 +127,6 @@ hipError_t flush(const Geom& g, Table W, const Hyper& hp, int32_t T, hipStream_t
 // --- sharded step phases ---
 hipError_t gather_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
                        int32_t t, float* out, int32_t* err, hipStream_t s);
-hipError_t dist_fwd_scatter(const Geom& g, const int32_t* ul, const int32_t* si, const int32_t* sj,
-                            int64_t n, Table P, const float* item_rows, float* item_grads,
-                            int64_t n_slots, const Hyper& hp, int32_t t, double* loss,
-                            int32_t* err, hipStream_t s);
 hipError_t add_rows(const Geom& g, Table W, const int32_t* rows, const float* grads, int64_t n,
                     int32_t* err, hipStream_t s);
 hipError_t apply_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,

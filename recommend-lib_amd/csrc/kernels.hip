@@ -77,12 +77,7 @@ __global__ __launch_bounds__(kBlock) void k_init_normal(float* __restrict__ W, i
 // ------------------------------------------------------------------------------------------------
 // Training step kernels
 // ------------------------------------------------------------------------------------------------
-struct RowPtrs {
-  const float* w;
-  float f;
-};
-
-// K1 — fused gather (with pending decay) + 2 dots + sigmoid + gradient scatter.
+// Atomic path (batches larger than kMaxSegBatch): K1 — fused gather (with pending decay) + 2 dots + sigmoid + gradient scatter.
 //   reads  3 rows + 3 stamps + 3 ids per triplet;  writes 3 rows of f32 atomic adds into G.
 template <int G, int EPL>
 __global__ __launch_bounds__(kBlock) void k_fwd_scatter(const int32_t* __restrict__ tu,
@@ -292,59 +287,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(Table T, const int32_t* 
   }
 }
 
-// requester side: local users vs received item rows; item grads go to a slot buffer [n_slots, ld]
-template <int G, int EPL>
-__global__ __launch_bounds__(kBlock) void k_dist_fwd_scatter(
-    const int32_t* __restrict__ ul, const int32_t* __restrict__ si, const int32_t* __restrict__ sj,
-    int64_t n, Table P, const float* __restrict__ rows, float* __restrict__ grads, int64_t n_slots,
-    Hyper hp, int ld, int32_t t, double* loss, int32_t* __restrict__ err) {
-  const int sub = threadIdx.x & (G - 1);
-  const int64_t ngroups = (int64_t)gridDim.x * (kBlock / G);
-  float lsum = 0.f;
-  for (int64_t b = blockIdx.x * (int64_t)(kBlock / G) + threadIdx.x / G; b < n; b += ngroups) {
-    const int32_t u = ul[b], a = si[b], c2 = sj[b];
-    if ((uint64_t)u >= (uint64_t)P.rows || (uint64_t)a >= (uint64_t)n_slots ||
-        (uint64_t)c2 >= (uint64_t)n_slots) {
-      if (sub == 0) atomicOr(err, 1);
-      continue;
-    }
-    const float fu = decay_pow(hp.log2a, t - 1 - P.stamp[u]);
-    const float* pu = P.W + (int64_t)u * ld + sub;
-    const float* qi = rows + (int64_t)a * ld + sub;
-    const float* qj = rows + (int64_t)c2 * ld + sub;
-    float vu[EPL], vi[EPL], vj[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      vu[k] = pu[G * k];
-      vi[k] = qi[G * k];
-      vj[k] = qj[G * k];
-    }
-    float di = 0.f, dj = 0.f;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      vu[k] *= fu;
-      di = fmaf(vu[k], vi[k], di);
-      dj = fmaf(vu[k], vj[k], dj);
-    }
-    di = group_sum<G>(di);
-    dj = group_sum<G>(dj);
-    const float x = di - dj;
-    const float c = 1.0f / (1.0f + expf(x));
-    if (sub == 0) lsum += softplus(-x);
-    float* gu = P.G + (int64_t)u * ld + sub;
-    float* gi = grads + (int64_t)a * ld + sub;
-    float* gj = grads + (int64_t)c2 * ld + sub;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const float cu = c * vu[k];
-      atomicAdd(gu + G * k, -c * (vi[k] - vj[k]));
-      atomicAdd(gi + G * k, -cu);
-      atomicAdd(gj + G * k, cu);
-    }
-  }
-  wave_add_loss(loss, lsum);
-}
-
 // owner side: received item grads summed into the shard's accumulator
 template <int G, int EPL>
 __global__ __launch_bounds__(kBlock) void k_add_rows(Table T, const int32_t* __restrict__ rows,
@@ -454,16 +396,6 @@ hipError_t gather_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, c
   if (n <= 0) return hipSuccess;
   BPRMF_DISPATCH(g, (k_gather_rows<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(
                         W, rows, n, hp, g.ld, t, out, err)));
-  return hipGetLastError();
-}
-
-hipError_t dist_fwd_scatter(const Geom& g, const int32_t* ul, const int32_t* si, const int32_t* sj,
-                            int64_t n, Table P, const float* item_rows, float* item_grads,
-                            int64_t n_slots, const Hyper& hp, int32_t t, double* loss,
-                            int32_t* err, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  BPRMF_DISPATCH(g, (k_dist_fwd_scatter<G_, E_><<<grid_for(n, G_), kBlock, 0, s>>>(
-                        ul, si, sj, n, P, item_rows, item_grads, n_slots, hp, g.ld, t, loss, err)));
   return hipGetLastError();
 }
 

@@ -98,6 +98,26 @@ def test_step_vs_oracle_all_geometries(rl, d):
     np.testing.assert_allclose(Qg, Q, rtol=1e-5, atol=1e-6)
 
 
+def test_large_batch_atomic_path_vs_oracle(rl):
+    """batch_size > kMaxSegBatch (8192) takes the f32-atomic path (fwd_scatter + apply_refs)."""
+    g = np.random.default_rng(8)
+    U, I, d, B = 500, 300, 64, 10000
+    P0 = (0.05 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, d))).astype(np.float32)
+    m = _model(rl, U, I, d, B, lr=0.02, wd=0.01)
+    m.set_weights(P0, Q0)
+    P, Q = P0.copy(), Q0.copy()
+    u, i, j = g.integers(0, U, 3 * B), g.integers(0, I, 3 * B), g.integers(0, I, 3 * B)
+    st = m.train_triplets(u, i, j)
+    assert st["steps"] == 3
+    for s in range(3):
+        sl = slice(s * B, (s + 1) * B)
+        O.bpr_step_dense(P, Q, u[sl], i[sl], j[sl], 0.02, 0.01)
+    Pg, Qg = m.get_weights()
+    np.testing.assert_allclose(Pg, P, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Qg, Q, rtol=1e-5, atol=1e-6)
+
+
 def test_lazy_decay_equals_dense_decay(rl):
     """Rows untouched for many steps carry (1-lr*wd)^k exactly as the dense SGD would."""
     g = np.random.default_rng(0)

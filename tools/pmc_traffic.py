@@ -1,0 +1,67 @@
+"""Per-step L2<->fabric traffic of the step kernels from rocprofv3 PMC CSVs.
+
+  python tools/pmc_traffic.py KEY FETCH_DIR WRITE_DIR [--out profiles/pmc_traffic.json]
+
+FETCH_SIZE and WRITE_SIZE (KB per dispatch) are averaged per kernel over all dispatches; the step
+traffic is the sum over the step kernels (user_step + item_step; + owner-side kernels when
+sharded).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half the bytes
+of a wide coalesced (16 B/lane) read, so it is doubled; WRITE_SIZE is exact for 16-B/lane stores.
+Infinity-Cache hits are counted by these counters (they are L2-miss requests), so for tables that
+fit the 256 MiB MALL this is L2-miss traffic, not strictly DRAM bytes.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+STEP_KERNELS = ("k_user_step", "k_item_step", "k_gather_rows", "k_add_rows", "k_apply_rows")
+
+
+def per_kernel(d, counter):
+    acc = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            for k in STEP_KERNELS:
+                if f"bprmf::{k}" in name:
+                    acc[k].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("key")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--factor", type=int, default=128)
+    a = ap.parse_args()
+    fetch = per_kernel(a.fetch_dir, "FETCH_SIZE")
+    write = per_kernel(a.write_dir, "WRITE_SIZE")
+    kernels = {k: dict(fetch_kb_raw=round(fetch.get(k, 0.0), 1), write_kb=round(write.get(k, 0.0), 1),
+                       bytes=round((2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024))
+               for k in sorted(set(fetch) | set(write))}
+    total = sum(v["bytes"] for v in kernels.values())
+    alg = a.batch * (24 * a.factor + 12)
+    entry = dict(hbm_bytes_per_step=total, algorithmic_bytes_per_step=alg,
+                 ratio_to_algorithmic=round(total / alg, 3), kernels=kernels,
+                 method="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); "
+                        "bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE halving); "
+                        "L2-miss traffic incl. Infinity-Cache hits")
+    data = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            data = json.load(f)
+    data[a.key] = entry
+    with open(a.out, "w") as f:
+        json.dump(data, f, indent=1)
+    print(json.dumps({a.key: entry}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

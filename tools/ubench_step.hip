@@ -184,7 +184,7 @@ int main(int argc, char** argv) {
   BatchBuf bb{dbatch, B};
   Hyper hp{0.01f, 0.001f, 1.0 - 1e-5, std::log2(1.0 - 1e-5)};
   float tb = time_loop(1, [&](int) {
-    CK(build_batches(sa, 0, 0, (int64_t)S * B, B, du, di, dj, U, I, bb, derr, 0));
+    CK(build_batches(sa, 0, 0, (int64_t)S * B, B, du, di, dj, U, I, 1, false, S, bb, derr, 0));
   });
   std::vector<int32_t> meta(4);
   CK(hipMemcpy(meta.data(), bb.view(0).meta, 16, hipMemcpyDeviceToHost));
@@ -210,25 +210,54 @@ int main(int argc, char** argv) {
            }));
   }
   printf("K1 user_step:                     %7.2f us\n", time_loop(S, [&](int k) {
-           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, 0));
+           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, nullptr, 0));
          }));
   printf("K2 item_step:                     %7.2f us\n", time_loop(S, [&](int k) {
-           CK(item_step(g, bb.view(k % S), B, Q, hp, dt, k, contrib, 0));
+           CK(item_step(g, bb.view(k % S), B, Q, hp, dt, k, contrib, nullptr, 0));
          }));
   if (g.G4 == 32 && g.S == 1) {
     const unsigned sb = (unsigned)((2 * B + 7) / 8);
     printf("K2 short segments only (timing):  %7.2f us\n", time_loop(S, [&](int k) {
-             k_item_step<32, 1><<<sb, 256>>>(bb.view(k % S), Q, hp, ld, dt, k, contrib, 0);
+             k_item_step<32, 1, false><<<sb, 256>>>(bb.view(k % S), Q, hp, ld, dt, k, contrib, 0, nullptr);
            }));
     const int lb = item_long_blocks(B);
     printf("K2 long segments only (timing):   %7.2f us\n", time_loop(S, [&](int k) {
-             k_item_step<32, 1><<<lb, 256>>>(bb.view(k % S), Q, hp, ld, dt, k, contrib, lb);
+             k_item_step<32, 1, false><<<lb, 256>>>(bb.view(k % S), Q, hp, ld, dt, k, contrib, lb, nullptr);
            }));
   }
   printf("K1+K2 step:                       %7.2f us\n", time_loop(S, [&](int k) {
-           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, 0));
-           CK(item_step(g, bb.view(k % S), B, Q, hp, dt, k, contrib, 0));
+           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, nullptr, 0));
+           CK(item_step(g, bb.view(k % S), B, Q, hp, dt, k, contrib, nullptr, 0));
          }));
+  // per-kernel event pairs (every 16th step) vs the loop average: which event flavour agrees?
+  for (unsigned flags : {0u, (unsigned)hipEventDisableSystemFence, (unsigned)hipEventReleaseToDevice}) {
+    std::vector<hipEvent_t> ev(4 * S);
+    for (auto& x : ev) CK(hipEventCreateWithFlags(&x, flags));
+    CK(hipDeviceSynchronize());
+    int np = 0;
+    for (int k = 0; k < S; ++k) {
+      const bool smp = (k % 16) == 0;
+      if (smp) CK(hipEventRecord(ev[4 * np], 0));
+      CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, nullptr, 0));
+      if (smp) CK(hipEventRecord(ev[4 * np + 1], 0));
+      if (smp) CK(hipEventRecord(ev[4 * np + 2], 0));
+      CK(item_step(g, bb.view(k % S), B, Q, hp, dt, k, contrib, nullptr, 0));
+      if (smp) CK(hipEventRecord(ev[4 * np + 3], 0));
+      np += smp;
+    }
+    CK(hipDeviceSynchronize());
+    double a = 0, b2 = 0;
+    for (int p = 0; p < np; ++p) {
+      float x, y;
+      CK(hipEventElapsedTime(&x, ev[4 * p], ev[4 * p + 1]));
+      CK(hipEventElapsedTime(&y, ev[4 * p + 2], ev[4 * p + 3]));
+      a += x;
+      b2 += y;
+    }
+    printf("events flags=0x%08x: user_step %.2f us  item_step %.2f us (%d samples)\n", flags,
+           a * 1e3 / np, b2 * 1e3 / np, np);
+    for (auto& x : ev) CK(hipEventDestroy(x));
+  }
   int32_t e = 0;
   CK(hipMemcpy(&e, derr, 4, hipMemcpyDeviceToHost));
   printf("err flag %d\n", e);

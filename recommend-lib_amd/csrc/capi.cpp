@@ -5,8 +5,9 @@
 //   Q  [local items, ld] fp32 + grad accumulator + int32 stamp      (embed_item.weight)
 //   positives of its users (features order) and their sorted CSR     (BPRData.features / train_mat)
 //   a triplet chunk buffer [chunk, 3] int32 filled by the sampler    (BPRData.features_fill)
-// A training step is two launches: fwd_scatter (gather, dots, sigmoid, f32-atomic grad scatter)
-// then apply_refs (claim each referenced row once via its stamp, lazy decay + SGD update).
+// Training runs in chunks of steps: one k_build_batches launch lays out every batch of the chunk
+// (segment.hip), then each step is k_user_step + k_item_step (step.hip), replayed from a captured
+// hipGraph.  Batches above kMaxSegBatch use the f32-atomic pair fwd_scatter + apply_refs.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>

@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded RCCL path even at one rank (exercises it on one GPU)")
+    ap.add_argument("--python-orchestration", action="store_true",
+                    help="sharded: per-step Python orchestration over torch.distributed instead of "
+                         "the library's runner")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,11 +135,21 @@ def main():
         m = rl.ShardedBPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed,
                             device=local)
         n_steps = m.set_train(pos)
+        if a.python_orchestration:
+            def run(first, k):
+                for s in range(first, first + k):
+                    e, st = divmod(s, n_steps)
+                    m.step(e, st)
+        else:  # the library's runner: chunks of steps, RCCL exchanges issued from C++
+            m.attach_runner("rccl")
 
-        def run(first, k):
-            for s in range(first, first + k):
-                e, st = divmod(s, n_steps)
-                m.step(e, st)
+            def run(first, k):
+                done = 0
+                while done < k:
+                    e, s = divmod(first + done, n_steps)
+                    c = min(k - done, n_steps - s)
+                    m.train_steps(e, s, c)
+                    done += c
 
     def timed(first, k):
         if dist:
@@ -168,7 +181,10 @@ def main():
         roof = None
         if kp and (kp["step_graph"]["count"] or kp["user_step"]["count"]):
             us = {k: v["ms"] / v["count"] * 1e3 for k, v in kp.items() if v["count"]}
-            if "step_graph" in us:  # events around graph replays of whole steps (GPU-bound)
+            if "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
+                step_us, what = us["step_graph"], ("sharded step: owner gather + row exchange + "
+                                                   "user_step + item_step + grad exchange + owner apply")
+            elif "step_graph" in us:  # events around graph replays of whole steps (GPU-bound)
                 step_us, what = us["step_graph"], "step graph: user_step + item_step (+ their gap)"
             else:  # eager (sharded): events around the two kernels of sampled steps
                 step_us, what = us["user_step"] + us["item_step"], "user_step + item_step"

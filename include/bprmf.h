@@ -167,6 +167,25 @@ int bprmf_dist_sample_dev(bprmf_handle* h, uint32_t epoch, int64_t first, int64_
 /* row stride (floats) of device row buffers used by the dist_* exchange functions */
 int bprmf_row_stride(bprmf_handle* h, int32_t* ld);
 
+/* ---- sharded runner: whole chunks of sharded steps driven by the library ------------------ */
+/* The same step as the phases above, with the exchanges issued by the library: no host round
+ * trip per step.  Transport: an RCCL communicator the handle owns (rank 0 makes the 128-byte
+ * unique id, the caller broadcasts it, every rank calls bprmf_dist_init_rccl), or `loopback`:
+ * handles of ONE process with the same group key exchange through device copies (tests; one host
+ * thread per handle).  Steps are global: every rank runs the same (epoch, first_step, n_steps),
+ * steps past a shard's own epoch are empty for it. */
+int bprmf_dist_unique_id(uint8_t* id128);
+int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id128);
+int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group);
+/* Steps [first_step, first_step+n_steps) of `epoch` from the device sampler (BPRMFRecommender.py:
+ * 157-178 over this shard's users); stats: this shard's triplets and loss. */
+int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                           bprmf_stats* stats);
+/* Replay: u/i/j[n_steps * batch_size] host triplets (global ids, this shard's users; u < 0 marks
+ * an empty slot), batch_size slots per step. */
+int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
+                            int64_t n_steps, bprmf_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,8 @@
 """Build libbprmf_amd.so in-tree for gfx950 with hipcc (no torch JIT cache, no pip install).
 
-The shared library is the product: kernels.hip (device code) + capi.cpp (the C ABI of
-include/bprmf.h).  It is placed next to this file so it travels to the GPU box with the repo.
+The shared library is the product: the gfx950 kernels (kernels.hip, segment.hip, step.hip,
+dist.hip) + the C ABI of include/bprmf.h (capi.cpp, dist.cpp; RCCL for the sharded runner).
+It is placed next to this file so it travels to the GPU box with the repo.
 """
 import os
 import subprocess
@@ -10,8 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libbprmf_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "capi.cpp")]
-HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h")] + [os.path.join(ROOT, "include", "bprmf.h")]
+SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "dist.hip", "capi.cpp", "dist.cpp")]
+HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h", "handle.h")] + [os.path.join(ROOT, "include", "bprmf.h")]
 ARCH = os.environ.get("BPRMF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -35,7 +36,7 @@ def build(force=False, verbose=False):
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
-           "-o", tmp] + SOURCES
+           "-o", tmp] + SOURCES + ["-L/opt/rocm/lib", "-lrccl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -19,14 +19,14 @@
 #include <string>
 #include <vector>
 
-#include "../../include/bprmf.h"
-#include "kernels.h"
+#include "handle.h"
 
 using namespace bprmf;
 
 static thread_local std::string g_err;
 
-static int fail(int code, const char* fmt, ...) {
+namespace bprmf {
+int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -35,65 +35,13 @@ static int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-#define HIPCHK(x)                                                                    \
-  do {                                                                               \
-    hipError_t e_ = (x);                                                             \
-    if (e_ != hipSuccess) return fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
-  } while (0)
-
-struct StepGraph {  // a captured chunk of step launches (launch_step_graph)
-  int64_t nb = 0;
-  hipGraphExec_t exec = nullptr;
-};
-constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step
-
-struct bprmf_handle {
-  bprmf_config cfg;
-  Geom geom;
-  Hyper hp;
-  int64_t U = 0, I = 0;  // local rows
-  Table P{}, Q{};
-  // training data
-  int64_t npos = 0;
-  int32_t* d_pos_u = nullptr;
-  int32_t* d_pos_i = nullptr;
-  int64_t* d_indptr = nullptr;
-  int32_t* d_indices = nullptr;
-  int feistel_h = 1;
-  uint32_t k0 = 0, k1 = 0;  // shard sampler key
-  // triplet chunk
-  int32_t* d_trip = nullptr;  // [3, cap]
-  // segmented step (batch_size <= kMaxSegBatch): per-batch sorted layouts + per-triplet c*P_u
-  int32_t* d_batch = nullptr;  // batch_cap * BatchBuf::stride_for(B) int32
-  int64_t batch_cap = 0;
-  float* d_contrib = nullptr;  // [B, ld]
-  int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
-  int64_t plan_steps = 0;      // batches of the current sharded plan
-  int64_t trip_cap = 0;
-  // misc device scalars
-  double* d_loss = nullptr;
-  int32_t* d_err = nullptr;
-  int32_t t = 0;  // optimizer steps taken
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // live per-kernel timing (bprmf_profile): event pairs around each launch of each kind
-  bool prof_on = false;
-  std::vector<hipEvent_t> prof_pool;
-  size_t prof_used = 0;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_rec[BPRMF_KPROF_KINDS];
-  int64_t prof_weight[BPRMF_KPROF_KINDS] = {};  // extra units per pair (a step-graph pair = nb steps)
-  // captured step sequences (BPRMF_NO_GRAPH=1 disables: eager launches)
-  bool use_graphs = true;
-  std::vector<StepGraph> graphs;
-};
+}  // namespace bprmf
 
 static void drop_graphs(bprmf_handle* h);
 
 // Profiling events skip the system-scope fence a default event record performs (an L2 write-back
 // that would otherwise land inside the measured interval: +2 us per kernel measured on gfx950).
-static hipEvent_t prof_event(bprmf_handle* h) {
+hipEvent_t bprmf::prof_event(bprmf_handle* h) {
   if (h->prof_used == h->prof_pool.size()) {
     hipEvent_t e = nullptr;
     if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
@@ -102,33 +50,8 @@ static hipEvent_t prof_event(bprmf_handle* h) {
   return h->prof_pool[h->prof_used++];
 }
 
-// record an event before (begin) / after a launch of `kind` when profiling is on
-struct ProfScope {
-  bprmf_handle* h;
-  int kind;
-  hipEvent_t a = nullptr;
-  ProfScope(bprmf_handle* hh, int k, bool sampled = true) : h(hh), kind(k) {
-    if (h->prof_on && sampled && (a = prof_event(h))) hipEventRecord(a, h->stream);
-  }
-  ~ProfScope() {
-    if (!a) return;
-    hipEvent_t b = prof_event(h);
-    if (!b) return;
-    hipEventRecord(b, h->stream);
-    h->prof_rec[kind].push_back({a, b});
-  }
-};
-
-static int set_dev(bprmf_handle* h) {
+int bprmf::set_dev(bprmf_handle* h) {
   HIPCHK(hipSetDevice(h->cfg.device));
-  return 0;
-}
-
-template <typename T>
-static int dalloc(T** p, int64_t count) {
-  *p = nullptr;
-  if (count <= 0) return 0;
-  HIPCHK(hipMalloc((void**)p, sizeof(T) * (size_t)count));
   return 0;
 }
 
@@ -139,7 +62,7 @@ static int64_t chunk_triplets(const bprmf_handle* h) {
   return steps * B;
 }
 
-static int ensure_trip(bprmf_handle* h, int64_t n) {
+int bprmf::ensure_trip(bprmf_handle* h, int64_t n) {
   if (n <= h->trip_cap) return 0;
   if (h->d_trip) HIPCHK(hipFree(h->d_trip));
   h->d_trip = nullptr;
@@ -149,7 +72,7 @@ static int ensure_trip(bprmf_handle* h, int64_t n) {
   return 0;
 }
 
-static int check_err_flag(bprmf_handle* h) {
+int bprmf::check_err_flag(bprmf_handle* h) {
   int32_t e = 0;
   HIPCHK(hipMemcpyAsync(&e, h->d_err, sizeof e, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -264,6 +187,7 @@ int bprmf_destroy(bprmf_handle* h) {
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
+  dist_free(h->dist);
   for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
@@ -377,7 +301,9 @@ int bprmf_epoch_size(bprmf_handle* h, int64_t* n_triplets, int64_t* n_steps) {
   return 0;
 }
 
-static SamplerArgs sampler_args(bprmf_handle* h) {
+}  // extern "C"
+
+SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   SamplerArgs a;
   a.pos_u = h->d_pos_u;
   a.pos_i = h->d_pos_i;
@@ -394,7 +320,7 @@ static SamplerArgs sampler_args(bprmf_handle* h) {
 }
 
 // sum of the per-wave loss slots (copied back once per call)
-static int read_loss(bprmf_handle* h, double* loss) {
+int bprmf::read_loss(bprmf_handle* h, double* loss) {
   std::vector<double> slots(kLossSlots);
   HIPCHK(hipMemcpyAsync(slots.data(), h->d_loss, sizeof(double) * kLossSlots, hipMemcpyDeviceToHost,
                         h->stream));
@@ -405,14 +331,14 @@ static int read_loss(bprmf_handle* h, double* loss) {
   return 0;
 }
 
-static int begin_call(bprmf_handle* h) {
+int bprmf::begin_call(bprmf_handle* h) {
   if (int r = set_dev(h)) return r;
   HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   return 0;
 }
 
-static int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
+int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   double loss = 0;
   if (int r = read_loss(h, &loss)) return r;
@@ -429,10 +355,9 @@ static int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   return 0;
 }
 
-// run steps over device triplets tu/ti/tj[0..n) in batches of B
-static bool seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSegBatch; }
+bool bprmf::seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSegBatch; }
 
-static int ensure_seg(bprmf_handle* h, int64_t n_batches) {
+int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   const int64_t B = h->cfg.batch_size;
   if (!h->d_contrib) {
     if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
@@ -447,6 +372,8 @@ static int ensure_seg(bprmf_handle* h, int64_t n_batches) {
   h->batch_cap = n_batches;
   return 0;
 }
+
+extern "C" {
 
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done);
@@ -525,7 +452,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
-                         h->cfg.item_num, 1, false, nb, bb, h->d_err, h->stream));
+                         h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream));
   }
   if (h->use_graphs) {
     // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
@@ -819,7 +746,7 @@ int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, (int)B, nullptr, nullptr,
-                         nullptr, h->U, h->cfg.item_num, h->cfg.world, true, n_steps, bb, h->d_err,
+                         nullptr, h->U, h->cfg.item_num, h->cfg.world, true, 0, n_steps, bb, h->d_err,
                          h->stream));
   }
   return dist_counts(h, n_steps, owner_counts);
@@ -848,7 +775,7 @@ int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, 
   HIPCHK(hipMemcpyAsync(tj, j, 4 * n, hipMemcpyHostToDevice, h->stream));
   const BatchBuf bb{h->d_batch, (int)B};
   HIPCHK(build_batches(sampler_args(h), 0, 0, n, (int)B, tu, ti, tj, h->U, h->cfg.item_num,
-                       h->cfg.world, true, n_steps, bb, h->d_err, h->stream));
+                       h->cfg.world, true, 0, n_steps, bb, h->d_err, h->stream));
   return dist_counts(h, n_steps, owner_counts);
 }
 

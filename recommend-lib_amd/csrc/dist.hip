@@ -1,0 +1,227 @@
+// dist.hip — kernels of the sharded (multi-GPU) step that run around the exchanges (dist.cpp).
+//
+// Users are owned by u % world and items by i % world.  A rank's batch of a step needs the rows
+// of the distinct items it references (its "requests", owner-major, as the builder orders item
+// segments).  Per chunk of n steps every rank exchanges its requests once:
+//   ids_send [world][n][cap]  the requests of step k to owner p (local rows), -1 padded
+//   ids_recv [world][n][cap]  what peer q requests from this rank (sorted ascending, -1 padded)
+// and the owner derives, per step, an apply plan: for each distinct requested row its leader
+// position (the lowest requesting peer) lists the positions of every peer's gradient for that
+// row, in peer order, so the owner's sum over peers has a fixed order (bitwise reproducible).
+// Per step: k_owner_gather (rows at step t-1, packed per requesting peer) -> exchange ->
+// K1/K2 (step.hip, sharded instantiations) -> exchange of per-slot gradients ->
+// k_owner_apply (fixed-order sum, lazy decay + SGD, one writer per row).
+// Reference semantics: the same SGD step as BPRMFRecommender.py:172-176 on the union batch.
+#include "device_common.h"
+
+namespace bprmf {
+
+static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// largest per-owner request count of the chunk (the exchange capacity), max-reduced into *cap
+__global__ void k_own_max(BatchBuf bb, int64_t n, int world, int32_t* __restrict__ cap) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= n * world) return;
+  const int32_t c = bb.view(x / world).own[x % world];
+  if (c > 0) atomicMax(cap, c);
+}
+
+// ids_send[p][k][idx] = request idx of step k to owner p (its local row), -1 past the count
+__global__ void k_pack_ids(BatchBuf bb, int64_t n, int world, int cap,
+                           int32_t* __restrict__ ids_send) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= (int64_t)world * n * cap) return;
+  const int idx = (int)(x % cap);
+  const int64_t k = (x / cap) % n;
+  const int p = (int)(x / ((int64_t)cap * n));
+  const BatchView v = bb.view(k);
+  int pre = 0;
+  for (int o = 0; o < p; ++o) pre += v.own[o];
+  ids_send[x] = idx < v.own[p] ? v.ukey[pre + idx] : -1;
+}
+
+// first position of `row` in an ascending, -1 padded list (compared unsigned: pads sort last)
+static __device__ __forceinline__ int find_row(const int32_t* __restrict__ list, int cap, uint32_t row) {
+  int lo = 0, hi = cap;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((uint32_t)list[mid] < row) lo = mid + 1; else hi = mid;
+  }
+  return (lo < cap && (uint32_t)list[lo] == row) ? lo : -1;
+}
+
+// apply plan: aplan[k][p][idx][q] = q*cap + (position of row in peer q's list of step k), -1 if q
+// does not request it; a position whose row an earlier peer also requests (or a pad) gets
+// aplan[..][0] = -2 (not a leader: skipped by k_owner_apply).
+__global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
+                             int32_t* __restrict__ aplan) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= n * world * (int64_t)cap) return;
+  const int idx = (int)(x % cap);
+  const int p = (int)((x / cap) % world);
+  const int64_t k = x / ((int64_t)cap * world);
+  int32_t* rec = aplan + x * world;
+  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+  if (row < 0) {
+    rec[0] = -2;
+    return;
+  }
+  for (int q = 0; q < p; ++q)
+    if (find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row) >= 0) {
+      rec[0] = -2;
+      return;
+    }
+  for (int q = 0; q < world; ++q) {
+    int pos = -1;
+    if (q == p) pos = idx;
+    else if (q > p) pos = find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row);
+    rec[q] = pos < 0 ? -1 : q * cap + pos;
+  }
+}
+
+// owner: rows requested by every peer for step k, brought to step t-1, packed [world][cap][ld]
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t* __restrict__ ids_recv,
+                                                        int64_t n, int world, int cap, int k,
+                                                        Hyper hp, int ld,
+                                                        const int32_t* __restrict__ tbase,
+                                                        float* __restrict__ rows_send) {
+  const int sub = threadIdx.x & (G4 - 1);
+  const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
+  if (x >= (int64_t)world * cap) return;
+  const int p = (int)(x / cap), idx = (int)(x % cap);
+  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+  if ((uint32_t)row >= (uint32_t)Q.rows) return;
+  const int32_t t = *tbase + k + 1;
+  const float* w = Q.W + (int64_t)row * ld + 4 * sub;
+  float4 v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
+  const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[row]);
+  float* o = rows_send + x * ld + 4 * sub;
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
+}
+
+// owner: for each distinct row of step k (its leader position) sum the peers' gradients in peer
+// order and apply W = V - lr (g + wd V) with the pending decay; one writer per row.
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* __restrict__ ids_recv,
+                                                       const int32_t* __restrict__ aplan, int64_t n,
+                                                       int world, int cap, int k, Hyper hp, int ld,
+                                                       const int32_t* __restrict__ tbase,
+                                                       const float* __restrict__ grads_recv) {
+  const int sub = threadIdx.x & (G4 - 1);
+  const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
+  if (x >= (int64_t)world * cap) return;
+  const int32_t* rec = aplan + ((int64_t)k * world * cap + x) * world;
+  const int32_t r0 = rec[0];
+  if (r0 == -2) return;
+  const int p = (int)(x / cap), idx = (int)(x % cap);
+  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+  const int32_t t = *tbase + k + 1;
+  float* w = Q.W + (int64_t)row * ld + 4 * sub;
+  float4 cur[S], g[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    cur[s] = ld4(w + 4 * G4 * s);
+    g[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int32_t stamp = Q.stamp[row];
+  for (int q0 = 0; q0 < world; q0 += 8) {  // up to 8 peers' rows in flight, summed in peer order
+    int32_t pos[8];
+    float4 gr[8][S];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      pos[m] = q0 + m < world ? (q0 + m == 0 ? r0 : rec[q0 + m]) : -1;
+      if (pos[m] >= 0) {
+        const float* gp = grads_recv + (int64_t)pos[m] * ld + 4 * sub;
+#pragma unroll
+        for (int s = 0; s < S; ++s) gr[m][s] = ld4(gp + 4 * G4 * s);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      if (pos[m] >= 0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          g[s] = make_float4(g[s].x + gr[m][s].x, g[s].y + gr[m][s].y, g[s].z + gr[m][s].z,
+                             g[s].w + gr[m][s].w);
+      }
+  }
+  const float f = decay_pow(hp.log2a, t - 1 - stamp);
+  const float lr = hp.lr, wd = hp.wd;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const float4 v = make_float4(cur[s].x * f, cur[s].y * f, cur[s].z * f, cur[s].w * f);
+    st4(w + 4 * G4 * s,
+        make_float4(fmaf(-lr, fmaf(wd, v.x, g[s].x), v.x), fmaf(-lr, fmaf(wd, v.y, g[s].y), v.y),
+                    fmaf(-lr, fmaf(wd, v.z, g[s].z), v.z), fmaf(-lr, fmaf(wd, v.w, g[s].w), v.w)));
+  }
+  if (sub == 0) Q.stamp[row] = t;
+}
+
+#define BPRMF_DISPATCH4D(geom, BODY)                               \
+  switch ((geom).G4 * 10 + (geom).S) {                             \
+    case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
+    case 21: { constexpr int G4_ = 2, S_ = 1; BODY; } break;       \
+    case 41: { constexpr int G4_ = 4, S_ = 1; BODY; } break;       \
+    case 81: { constexpr int G4_ = 8, S_ = 1; BODY; } break;       \
+    case 161: { constexpr int G4_ = 16, S_ = 1; BODY; } break;     \
+    case 321: { constexpr int G4_ = 32, S_ = 1; BODY; } break;     \
+    case 641: { constexpr int G4_ = 64, S_ = 1; BODY; } break;     \
+    case 642: { constexpr int G4_ = 64, S_ = 2; BODY; } break;     \
+    case 643: { constexpr int G4_ = 64, S_ = 3; BODY; } break;     \
+    case 644: { constexpr int G4_ = 64, S_ = 4; BODY; } break;     \
+    default: return hipErrorInvalidValue;                          \
+  }
+
+static unsigned blocks_for(int64_t threads) { return (unsigned)((threads + kBlock - 1) / kBlock); }
+
+hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_own_max<<<blocks_for(n * world), kBlock, 0, s>>>(bb, n, world, cap);
+  return hipGetLastError();
+}
+
+hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
+                         hipStream_t s) {
+  if (n <= 0 || cap <= 0) return hipSuccess;
+  k_pack_ids<<<blocks_for((int64_t)world * n * cap), kBlock, 0, s>>>(bb, n, world, cap, ids_send);
+  return hipGetLastError();
+}
+
+hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
+                           hipStream_t s) {
+  if (n <= 0 || cap <= 0) return hipSuccess;
+  k_owner_plan<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap, aplan);
+  return hipGetLastError();
+}
+
+hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
+                             int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
+                             hipStream_t s) {
+  if (cap <= 0) return hipSuccess;
+  BPRMF_DISPATCH4D(g, ({
+    const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
+    k_owner_gather<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, n, world, cap, k, hp, g.ld,
+                                                      tbase, rows_send);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
+                            int64_t n, int world, int cap, int k, const Hyper& hp,
+                            const int32_t* tbase, const float* grads_recv, hipStream_t s) {
+  if (cap <= 0) return hipSuccess;
+  BPRMF_DISPATCH4D(g, ({
+    const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
+    k_owner_apply<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, aplan, n, world, cap, k, hp,
+                                                     g.ld, tbase, grads_recv);
+  }));
+  return hipGetLastError();
+}
+
+}  // namespace bprmf

@@ -1,0 +1,113 @@
+// handle.h — the bprmf_handle behind include/bprmf.h and the host helpers shared by capi.cpp
+// (single-GPU training, weights, scoring) and dist.cpp (the sharded multi-GPU runner).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/bprmf.h"
+#include "kernels.h"
+
+namespace bprmf {
+
+int fail(int code, const char* fmt, ...);
+
+#define HIPCHK(x)                                                                           \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) return bprmf::fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+struct StepGraph {  // a captured chunk of step launches (launch_step_graph)
+  int64_t nb = 0;
+  hipGraphExec_t exec = nullptr;
+};
+constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step
+
+struct DistState;  // dist.cpp: the sharded runner's transport, plan and exchange buffers
+void dist_free(DistState* d);
+
+}  // namespace bprmf
+
+struct bprmf_handle {
+  bprmf_config cfg;
+  bprmf::Geom geom;
+  bprmf::Hyper hp;
+  int64_t U = 0, I = 0;  // local rows
+  bprmf::Table P{}, Q{};
+  // training data
+  int64_t npos = 0;
+  int32_t* d_pos_u = nullptr;
+  int32_t* d_pos_i = nullptr;
+  int64_t* d_indptr = nullptr;
+  int32_t* d_indices = nullptr;
+  int feistel_h = 1;
+  uint32_t k0 = 0, k1 = 0;  // shard sampler key
+  // triplet chunk
+  int32_t* d_trip = nullptr;  // [3, cap]
+  // segmented step (batch_size <= kMaxSegBatch): per-batch sorted layouts + per-triplet c*P_u
+  int32_t* d_batch = nullptr;  // batch_cap * BatchBuf::stride_for(B) int32
+  int64_t batch_cap = 0;
+  float* d_contrib = nullptr;  // [B, ld]
+  int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
+  int64_t plan_steps = 0;      // batches of the current sharded plan
+  int64_t trip_cap = 0;
+  // misc device scalars
+  double* d_loss = nullptr;
+  int32_t* d_err = nullptr;
+  int32_t t = 0;  // optimizer steps taken
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // live per-kernel timing (bprmf_profile): event pairs around each launch of each kind
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  size_t prof_used = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_rec[BPRMF_KPROF_KINDS];
+  int64_t prof_weight[BPRMF_KPROF_KINDS] = {};  // extra units per pair (a step-graph pair = nb steps)
+  // captured step sequences (BPRMF_NO_GRAPH=1 disables: eager launches)
+  bool use_graphs = true;
+  std::vector<bprmf::StepGraph> graphs;
+  // sharded runner (bprmf_dist_init*), null until a transport is attached
+  bprmf::DistState* dist = nullptr;
+};
+
+namespace bprmf {
+
+int set_dev(bprmf_handle* h);
+template <typename T>
+int dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) return 0;
+  HIPCHK(hipMalloc((void**)p, sizeof(T) * (size_t)count));
+  return 0;
+}
+hipEvent_t prof_event(bprmf_handle* h);
+// record an event before (begin) / after a launch of `kind` when profiling is on
+struct ProfScope {
+  bprmf_handle* h;
+  int kind;
+  hipEvent_t a = nullptr;
+  ProfScope(bprmf_handle* hh, int k, bool sampled = true) : h(hh), kind(k) {
+    if (h->prof_on && sampled && (a = prof_event(h))) hipEventRecord(a, h->stream);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = prof_event(h);
+    if (!b) return;
+    hipEventRecord(b, h->stream);
+    h->prof_rec[kind].push_back({a, b});
+  }
+};
+int ensure_trip(bprmf_handle* h, int64_t n);
+int ensure_seg(bprmf_handle* h, int64_t n_batches);
+bool seg_mode(const bprmf_handle* h);
+int check_err_flag(bprmf_handle* h);
+SamplerArgs sampler_args(bprmf_handle* h);
+int read_loss(bprmf_handle* h, double* loss);
+int begin_call(bprmf_handle* h);
+int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps);
+
+}  // namespace bprmf

@@ -33,6 +33,7 @@ struct Table {
 //   ij    [B][2]    (i, j) item rows of the triplets, sorted by (local) user row
 //   urec  [B][8]    user segment s: {u, beg, end, i_beg, j_beg, 0, 0, 0}      (meta[1] of them)
 //   irec  [2B][8]   item segment s: {item, beg, end, ref0..ref3, long}        (meta[2] of them)
+//                   (sharded mode: item = the segment's slot)
 //   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
 //                   sorted by item then position (fixed summation order)
 //   lrec  [B/8][8]  copies of the records of item segments with > kLongSeg references (meta[3];
@@ -102,11 +103,12 @@ hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const
 // segmented step: build `n_batches` batches of B (<= kMaxSegBatch) from the sampler (ru == null)
 // or from replayed ids; then per batch k: user_step (K1) and item_step (K2) with t = *tbase+k+1.
 // ru/ri/rj are GLOBAL ids (users are mapped to local rows u / world).  i_rows = global item count.
-// slots: write item slots (sharded exchange) instead of item rows into ij/urec.
+// slots: write item slots (sharded exchange) instead of item rows into ij/urec and irec/lrec:
+// the item segment index (slot_stride 0) or owner * slot_stride + index within the owner's range.
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
-                         int64_t u_rows, int64_t i_rows, int world, bool slots, int64_t n_batches,
-                         BatchBuf bb, int32_t* err, hipStream_t s);
+                         int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s);
 // item_rows != null: sharded K1 (item rows by slot from the exchange buffer)
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, double* loss, float* contrib,
@@ -131,5 +133,17 @@ hipError_t add_rows(const Geom& g, Table W, const int32_t* rows, const float* gr
                     int32_t* err, hipStream_t s);
 hipError_t apply_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
                       int32_t t, hipStream_t s);
+// --- sharded runner (dist.hip; layouts in dist.hip's header comment) ---
+hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s);
+hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
+                         hipStream_t s);
+hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
+                           hipStream_t s);
+hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
+                             int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
+                             hipStream_t s);
+hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
+                            int64_t n, int world, int cap, int k, const Hyper& hp,
+                            const int32_t* tbase, const float* grads_recv, hipStream_t s);
 
 }  // namespace bprmf

@@ -32,8 +32,8 @@ template <int IPT>
 __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
-    int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int user_bits,
-    int item_bits, BatchBuf bb, int32_t* __restrict__ err) {
+    int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int slot_stride,
+    int user_bits, int item_bits, BatchBuf bb, int32_t* __restrict__ err) {
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   __shared__ int32_t s_i[T * IPT];  // per sorted position: item row (world 1) or item slot
   __shared__ int32_t s_j[T * IPT];
   __shared__ int s_own[kMaxWorld];
+  __shared__ int s_opre[kMaxWorld];  // first item segment of each owner (padded slots)
   uint32_t* s_key = sm.key;
 
   const int tid = threadIdx.x;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     const int p = tid * IPT + k;
     key[k] = kNone;
     val[k] = (uint32_t)p;
-    if (p < nb) {
+    if (p < nb && !(ru && ru[b0 + p] < 0)) {  // replay: u < 0 is an empty slot
       int32_t u, i, j;
       bool sampled_ok = true;
       if (ru) {
@@ -186,7 +187,29 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     }
   }
   if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
-  __syncthreads();  // ioff, refs, slots visible block-wide
+  __syncthreads();  // ioff, refs, slots, s_own visible block-wide
+  if (slot_stride) {
+    if (tid == 0) {
+      int acc = 0;
+      for (int o = 0; o < world; ++o) {
+        s_opre[o] = acc;
+        acc += s_own[o];
+      }
+    }
+    __syncthreads();
+  }
+  // slot of item segment s as the step kernels address it: the segment index (compact), or
+  // owner * slot_stride + index within the owner's range (padded: the exchange buffers of the
+  // sharded runner hold slot_stride rows per owner)
+  auto slot_of = [&](int s) -> int {
+    if (!slot_stride) return s;
+    int lo = 0, hi = world - 1;  // largest owner o with s_opre[o] <= s
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_opre[mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    return lo * slot_stride + (s - s_opre[lo]);
+  };
   int nlong_mine = 0;
   {
     int s = iseg0;
@@ -198,7 +221,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         const int len = end - r;
         const int lng = len > kLongSeg;
         nlong_mine += lng;
-        store_rec(v.irec + (int64_t)s * kRec, (int)ik[k], r, end, v.refs[r],
+        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k], r, end, v.refs[r],
                   len > 1 ? v.refs[r + 1] : 0, len > 2 ? v.refs[r + 2] : 0,
                   len > 3 ? v.refs[r + 3] : 0, lng);
         ++s;
@@ -217,7 +240,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         const int end = v.ioff[s + 1];
         if (end - r > kLongSeg) {
           if (lpre < kMaxLongItems)
-            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, s, 0, 0, 0, 1);
+            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
           else
             v.irec[(int64_t)s * kRec + 7] = 0;  // over the cap: served by the short path
           ++lpre;
@@ -234,9 +257,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
       if (key[k] == kNone) continue;
-      reinterpret_cast<int2*>(v.ij)[p] = make_int2(s_i[p], s_j[p]);
+      const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
+      const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
+      reinterpret_cast<int2*>(v.ij)[p] = make_int2(ri_, rj_);
       if (uhead[k]) {
-        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], s_i[p], s_j[p], 0, 0, 0);
+        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], ri_, rj_, 0, 0, 0);
         ++s;
       }
     }
@@ -258,8 +283,8 @@ static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
 
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
-                         int64_t u_rows, int64_t i_rows, int world, bool slots, int64_t n_batches,
-                         BatchBuf bb, int32_t* err, hipStream_t s) {
+                         int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s) {
   if (n_batches <= 0) return hipSuccess;
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
   const int64_t iloc = (i_rows + world - 1) / world;
@@ -267,12 +292,12 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   const int ub = bits_for(u_rows), ib = bits_for(iloc * world);
   if (B <= kBuildThreads * 4)
     k_build_batches<4><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
-        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0, ub,
-        ib, bb, err);
+        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
+        slots ? slot_stride : 0, ub, ib, bb, err);
   else
     k_build_batches<8><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
-        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0, ub,
-        ib, bb, err);
+        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
+        slots ? slot_stride : 0, ub, ib, bb, err);
   return hipGetLastError();
 }
 

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyp
     }
   }
   (void)row;
-  finish_item<G4, S, SH>(Q, item, s, g, hp, ld, t, sub, grads);
+  finish_item<G4, S, SH>(Q, item, item, g, hp, ld, t, sub, grads);  // SH: item field = slot
 }
 
 // Expand BODY for every instantiated float4 geometry (G4_, S_).

@@ -66,6 +66,17 @@ class TorchComm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 
+    def broadcast_bytes(self, data, device):
+        """rank 0's bytes to every rank (the RCCL unique id of the library's communicator)."""
+        import torch
+        dev = torch.device("cpu") if self.backend == "gloo" else device
+        t = torch.zeros(len(data), dtype=torch.uint8, device=dev)
+        if self.rank == 0:
+            t.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        src = self.dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        self.dist.broadcast(t, src=src, group=self.group)
+        return bytes(t.cpu().numpy().tobytes())
+
 
 class ThreadGroup:
     """Shared state of an in-process group: `world` shards stepped by `world` threads (used to run
@@ -181,6 +192,27 @@ class HipShard:
         _lib.check(self.L.bprmf_dist_end_step(self.h, ctypes.byref(loss)))
         return loss.value
 
+    # -- the library-driven runner (bprmf_dist_init_* / bprmf_dist_train_*) --------------------
+    def runner_rccl(self, uid):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        _lib.check(self.L.bprmf_dist_init_rccl(self.h, ctypes.addressof(buf)))
+
+    def runner_loopback(self, key):
+        _lib.check(self.L.bprmf_dist_init_loopback(self.h, int(key)))
+
+    def runner_train_steps(self, epoch, first_step, n_steps):
+        st = _lib.Stats()
+        _lib.check(self.L.bprmf_dist_train_steps(self.h, int(epoch), int(first_step), int(n_steps),
+                                                 ctypes.byref(st)))
+        return st.as_dict()
+
+    def runner_train_replay(self, u, i, j, n_steps):
+        st = _lib.Stats()
+        u, i, j = (np.ascontiguousarray(x, dtype=np.int32) for x in (u, i, j))
+        _lib.check(self.L.bprmf_dist_train_replay(self.h, u.ctypes.data, i.ctypes.data,
+                                                  j.ctypes.data, int(n_steps), ctypes.byref(st)))
+        return st.as_dict()
+
     def get_weights(self):
         return self.m.get_weights()
 
@@ -216,6 +248,7 @@ class ShardedBPRMF:
         self.chunk_steps = int(chunk_steps)
         self.steps_per_epoch = None
         self._plan = None  # (epoch, first_step, n, send_counts, recv_counts)
+        self.runner = None  # attach_runner(): "rccl" | "loopback"
 
     # -- data -----------------------------------------------------------------------------------
     def set_train(self, positives):
@@ -235,10 +268,10 @@ class ShardedBPRMF:
         recv = self.comm.exchange_counts(send, self.device)
         self._plan = (epoch, first, n, send, recv)
 
-    def plan_replay(self, batches):
-        """Replay plan from GLOBAL batches: list of (u, i, j) arrays, one per step; this rank keeps
-        its own users' triplets (a batch of G*B global triplets splits unevenly across ranks, so
-        the local capacity batch_size must hold every rank's share)."""
+    def _local_batches(self, batches):
+        """This rank's share of GLOBAL batches (list of (u, i, j), one per step), batch_size slots
+        per step, u = -1 in empty slots (a batch of G*B global triplets splits unevenly across
+        ranks, so the local capacity batch_size must hold every rank's share)."""
         B = self.batch_size
         n = len(batches)
         U = np.full(n * B, -1, np.int32)
@@ -251,11 +284,46 @@ class ShardedBPRMF:
             if c > B:
                 raise ValueError(f"rank {self.rank} gets {c} triplets at step {k} > batch_size {B}")
             U[k * B:k * B + c], I[k * B:k * B + c], J[k * B:k * B + c] = u[mine], i[mine], j[mine]
+        return U, I, J, n
+
+    def plan_replay(self, batches):
+        """Replay plan (per-step Python orchestration) from GLOBAL batches, see _local_batches."""
+        U, I, J, n = self._local_batches(batches)
         send = self.b.plan_replay(U, I, J, n)
         recv = self.comm.exchange_counts(send, self.device)
         self._plan = ("replay", 0, n, send, recv)
 
-    # -- one step -------------------------------------------------------------------------------
+    # -- the library-driven runner: whole chunks of steps, exchanges issued from C++ -------------
+    def attach_runner(self, transport="rccl", key=0):
+        """transport "rccl": the library's own RCCL communicator (rank 0 makes the unique id, the
+        process group broadcasts it); "loopback": in-process shards sharing group `key` (tests)."""
+        if transport == "rccl":
+            uid = bytes(128)
+            if self.rank == 0:
+                buf = (ctypes.c_uint8 * 128)()
+                _lib.check(_lib.load().bprmf_dist_unique_id(ctypes.addressof(buf)))
+                uid = bytes(buf)
+            uid = self.comm.broadcast_bytes(uid, self.device)
+            self.b.runner_rccl(uid)
+        elif transport == "loopback":
+            self.b.runner_loopback(key)
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
+        self.runner = transport
+
+    def train_steps(self, epoch, first_step, n_steps):
+        """Global steps [first_step, first_step + n_steps) of `epoch` on every rank (same args)."""
+        return self.b.runner_train_steps(epoch, first_step, n_steps)
+
+    def train_epoch(self, epoch):
+        return self.train_steps(epoch, 0, self.steps_per_epoch)
+
+    def train_replay(self, batches):
+        """GLOBAL batches (list of (u, i, j), one per step) through the runner."""
+        U, I, J, n = self._local_batches(batches)
+        return self.b.runner_train_replay(U, I, J, n)
+
+    # -- one step (per-step Python orchestration over `comm`) -----------------------------------
     def step(self, epoch, step, want_loss=False):
         """Global step `step` of `epoch` (every rank calls it with the same arguments)."""
         self._ensure_plan(epoch, step)

@@ -101,3 +101,131 @@ def test_sharded_sampler_training(rl, golden):
                     (seed + 0x9E3779B97F4A7C15) & (2**64 - 1), 0, 0, 1000)
     for x, y in zip(got, want):
         assert np.array_equal(x, y)
+
+
+# ---- the library-driven runner (bprmf_dist_train_*): exchanges issued from C++ ---------------
+def _runner_threads(rl, world, key, fn):
+    """`world` shards in this process, one thread each, loopback transport group `key`."""
+    grp = rl.sharded.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            out[r] = fn(rl.sharded.ThreadComm(grp, r), r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    assert all(not t.is_alive() for t in ts), "runner threads did not finish"
+    return out
+
+
+def _batches(g, steps, GB, hot=True):
+    out = []
+    for _ in range(steps):
+        u, i, j = g.integers(0, U, GB), g.integers(0, I, GB), g.integers(0, I, GB)
+        if hot:
+            i[:40] = 7  # hot item (> kLongSeg references)
+        out.append((u, i, j))
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_runner_replay_equals_single_gpu_global_batch(rl, world):
+    g = np.random.default_rng(100 + world)
+    P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, D))).astype(np.float32)
+    GB, steps = 512, 7
+    batches = _batches(g, steps, GB)
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=GB, device=0, comm=comm)
+        m.set_weights(sh.shard_rows(P0, r, world), sh.shard_rows(Q0, r, world))
+        m.attach_runner("loopback", key=1000 + world)
+        st = m.train_replay(batches)
+        return m.get_weights(), st
+
+    parts = _runner_threads(rl, world, 1000 + world, fn)
+    P = sh.unshard_rows([p[0][0] for p in parts], U)
+    Q = sh.unshard_rows([p[0][1] for p in parts], I)
+    Pr, Qr = P0.copy(), Q0.copy()
+    loss = 0.0
+    for u, i, j in batches:
+        loss += O.bpr_step_dense(Pr, Qr, u, i, j, 0.05, 0.01)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+    assert sum(p[1]["triplets"] for p in parts) == steps * GB
+    got_loss = sum(p[1]["loss"] for p in parts)
+    assert abs(got_loss - loss) <= 1e-4 * abs(loss), (got_loss, loss)
+
+
+def test_runner_sampler_matches_python_orchestration_and_is_reproducible(rl, golden):
+    """Sampler mode, 2 shards: the C++ runner and the per-step Python orchestration take the same
+    steps (same batches, same exchanges); the runner is bitwise reproducible run to run."""
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    Uu, Ii = int(f["U"]), int(f["I"])
+    world, B, seed, d = 2, 1024, 5, 64
+    sh = rl.sharded
+
+    def runner(comm, r, key):
+        m = sh.ShardedBPRMF(Uu, Ii, d, batch_size=B, seed=seed, device=0, comm=comm)
+        S = m.set_train(pos)
+        m.attach_runner("loopback", key=key)
+        m.train_steps(0, 0, S)
+        m.train_steps(1, 0, 9)
+        return m.get_weights()
+
+    def python_path(comm, r):
+        m = sh.ShardedBPRMF(Uu, Ii, d, batch_size=B, seed=seed, device=0, comm=comm)
+        S = m.set_train(pos)
+        for s in range(S):
+            m.step(0, s)
+        for s in range(9):
+            m.step(1, s)
+        return m.get_weights()
+
+    a = _runner_threads(rl, world, 2001, lambda c, r: runner(c, r, 2001))
+    b = _runner_threads(rl, world, 2002, lambda c, r: runner(c, r, 2002))
+    c = _runner_threads(rl, world, 0, python_path)
+    for r in range(world):
+        for x, y, z in zip(a[r], b[r], c[r]):
+            assert np.array_equal(x, y), "runner not bitwise reproducible"
+            np.testing.assert_allclose(x, z, rtol=1e-5, atol=1e-6)
+
+
+def test_runner_rccl_transport_one_rank(rl):
+    """The RCCL transport (library-owned communicator, unique id broadcast by the process group)
+    at world 1 gives the loopback transport's result bit for bit."""
+    import os
+    import torch
+    import torch.distributed as dist
+    g = np.random.default_rng(7)
+    P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, D))).astype(np.float32)
+    batches = _batches(g, 5, 256)
+    sh = rl.sharded
+    res = []
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        for transport in ("rccl", "loopback"):
+            m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=256, device=0)
+            m.set_weights(P0, Q0)
+            m.attach_runner(transport, key=3001)
+            m.train_replay(batches)
+            res.append(m.get_weights())
+    finally:
+        if own:
+            dist.destroy_process_group()
+    for x, y in zip(*res):
+        assert np.array_equal(x, y)

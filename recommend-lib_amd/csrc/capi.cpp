@@ -183,7 +183,7 @@ int bprmf_destroy(bprmf_handle* h) {
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err,
-                  h->d_batch, h->d_contrib, h->d_tbase};
+                  h->d_batch, h->d_contrib, h->d_ugrad, h->d_tbase};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -361,6 +361,7 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   const int64_t B = h->cfg.batch_size;
   if (!h->d_contrib) {
     if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
+    if (int r = dalloc(&h->d_ugrad, B * h->geom.ld)) return r;
     if (int r = dalloc(&h->d_tbase, 1)) return r;
   }
   if (n_batches <= h->batch_cap) return 0;
@@ -402,10 +403,10 @@ static int launch_step_graph(bprmf_handle* h, int64_t nb) {
     for (int64_t k = 0; k < nb && e == hipSuccess; ++k) {
       const BatchView v = bb.view(k);
       e = user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss, h->d_contrib,
-                    nullptr, h->stream);
+                    h->d_ugrad, nullptr, h->stream);
       if (e == hipSuccess)
-        e = item_step(h->geom, v, B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
-                      h->stream);
+        e = item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                      h->d_ugrad, nullptr, h->stream);
     }
     hipGraph_t graph = nullptr;
     const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
@@ -477,12 +478,12 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
       {
         ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
         HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                         h->d_contrib, nullptr, h->stream));
+                         h->d_contrib, h->d_ugrad, nullptr, h->stream));
       }
       {
         ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
-        HIPCHK(item_step(h->geom, v, (int)B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, nullptr,
-                         h->stream));
+        HIPCHK(item_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                         h->d_ugrad, nullptr, h->stream));
       }
     }
   }
@@ -807,7 +808,7 @@ int bprmf_dist_user_step(bprmf_handle* h, int64_t k, const float* item_rows) {
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
   ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
   HIPCHK(user_step(h->geom, bb.view(k), h->cfg.batch_size, h->P, h->Q, h->hp, h->d_tbase, 0,
-                   h->d_loss, h->d_contrib, item_rows, h->stream));
+                   h->d_loss, h->d_contrib, h->d_ugrad, item_rows, h->stream));
   return 0;
 }
 
@@ -816,8 +817,8 @@ int bprmf_dist_item_grads(bprmf_handle* h, int64_t k, float* grads) {
   if (!grads) return fail(BPRMF_E_INVALID, "null grads");
   const BatchBuf bb{h->d_batch, h->cfg.batch_size};
   ProfScope ps(h, BPRMF_KPROF_APPLY);
-  HIPCHK(item_step(h->geom, bb.view(k), h->cfg.batch_size, h->Q, h->hp, h->d_tbase, 0,
-                   h->d_contrib, grads, h->stream));
+  HIPCHK(item_step(h->geom, bb.view(k), h->cfg.batch_size, h->P, h->Q, h->hp, h->d_tbase, 0,
+                   h->d_contrib, h->d_ugrad, grads, h->stream));
   return 0;
 }
 

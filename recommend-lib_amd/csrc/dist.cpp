@@ -10,7 +10,8 @@
 //   build_batches(slots padded by S per owner) -> cap = max requests per (step, owner), max over
 //   ranks -> pack + exchange the chunk's requests once -> owner apply plan;
 //   per step k: owner_gather -> exchange rows -> user_step (SH) -> item_step (SH: per-slot grads)
-//   -> exchange grads -> owner_apply.
+//   -> exchange grads -> owner_apply.  A rank's requests to itself never enter the exchange: the
+//   gather writes them into its slots and the apply reads their gradients in place.
 // Exchange sizes are cap rows per peer per step (uniform), so every rank posts matching sizes
 // without a per-step count exchange.  Semantics: SURVEY.md §8e — a world-W run with per-rank
 // batch B equals one step over the union batch (BPRMFRecommender.py:172-176).
@@ -29,7 +30,8 @@ namespace bprmf {
 
 struct Transport {
   virtual ~Transport() = default;
-  // all-to-all of per-peer blocks of `bytes`: send[p] goes to rank p, recv[p] comes from rank p
+  // all-to-all of per-peer blocks of `bytes`: send[p] goes to rank p, recv[p] comes from rank p;
+  // send[rank] == nullptr: no self block (the caller placed it already)
   virtual int exchange(bprmf_handle* h, const void* const* send, void* const* recv, size_t bytes) = 0;
   // in-place max over ranks of one device int32
   virtual int max_i32(bprmf_handle* h, int32_t* dev) = 0;
@@ -49,7 +51,7 @@ struct RcclTransport final : Transport {
   int exchange(bprmf_handle* h, const void* const* send, void* const* recv, size_t bytes) override {
     if (!bytes) return 0;
     const int W = h->cfg.world, R = h->cfg.rank;
-    HIPCHK(hipMemcpyAsync(recv[R], send[R], bytes, hipMemcpyDeviceToDevice, h->stream));
+    if (send[R]) HIPCHK(hipMemcpyAsync(recv[R], send[R], bytes, hipMemcpyDeviceToDevice, h->stream));
     if (W == 1) return 0;
     NCCLCHK(ncclGroupStart());
     for (int p = 0; p < W; ++p) {
@@ -107,6 +109,7 @@ struct LoopTransport final : Transport {
     g->barrier();
     int rc = 0;
     for (int p = 0; p < W && !rc && bytes; ++p) {
+      if (!g->send[p][R]) continue;
       const hipError_t e = hipMemcpyAsync(recv[p], g->send[p][R], bytes, hipMemcpyDeviceToDevice, h->stream);
       if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "loopback copy: %s", hipGetErrorString(e));
     }
@@ -259,32 +262,33 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     {
       ProfScope ps(h, BPRMF_KPROF_OWNER, sampled && !ea);
       HIPCHK(dist_owner_gather(h->geom, h->Q, d->ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase,
-                               d->rows_send, h->stream));
+                               d->rows_send, R, d->rows_recv + (int64_t)R * d->S * ld, h->stream));
     }
     for (int p = 0; p < W; ++p) {
-      sp[p] = d->rows_send + (int64_t)p * cap * ld;
+      sp[p] = p == R ? nullptr : d->rows_send + (int64_t)p * cap * ld;
       rp[p] = d->rows_recv + (int64_t)p * d->S * ld;
     }
     if (int r = d->tr->exchange(h, sp.data(), rp.data(), row_bytes)) return r;
     {
       ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled && !ea);
       HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                       h->d_contrib, d->rows_recv, h->stream));
+                       h->d_contrib, h->d_ugrad, d->rows_recv, h->stream));
     }
     {
       ProfScope ps(h, BPRMF_KPROF_APPLY, sampled && !ea);
-      HIPCHK(item_step(h->geom, v, B, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                       d->grads_send, h->stream));
+      HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                       h->d_ugrad, d->grads_send, h->stream));
     }
     for (int p = 0; p < W; ++p) {
-      sp[p] = d->grads_send + (int64_t)p * d->S * ld;
+      sp[p] = p == R ? nullptr : d->grads_send + (int64_t)p * d->S * ld;
       rp[p] = d->grads_recv + (int64_t)p * cap * ld;
     }
     if (int r = d->tr->exchange(h, sp.data(), rp.data(), row_bytes)) return r;
     {
       ProfScope ps(h, BPRMF_KPROF_OWNER, sampled && !ea);
       HIPCHK(dist_owner_apply(h->geom, h->Q, d->ids_recv, d->aplan, n, W, cap, (int)k, h->hp,
-                              h->d_tbase, d->grads_recv, h->stream));
+                              h->d_tbase, d->grads_recv, R, d->grads_send + (int64_t)R * d->S * ld,
+                              h->stream));
     }
   }
   if (ea) {
@@ -295,7 +299,6 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
       h->prof_weight[BPRMF_KPROF_STEPS] += n - 1;
     }
   }
-  (void)R;
   h->t += (int32_t)n;
   return 0;
 }

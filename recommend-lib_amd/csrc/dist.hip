@@ -8,7 +8,8 @@
 // and the owner derives, per step, an apply plan: for each distinct requested row its leader
 // position (the lowest requesting peer) lists the positions of every peer's gradient for that
 // row, in peer order, so the owner's sum over peers has a fixed order (bitwise reproducible).
-// Per step: k_owner_gather (rows at step t-1, packed per requesting peer) -> exchange ->
+// Per step: k_owner_gather (rows at step t-1, packed per requesting peer; this rank's own
+// requests written straight into its slot buffer) -> exchange with the other ranks ->
 // K1/K2 (step.hip, sharded instantiations) -> exchange of per-slot gradients ->
 // k_owner_apply (fixed-order sum, lazy decay + SGD, one writer per row).
 // Reference semantics: the same SGD step as BPRMFRecommender.py:172-176 on the union batch.
@@ -80,13 +81,15 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
   }
 }
 
-// owner: rows requested by every peer for step k, brought to step t-1, packed [world][cap][ld]
+// owner: rows requested by every peer for step k, brought to step t-1, packed [world][cap][ld];
+// this rank's own requests go straight to their slots (self_rows, no exchange copy)
 template <int G4, int S>
 __global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t* __restrict__ ids_recv,
                                                         int64_t n, int world, int cap, int k,
                                                         Hyper hp, int ld,
                                                         const int32_t* __restrict__ tbase,
-                                                        float* __restrict__ rows_send) {
+                                                        float* __restrict__ rows_send, int self,
+                                                        float* __restrict__ self_rows) {
   const int sub = threadIdx.x & (G4 - 1);
   const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
   if (x >= (int64_t)world * cap) return;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t*
 #pragma unroll
   for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
   const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[row]);
-  float* o = rows_send + x * ld + 4 * sub;
+  float* o = (p == self ? self_rows + (int64_t)idx * ld : rows_send + x * ld) + 4 * sub;
 #pragma unroll
   for (int s = 0; s < S; ++s)
     st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
@@ -112,7 +115,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
                                                        const int32_t* __restrict__ aplan, int64_t n,
                                                        int world, int cap, int k, Hyper hp, int ld,
                                                        const int32_t* __restrict__ tbase,
-                                                       const float* __restrict__ grads_recv) {
+                                                       const float* __restrict__ grads_recv, int self,
+                                                       const float* __restrict__ self_grads) {
   const int sub = threadIdx.x & (G4 - 1);
   const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
   if (x >= (int64_t)world * cap) return;
@@ -137,7 +141,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
     for (int m = 0; m < 8; ++m) {
       pos[m] = q0 + m < world ? (q0 + m == 0 ? r0 : rec[q0 + m]) : -1;
       if (pos[m] >= 0) {
-        const float* gp = grads_recv + (int64_t)pos[m] * ld + 4 * sub;
+        const int q = pos[m] / cap, i = pos[m] - q * cap;
+        const float* gp = (q == self ? self_grads + (int64_t)i * ld : grads_recv + (int64_t)pos[m] * ld) + 4 * sub;
 #pragma unroll
         for (int s = 0; s < S; ++s) gr[m][s] = ld4(gp + 4 * G4 * s);
       }
@@ -202,24 +207,25 @@ hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int ca
 
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
                              int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
-                             hipStream_t s) {
+                             int self, float* self_rows, hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
     const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
     k_owner_gather<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, n, world, cap, k, hp, g.ld,
-                                                      tbase, rows_send);
+                                                      tbase, rows_send, self, self_rows);
   }));
   return hipGetLastError();
 }
 
 hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                             int64_t n, int world, int cap, int k, const Hyper& hp,
-                            const int32_t* tbase, const float* grads_recv, hipStream_t s) {
+                            const int32_t* tbase, const float* grads_recv, int self,
+                            const float* self_grads, hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
     const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
     k_owner_apply<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, aplan, n, world, cap, k, hp,
-                                                     g.ld, tbase, grads_recv);
+                                                     g.ld, tbase, grads_recv, self, self_grads);
   }));
   return hipGetLastError();
 }

@@ -50,7 +50,8 @@ struct bprmf_handle {
   // segmented step (batch_size <= kMaxSegBatch): per-batch sorted layouts + per-triplet c*P_u
   int32_t* d_batch = nullptr;  // batch_cap * BatchBuf::stride_for(B) int32
   int64_t batch_cap = 0;
-  float* d_contrib = nullptr;  // [B, ld]
+  float* d_contrib = nullptr;  // [B, ld] c*P_u per triplet (K1 -> K2)
+  float* d_ugrad = nullptr;    // [B, ld] user gradient per triplet of multi-triplet users
   int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;

@@ -29,45 +29,48 @@ struct Table {
 };
 
 // One batch of a step, as laid out by k_build_batches (int32, positions within the batch).  Every
-// step kernel reaches its rows after ONE dependent load of a 32-byte record:
-//   ij    [B][2]    (i, j) item rows of the triplets, sorted by (local) user row
-//   urec  [B][8]    user segment s: {u, beg, end, i_beg, j_beg, 0, 0, 0}      (meta[1] of them)
+// step kernel reaches its rows after ONE dependent load of a 16- or 32-byte record:
+//   trec  [B][4]    per triplet, sorted by (local) user row: {i, j, u, single}; single = the user
+//                   has no other triplet in the batch (K1 then updates the user row itself)
+//   mrec  [B/2][8]  user segments with more than one triplet: {u, beg, end, 0...} (meta[4] of them;
+//                   K2 sums their per-triplet user gradients in position order)
 //   irec  [2B][8]   item segment s: {item, beg, end, ref0..ref3, long}        (meta[2] of them)
 //                   (sharded mode: item = the segment's slot)
-//   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
-//                   sorted by item then position (fixed summation order)
 //   lrec  [B/8][8]  copies of the records of item segments with > kLongSeg references (meta[3];
 //                   at most 2B/(kLongSeg+1) < B/8 of them)
+//   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
+//                   sorted by item then position (fixed summation order)
 //   useg  [B+1], ioff [2B+1]   builder scratch (segment starts)
 //   ukey  [2B]      sharded mode: the distinct items as the owner's local row, segment order
-//   meta  [4]       {triplets, user segments, item segments, long item segments}
+//   meta  [8]       {triplets, user segments, item segments, long item segments, multi user segs}
 //   own   [64]      sharded mode: item segments per owner rank (segments are owner-major)
 // Item segments are ordered by key = (item % world) * iloc + item / world (= item when world 1).
-// In sharded mode ij / urec hold item SLOTS (segment indices: rows of the exchange buffers).
+// In sharded mode trec holds item SLOTS (rows of the exchange buffers) instead of item rows.
 constexpr int kRec = 8;
 constexpr int kLongSeg = 16;
 constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
 constexpr int kMaxWorld = 64;
 struct BatchView {
-  int32_t *ij, *urec, *irec, *refs, *lrec, *useg, *ioff, *ukey, *meta, *own;
+  int32_t *trec, *mrec, *irec, *lrec, *refs, *useg, *ioff, *ukey, *meta, *own;
 };
 struct BatchBuf {
   int32_t* base;
   int B;
-  __host__ __device__ static int64_t stride_for(int B) { return 34LL * B + 6 + kMaxWorld; }
+  // a multiple of 4 ints: every batch (and its int4 records) stays 16-byte aligned
+  __host__ __device__ static int64_t stride_for(int B) { return 32LL * B + 76; }
   __host__ __device__ BatchView view(int64_t k) const {
     int32_t* p = base + k * stride_for(B);
     BatchView v;
-    v.ij = p;
-    v.urec = p + 2LL * B;
-    v.irec = p + 10LL * B;
-    v.refs = p + 26LL * B;
-    v.lrec = p + 28LL * B;
-    v.useg = p + 29LL * B;
-    v.ioff = p + 30LL * B + 1;
-    v.ukey = p + 32LL * B + 2;
-    v.meta = p + 34LL * B + 2;
-    v.own = p + 34LL * B + 6;
+    v.trec = p;
+    v.mrec = p + 4LL * B;
+    v.irec = p + 8LL * B;
+    v.lrec = p + 24LL * B;
+    v.refs = p + 25LL * B;
+    v.useg = p + 27LL * B;
+    v.ioff = p + 28LL * B + 1;
+    v.ukey = p + 30LL * B + 2;
+    v.meta = p + 32LL * B + 4;
+    v.own = p + 32LL * B + 12;
     return v;
   }
 };
@@ -109,14 +112,17 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s);
-// item_rows != null: sharded K1 (item rows by slot from the exchange buffer)
+// K1, one lane group per triplet: c*P_u -> contrib[p]; single-triplet users updated in place,
+// the others' per-triplet gradients -> ugrad[p].  item_rows != null: sharded K1 (item rows by
+// slot from the exchange buffer)
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib,
+                     const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s);
-// grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying)
-hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, const float* contrib, float* grads,
-                     hipStream_t s);
+// K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
+// grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items)
+hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, const float* contrib, const float* ugrad,
+                     float* grads, hipStream_t s);
 int item_long_blocks(int B);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
@@ -141,9 +147,10 @@ hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int ca
                            hipStream_t s);
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
                              int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
-                             hipStream_t s);
+                             int self, float* self_rows, hipStream_t s);
 hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                             int64_t n, int world, int cap, int k, const Hyper& hp,
-                            const int32_t* tbase, const float* grads_recv, hipStream_t s);
+                            const int32_t* tbase, const float* grads_recv, int self,
+                            const float* self_grads, hipStream_t s);
 
 }  // namespace bprmf

@@ -250,19 +250,37 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     }
   }
 
-  // 3. triplet records, now that s_i/s_j hold the final item rows (world 1) or slots
+  // 3. triplet records, now that s_i/s_j hold the final item rows (world 1) or slots, and the
+  //    records of user segments with more than one triplet (K2 finishes those users)
+  int nmulti_mine = 0;
   {
     int s = seg0;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
+      if (uhead[k]) {
+        nmulti_mine += v.useg[s + 1] - p > 1;
+        ++s;
+      }
+    }
+  }
+  __syncthreads();  // sscan reuse
+  int mpre = 0, n_multi = 0;
+  Scan().exclusive_scan(nmulti_mine, mpre, 0, n_multi, sscan, rocprim::plus<int>());
+  {
+    int s = seg0 - 1;  // segment of this thread's first position when that is not a head
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
       if (key[k] == kNone) continue;
+      if (uhead[k]) ++s;
+      const int beg = v.useg[s], end = v.useg[s + 1];
       const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
       const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
-      reinterpret_cast<int2*>(v.ij)[p] = make_int2(ri_, rj_);
-      if (uhead[k]) {
-        store_rec(v.urec + (int64_t)s * kRec, (int)key[k], p, v.useg[s + 1], ri_, rj_, 0, 0, 0);
-        ++s;
+      reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], end - beg == 1);
+      if (uhead[k] && end - beg > 1) {
+        store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], beg, end, 0, 0, 0, 0, 0);
+        ++mpre;
       }
     }
   }
@@ -272,6 +290,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     v.meta[1] = n_useg;
     v.meta[2] = n_iseg;
     v.meta[3] = min(n_long, kMaxLongItems);
+    v.meta[4] = n_multi;
   }
 }
 

@@ -1,14 +1,16 @@
 // step.hip — the two per-step kernels of the segmented (atomic-free, deterministic) BPR-MF step,
 // over the batch layout built by k_build_batches (segment.hip).
 //
-//   k_user_step (K1) one lane group per user segment: gather P_u, Q_i, Q_j with their pending
-//     weight decay, x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x) = -dL/dx; the user's gradient
-//     -c (Q_i - Q_j) is summed in registers over the segment; c*P_u is stored per triplet for K2;
-//     the updated user row W = V - lr (g + wd V) is written in place (every read of P_u in the
-//     step belongs to this segment).
+//   k_user_step (K1) one lane group per triplet: gather P_u, Q_i, Q_j with their pending weight
+//     decay, x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x) = -dL/dx; c*P_u is stored for K2.  A
+//     user with one triplet in the batch is updated right there, W = V - lr (g + wd V) with
+//     g = -c (Q_i - Q_j) (no other read of P_u in the step); otherwise g goes to ugrad[p].
 //   k_item_step (K2) one lane group per distinct item; items with more than kLongSeg references
 //     get a whole workgroup and an LDS reduction in group order.  g = sum of -/+ c*P_u over the
-//     item's references in a fixed order, then the same SGD + weight decay update.
+//     item's references in a fixed order, then the same SGD + weight decay update.  The users with
+//     several triplets are finished here too: g = their ugrad rows summed in position order.
+// Every triplet is one group in K1 whatever its user's multiplicity, so no group walks a chain of
+// dependent row loads (heavy users were K1's tail when a group owned a whole user segment).
 // Reference semantics: BPRMFRecommender.py:172-176 (forward :42-50, loss :174, SGD(wd) :154).
 //
 // Row layout: G4 lanes per row, each lane one float4 per stripe (16 B/lane, whole 64..1024 B rows
@@ -44,75 +46,66 @@ static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, floa
                      fmaf(-lr, fmaf(wd, v.z, g.z), v.z), fmaf(-lr, fmaf(wd, v.w, g.w), v.w));
 }
 
-// SH (sharded): i/j are slots of item_rows, the rows the owners sent for this step, already
-// brought to step t-1 by the owner (no stamps here).
+// K1, one lane group per triplet p (sorted by user).  SH (sharded): i/j are slots of item_rows,
+// the rows the owners sent for this step, already brought to step t-1 by the owner (no stamps).
 template <int G4, int S, bool SH>
 __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
                                                       int ld, const int32_t* __restrict__ tbase,
                                                       int step, double* loss,
                                                       float* __restrict__ contrib,
+                                                      float* __restrict__ ugrad,
                                                       const float* __restrict__ item_rows) {
   const int sub = threadIdx.x & (G4 - 1);
-  const int s = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
-  // independent loads: the record (allocated for every s < B), the segment count, the step base
-  const int4 r0 = reinterpret_cast<const int4*>(bv.urec + (int64_t)s * kRec)[0];
-  const int r1x = bv.urec[(int64_t)s * kRec + 4];
-  const int n_useg = bv.meta[1];
+  const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
+  // independent loads: the record (allocated for every p < B), the triplet count, the step base
+  const int4 r = reinterpret_cast<const int4*>(bv.trec)[p];
+  const int n = bv.meta[0];
   const int32_t t = *tbase + step + 1;
   float lsum = 0.f;
-  if (s < n_useg) {
-    const int32_t u = r0.x;
-    const int beg = r0.y, end = r0.z;
-    int32_t i = r0.w, j = r1x;
+  if (p < n) {
+    const int32_t i = r.x, j = r.y, u = r.z;
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
-    float4 pu[S], g[S];
+    const float* qbase = SH ? item_rows : Q.W;
+    const float* qi = qbase + (int64_t)i * ld + 4 * sub;
+    const float* qj = qbase + (int64_t)j * ld + 4 * sub;
+    float4 pu[S], vi[S], vj[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       pu[k] = ld4(pw + 4 * G4 * k);
-      g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vi[k] = ld4(qi + 4 * G4 * k);
+      vj[k] = ld4(qj + 4 * G4 * k);
     }
-    const float fu = decay_pow(hp.log2a, t - 1 - P.stamp[u]);
+    const int32_t su = P.stamp[u];
+    const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
+    const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
+    const float fu = decay_pow(hp.log2a, t - 1 - su);
+    float di = 0.f, dj = 0.f;
 #pragma unroll
-    for (int k = 0; k < S; ++k) pu[k] = scale4(pu[k], fu);
-    for (int p = beg; p < end; ++p) {
-      int2 nxt = make_int2(0, 0);
-      if (p + 1 < end) nxt = reinterpret_cast<const int2*>(bv.ij)[p + 1];
-      const float* qbase = SH ? item_rows : Q.W;
-      const float* qi = qbase + (int64_t)i * ld + 4 * sub;
-      const float* qj = qbase + (int64_t)j * ld + 4 * sub;
-      float4 vi[S], vj[S];
-#pragma unroll
-      for (int k = 0; k < S; ++k) {
-        vi[k] = ld4(qi + 4 * G4 * k);
-        vj[k] = ld4(qj + 4 * G4 * k);
-      }
-      const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
-      const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
-      float di = 0.f, dj = 0.f;
-#pragma unroll
-      for (int k = 0; k < S; ++k) {
-        vi[k] = scale4(vi[k], fi);
-        vj[k] = scale4(vj[k], fj);
-        di = dot4(pu[k], vi[k], di);
-        dj = dot4(pu[k], vj[k], dj);
-      }
-      di = group_sum<G4>(di);
-      dj = group_sum<G4>(dj);
-      const float x = di - dj;
-      const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
-      if (sub == 0 && loss) lsum += softplus(-x);
-      float* cb = contrib + (int64_t)p * ld + 4 * sub;
-#pragma unroll
-      for (int k = 0; k < S; ++k) {
-        g[k] = fma4(-c, sub4(vi[k], vj[k]), g[k]);
-        st4(cb + 4 * G4 * k, scale4(pu[k], c));
-      }
-      i = nxt.x;
-      j = nxt.y;
+    for (int k = 0; k < S; ++k) {
+      pu[k] = scale4(pu[k], fu);
+      vi[k] = scale4(vi[k], fi);
+      vj[k] = scale4(vj[k], fj);
+      di = dot4(pu[k], vi[k], di);
+      dj = dot4(pu[k], vj[k], dj);
     }
+    di = group_sum<G4>(di);
+    dj = group_sum<G4>(dj);
+    const float x = di - dj;
+    const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
+    if (sub == 0 && loss) lsum = softplus(-x);
+    float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4(pw + 4 * G4 * k, sgd4(pu[k], g[k], hp.lr, hp.wd));
-    if (sub == 0) P.stamp[u] = t;
+    for (int k = 0; k < S; ++k) st4(cb + 4 * G4 * k, scale4(pu[k], c));
+    if (r.w) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        st4(pw + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
+      if (sub == 0) P.stamp[u] = t;
+    } else {  // K2 sums the segment's gradients in position order
+      float* ub = ugrad + (int64_t)p * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) st4(ub + 4 * G4 * k, scale4(sub4(vi[k], vj[k]), -c));
+    }
   }
   if (loss) wave_add_loss(loss, lsum);
 }
@@ -159,15 +152,61 @@ static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int sl
   }
 }
 
+// sum of the rows src[beg..end) in order (lanes fetch G4 indices at once, 8 rows in flight)
+template <int G4, int S>
+static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __restrict__ src,
+                                                int beg, int end, int ld, int sub) {
+#pragma unroll
+  for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int m0 = beg; m0 < end; m0 += 8) {
+    float4 rows[8][S];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      if (m0 + m < end) {
+        const float* rp = src + (int64_t)(m0 + m) * ld + 4 * sub;
+#pragma unroll
+        for (int k = 0; k < S; ++k) rows[m][k] = ld4(rp + 4 * G4 * k);
+      }
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      if (m0 + m < end) {
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+          g[k] = make_float4(g[k].x + rows[m][k].x, g[k].y + rows[m][k].y, g[k].z + rows[m][k].z,
+                             g[k].w + rows[m][k].w);
+      }
+  }
+}
+
 template <int G4, int S, bool SH>
-__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyper hp, int ld,
-                                                      const int32_t* __restrict__ tbase, int step,
-                                                      const float* __restrict__ contrib,
-                                                      int long_blocks, float* __restrict__ grads) {
+__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp,
+                                                      int ld, const int32_t* __restrict__ tbase,
+                                                      int step, const float* __restrict__ contrib,
+                                                      const float* __restrict__ ugrad,
+                                                      int long_blocks, int item_blocks,
+                                                      float* __restrict__ grads) {
   constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
   const int32_t t = *tbase + step + 1;
+  if ((int)blockIdx.x >= long_blocks + item_blocks) {  // users with several triplets
+    const int m = ((int)blockIdx.x - long_blocks - item_blocks) * NG + grp;
+    const int4 r0 = reinterpret_cast<const int4*>(bv.mrec + (int64_t)m * kRec)[0];
+    const int n_multi = bv.meta[4];
+    if (m >= n_multi) return;
+    const int32_t u = r0.x;
+    float* pw = P.W + (int64_t)u * ld + 4 * sub;
+    float4 cur[S], g[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) cur[k] = ld4(pw + 4 * G4 * k);
+    const int32_t su = P.stamp[u];
+    sum_rows<G4, S>(g, ugrad, r0.y, r0.z, ld, sub);
+    const float f = decay_pow(hp.log2a, t - 1 - su);
+#pragma unroll
+    for (int k = 0; k < S; ++k) st4(pw + 4 * G4 * k, sgd4(scale4(cur[k], f), g[k], hp.lr, hp.wd));
+    if (sub == 0) P.stamp[u] = t;
+    return;
+  }
   if ((int)blockIdx.x < long_blocks) {
     __shared__ float4 part[NG][G4 * S];
     const int4 r0 = reinterpret_cast<const int4*>(bv.lrec + (int64_t)blockIdx.x * kRec)[0];
@@ -275,35 +314,38 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table Q, Hyp
   }
 
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib,
+                     const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s) {
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
     if (item_rows)
       k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
-                                                           contrib, item_rows);
+                                                           contrib, ugrad, item_rows);
     else
       k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
-                                                            contrib, nullptr);
+                                                            contrib, ugrad, nullptr);
   }));
   return hipGetLastError();
 }
 
 int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg + 1)); }
 
-hipError_t item_step(const Geom& g, BatchView bv, int B, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, const float* contrib, float* grads,
-                     hipStream_t s) {
+hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                     const int32_t* tbase, int step, const float* contrib, const float* ugrad,
+                     float* grads, hipStream_t s) {
   const int long_blocks = item_long_blocks(B);
   BPRMF_DISPATCH4(g, ({
-    const unsigned blocks =
-        (unsigned)(long_blocks + (2LL * B + kBlock / G4_ - 1) / (kBlock / G4_));
+    constexpr int NG = kBlock / G4_;
+    const int item_blocks = (int)((2LL * B + NG - 1) / NG);
+    const int user_blocks = (int)((B / 2 + NG - 1) / NG);  // multi-triplet users <= B/2
+    const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks);
     if (grads)
-      k_item_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
-                                                           long_blocks, grads);
+      k_item_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
+                                                           ugrad, long_blocks, item_blocks, grads);
     else
-      k_item_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, Q, hp, g.ld, tbase, step, contrib,
-                                                            long_blocks, nullptr);
+      k_item_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
+                                                            contrib, ugrad, long_blocks,
+                                                            item_blocks, nullptr);
   }));
   return hipGetLastError();
 }

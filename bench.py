@@ -6,7 +6,8 @@ A "step" = one BPR-MF training step over one batch of B triplets per GPU: on-dev
 sampling + batch build (amortised: one build launch per chunk of steps, inside the timed region),
 then user_step (gathers, dots, sigmoid, user update, c*P_u per triplet) and item_step (per-item
 fixed-order gradient sum, item update).  N>1: one process per GPU (torch.distributed.run), users
-and items row-sharded, item rows / gradients exchanged with RCCL all-to-all every step.
+and items row-sharded; every step the owners' item rows go to the requesting ranks and their
+gradients come back, both exchanges issued by the library (IPC peer writes over xGMI, or RCCL).
 Workload: 138,493 users x 26,744 items (ml-20m shape, data/ml-20m/README.txt:4), ~1e7 synthetic
 positives (lognormal degree, Zipf items), d=128, num_ng=4, lr=0.01, wd=0.001, B=4096 (the
 reference CLI defaults, BPRMFRecommender.py:53-116).
@@ -97,6 +98,9 @@ def main():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded RCCL path even at one rank (exercises it on one GPU)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"],
+                    help="sharded runner exchange: IPC peer writes (auto: unless a rank cannot map "
+                         "its peers) or RCCL send/recv")
     ap.add_argument("--python-orchestration", action="store_true",
                     help="sharded: per-step Python orchestration over torch.distributed instead of "
                          "the library's runner")
@@ -140,8 +144,8 @@ def main():
                 for s in range(first, first + k):
                     e, st = divmod(s, n_steps)
                     m.step(e, st)
-        else:  # the library's runner: chunks of steps, RCCL exchanges issued from C++
-            m.attach_runner("rccl")
+        else:  # the library's runner: chunks of steps, exchanges issued from C++
+            m.attach_runner(a.transport)
 
             def run(first, k):
                 done = 0
@@ -207,7 +211,8 @@ def main():
                "config": {"workload": "BPR-MF training, ml-20m shape", "users": U, "items": I,
                           "positives": int(len(pos)), "factor_num": d, "batch_size_per_gpu": B,
                           "global_batch": B * world, "num_ng": 4, "lr": 0.01, "wd": 0.001,
-                          "parallelism": (f"users+items row-sharded x{world}, RCCL all-to-all"
+                          "parallelism": (f"users+items row-sharded x{world}, "
+                                          f"{'python/torch.distributed' if a.python_orchestration else m.runner} exchange"
                                           if sharded else "single GPU"),
                           "semantics": "exact batch-synchronous SGD (reference step), lazy weight decay"},
                "roofline": roof, "cpu_baseline": cpu}

@@ -176,6 +176,13 @@ int bprmf_row_stride(bprmf_handle* h, int32_t* ld);
  * steps past a shard's own epoch are empty for it. */
 int bprmf_dist_unique_id(uint8_t* id128);
 int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id128);
+/* IPC transport (one process per GPU, same node): phase 1 allocates the buffers peers write into
+ * and returns their hipIpc handles in blob[BPRMF_IPC_BLOB_BYTES]; the caller all-gathers the
+ * blobs (rank order); phase 2 maps every peer's buffers.  Exchanges are kernels writing straight
+ * into the peers' memory over xGMI, completion by per-source flags (no host round trip). */
+#define BPRMF_IPC_BLOB_BYTES 512
+int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob);
+int bprmf_dist_init_ipc(bprmf_handle* h, const uint8_t* blobs);
 int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group);
 /* Steps [first_step, first_step+n_steps) of `epoch` from the device sampler (BPRMFRecommender.py:
  * 157-178 over this shard's users); stats: this shard's triplets and loss. */

@@ -42,6 +42,7 @@ class KProf(ctypes.Structure):
         return {k: dict(count=int(self.count[n]), ms=float(self.ms[n])) for n, k in enumerate(self.KINDS)}
 
 
+IPC_BLOB_BYTES = 512  # BPRMF_IPC_BLOB_BYTES
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 # name -> argtypes (restype int unless noted); mirrors include/bprmf.h
@@ -78,6 +79,8 @@ SIGNATURES = {
     "bprmf_dist_unique_id": [_P],
     "bprmf_dist_init_rccl": [_P, _P],
     "bprmf_dist_init_loopback": [_P, _I64],
+    "bprmf_dist_ipc_export": [_P, _P],
+    "bprmf_dist_init_ipc": [_P, _P],
     "bprmf_dist_train_steps": [_P, ctypes.c_uint32, _I64, _I64, _P],
     "bprmf_dist_train_replay": [_P, _P, _P, _P, _I64, _P],
     "bprmf_row_stride": [_P, ctypes.POINTER(ctypes.c_int32)],

@@ -78,6 +78,7 @@ int bprmf::check_err_flag(bprmf_handle* h) {
   HIPCHK(hipStreamSynchronize(h->stream));
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
+    if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
     return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
   }

@@ -2,6 +2,9 @@
 //
 // One handle per GPU (one process per GPU under torch.distributed.run).  The runner drives whole
 // chunks of steps from C++: no Python per step.  Transports:
+//   ipc       a push kernel writes each peer's block straight into the peer's buffer (mapped with
+//             hipIpc; xGMI peer writes) and raises a per-source flag; a one-block wait kernel
+//             spins on this rank's flags.  A few us per exchange, no host in the loop.
 //   rccl      an RCCL communicator owned by the handle (ncclCommInitRank from a unique id the
 //             caller broadcasts); per-peer blocks move with grouped ncclSend/ncclRecv over xGMI.
 //   loopback  handles of one process exchanging through a shared table + device copies (the
@@ -16,6 +19,7 @@
 // without a per-step count exchange.  Semantics: SURVEY.md §8e — a world-W run with per-rank
 // batch B equals one step over the union batch (BPRMFRecommender.py:172-176).
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -28,13 +32,46 @@
 
 namespace bprmf {
 
+enum XKind { X_ROWS = 0, X_GRADS = 1, X_IDS = 2, X_MAX = 3, X_KINDS = 4 };
+
+struct Xchg {  // one all-to-all of per-peer blocks
+  int kind;
+  const void* const* send;  // send[p]: the block for rank p (nullptr at this rank: already placed)
+  void* const* recv;        // recv[p]: where the block from rank p lands (this rank's memory)
+  size_t bytes;
+  const int32_t* tbase;  // per-step exchange: sequence number *tbase + k + 1 (graph-safe)
+  int k;
+  int32_t seq;  // per-chunk exchange (tbase == nullptr)
+};
+
 struct Transport {
   virtual ~Transport() = default;
-  // all-to-all of per-peer blocks of `bytes`: send[p] goes to rank p, recv[p] comes from rank p;
-  // send[rank] == nullptr: no self block (the caller placed it already)
-  virtual int exchange(bprmf_handle* h, const void* const* send, void* const* recv, size_t bytes) = 0;
-  // in-place max over ranks of one device int32
-  virtual int max_i32(bprmf_handle* h, int32_t* dev) = 0;
+  virtual int exchange(bprmf_handle* h, const Xchg& x) = 0;
+  // in-place max over ranks of one device int32; vals: [world] scratch peers may write into
+  virtual int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) {
+    const int W = h->cfg.world;
+    std::vector<const void*> sp(W, dev);
+    std::vector<void*> rp(W);
+    for (int p = 0; p < W; ++p) rp[p] = vals + p;
+    if (int r = exchange(h, Xchg{X_MAX, sp.data(), rp.data(), 4, nullptr, 0, seq})) return r;
+    HIPCHK(max_vals(vals, W, dev, h->stream));
+    return 0;
+  }
+  // exchange() only enqueues stream work (no host synchronisation): hipGraph-capturable
+  virtual bool capturable() const { return false; }
+  virtual bool ready() const { return true; }
+  // device memory that peers write into (the IPC transport exports it)
+  virtual int alloc_shared(bprmf_handle* h, int kind, size_t bytes, void** p) {
+    (void)h;
+    (void)kind;
+    *p = nullptr;
+    HIPCHK(hipMalloc(p, bytes));
+    return 0;
+  }
+  virtual void free_shared(void* p) {
+    if (p) (void)!hipFree(p);
+  }
+  bool self_exchange = false;  // test hook: this rank's own blocks also go through the transport
 };
 
 #define NCCLCHK(x)                                                                      \
@@ -48,23 +85,106 @@ struct RcclTransport final : Transport {
   ~RcclTransport() override {
     if (comm) ncclCommDestroy(comm);
   }
-  int exchange(bprmf_handle* h, const void* const* send, void* const* recv, size_t bytes) override {
-    if (!bytes) return 0;
+  bool capturable() const override { return true; }
+  int exchange(bprmf_handle* h, const Xchg& x) override {
+    if (!x.bytes) return 0;
     const int W = h->cfg.world, R = h->cfg.rank;
-    if (send[R]) HIPCHK(hipMemcpyAsync(recv[R], send[R], bytes, hipMemcpyDeviceToDevice, h->stream));
-    if (W == 1) return 0;
+    if (x.send[R] && !self_exchange)
+      HIPCHK(hipMemcpyAsync(x.recv[R], x.send[R], x.bytes, hipMemcpyDeviceToDevice, h->stream));
+    if (W == 1 && !self_exchange) return 0;
     NCCLCHK(ncclGroupStart());
     for (int p = 0; p < W; ++p) {
-      if (p == R) continue;
-      NCCLCHK(ncclSend(send[p], bytes, ncclUint8, p, comm, h->stream));
-      NCCLCHK(ncclRecv(recv[p], bytes, ncclUint8, p, comm, h->stream));
+      if (p == R && (!self_exchange || !x.send[R])) continue;
+      NCCLCHK(ncclSend(x.send[p], x.bytes, ncclUint8, p, comm, h->stream));
+      NCCLCHK(ncclRecv(x.recv[p], x.bytes, ncclUint8, p, comm, h->stream));
     }
     NCCLCHK(ncclGroupEnd());
     return 0;
   }
-  int max_i32(bprmf_handle* h, int32_t* dev) override {
+  int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) override {
+    (void)vals;
+    (void)seq;
     if (h->cfg.world == 1) return 0;
     NCCLCHK(ncclAllReduce(dev, dev, 1, ncclInt32, ncclMax, comm, h->stream));
+    return 0;
+  }
+};
+
+// ---- IPC: blocks pushed by a kernel straight into the peers' buffers (xGMI peer writes) -----
+// Peers write into "landing" buffers, allocated uncached (their writes bypass this GPU's L2, so
+// no reader sees a stale line) and exported with hipIpcGetMemHandle; each rank maps the peers'
+// handles.  Layouts are symmetric: the block rank R sends to p lands in p's buffer at the offset
+// where R's own buffer keeps the block from R.  Completion: per-(kind, source) flags carrying the
+// exchange's sequence number (the step number for per-step exchanges).  Rows and request lists
+// are then copied by a receive kernel (which waits per peer) into ordinary cached buffers, since
+// the step kernels read them many times; gradients and capacities are read once, in place.
+constexpr int kIpcHandles = X_KINDS + 1;  // the four landing buffers + the flag array
+struct IpcTransport final : Transport {
+  int world = 0, rank = 0;
+  void* recv_base[X_KINDS] = {};          // the buffers the runner reads (alloc_shared)
+  void* local[kIpcHandles] = {};          // this rank's landing buffers (X_KINDS: flags)
+  std::vector<void*> remote[kIpcHandles];  // [world] peers' mappings (self: local)
+  uint32_t* done = nullptr;                // [X_KINDS] last-block counters of the push kernels
+  bool opened = false;
+  static bool copied(int kind) { return kind == X_ROWS || kind == X_IDS; }
+  ~IpcTransport() override {
+    for (int b = 0; b < kIpcHandles; ++b)
+      for (int p = 0; p < (int)remote[b].size(); ++p)
+        if (p != rank && remote[b][p]) (void)!hipIpcCloseMemHandle(remote[b][p]);
+    for (int b = 0; b < kIpcHandles; ++b) {
+      if (b < X_KINDS && copied(b) && recv_base[b]) (void)!hipFree(recv_base[b]);
+      if (local[b]) (void)!hipFree(local[b]);
+    }
+    if (done) (void)!hipFree(done);
+  }
+  bool capturable() const override { return true; }
+  bool ready() const override { return opened; }
+  int alloc_shared(bprmf_handle* h, int kind, size_t bytes, void** p) override {
+    (void)h;
+    *p = nullptr;
+    HIPCHK(hipExtMallocWithFlags(&local[kind], std::max<size_t>(bytes, 256), hipDeviceMallocUncached));
+    if (copied(kind)) {
+      HIPCHK(hipMalloc(&recv_base[kind], std::max<size_t>(bytes, 256)));
+    } else {
+      recv_base[kind] = local[kind];
+    }
+    *p = recv_base[kind];
+    return 0;
+  }
+  void free_shared(void* p) override { (void)p; }  // owned (and freed) by the transport
+  int32_t* flags() const { return static_cast<int32_t*>(local[X_KINDS]); }
+  int exchange(bprmf_handle* h, const Xchg& x) override {
+    if (!x.bytes) return 0;
+    if (world == 1) {  // no peers: only a self block, if the caller did not place it
+      if (x.send[0]) HIPCHK(hipMemcpyAsync(x.recv[0], x.send[0], x.bytes, hipMemcpyDeviceToDevice, h->stream));
+      return 0;
+    }
+    PushArgs a{};
+    const char* base = static_cast<const char*>(recv_base[x.kind]);
+    const ptrdiff_t off = static_cast<const char*>(x.recv[rank]) - base;  // this rank's block
+    for (int p = 0; p < world; ++p) {
+      a.src[p] = x.send[p];
+      if (p == rank) {
+        a.dst[p] = x.recv[p];
+      } else {
+        a.dst[p] = static_cast<char*>(remote[x.kind][p]) + off;
+        a.flag[p] = static_cast<int32_t*>(remote[X_KINDS][p]) + x.kind * kMaxWorld + rank;
+      }
+    }
+    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, done + x.kind, h->stream));
+    const int32_t* fl = flags() + x.kind * kMaxWorld;
+    if (!copied(x.kind)) {
+      HIPCHK(ipc_wait(fl, world, rank, x.tbase, x.k, x.seq, h->d_err, h->stream));
+      return 0;
+    }
+    PushArgs c{};  // landing -> working buffer, per peer
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      const ptrdiff_t o = static_cast<const char*>(x.recv[p]) - base;
+      c.src[p] = static_cast<const char*>(local[x.kind]) + o;
+      c.dst[p] = x.recv[p];
+    }
+    HIPCHK(ipc_recv(c, world, rank, (int64_t)x.bytes, fl, x.tbase, x.k, x.seq, h->d_err, h->stream));
     return 0;
   }
 };
@@ -102,15 +222,15 @@ struct LoopTransport final : Transport {
       delete g;
     }
   }
-  int exchange(bprmf_handle* h, const void* const* send, void* const* recv, size_t bytes) override {
+  int exchange(bprmf_handle* h, const Xchg& x) override {
     const int W = h->cfg.world, R = h->cfg.rank;
     HIPCHK(hipStreamSynchronize(h->stream));  // this shard's blocks are complete
-    g->send[R] = send;
+    g->send[R] = x.send;
     g->barrier();
     int rc = 0;
-    for (int p = 0; p < W && !rc && bytes; ++p) {
+    for (int p = 0; p < W && !rc && x.bytes; ++p) {
       if (!g->send[p][R]) continue;
-      const hipError_t e = hipMemcpyAsync(recv[p], g->send[p][R], bytes, hipMemcpyDeviceToDevice, h->stream);
+      const hipError_t e = hipMemcpyAsync(x.recv[p], g->send[p][R], x.bytes, hipMemcpyDeviceToDevice, h->stream);
       if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "loopback copy: %s", hipGetErrorString(e));
     }
     const hipError_t e = hipStreamSynchronize(h->stream);
@@ -118,7 +238,9 @@ struct LoopTransport final : Transport {
     g->barrier();  // every peer has read this shard's send blocks
     return rc;
   }
-  int max_i32(bprmf_handle* h, int32_t* dev) override {
+  int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) override {
+    (void)vals;
+    (void)seq;
     int32_t v = 0;
     HIPCHK(hipMemcpyAsync(&v, dev, 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -132,29 +254,56 @@ struct LoopTransport final : Transport {
   }
 };
 
+struct DistGraph {  // a captured chunk of sharded steps (fixed n, cap and buffers)
+  int64_t n = 0;
+  int cap = 0;
+  const void* bufs[4] = {};
+  hipGraphExec_t exec = nullptr;
+};
+
+// Buffers of the runner.  Sizes are fixed at attach (peers of the IPC transport hold mappings of
+// the shared ones): S = slot stride per owner, nmax = steps per chunk.  The request lists and
+// their apply plans alternate between two parities, so a rank may publish chunk c+1's requests
+// while a slower peer still applies chunk c.
 struct DistState {
   Transport* tr = nullptr;
+  std::vector<DistGraph> graphs;
   int S = 0;             // requester-side slot stride per owner (rows)
   int cap = 0;           // rows per peer per step of the current chunk
-  int64_t ids_n = 0, aplan_n = 0;
-  int32_t* ids_send = nullptr;  // [W][n][cap]
-  int32_t* ids_recv = nullptr;  // [W][n][cap]
-  int32_t* aplan = nullptr;     // [n][W][cap][W]
+  int64_t nmax = 0;      // steps per chunk
+  int64_t chunks = 0;    // chunks run (parity, per-chunk sequence numbers)
+  int64_t aplan_n[2] = {0, 0};
+  int32_t* ids_send = nullptr;     // [W][n][cap]
+  int32_t* ids_recv = nullptr;     // shared, 2 parities x [W][nmax][S]
+  int32_t* aplan[2] = {nullptr, nullptr};  // [n][W][cap][W] per parity
+  int32_t* vals = nullptr;         // shared, 2 parities x [W] (capacity max)
   int32_t* d_cap = nullptr;
   float* rows_send = nullptr;   // owner:     [W][cap][ld]
-  float* rows_recv = nullptr;   // requester: [W][S][ld] (slot order)
+  float* rows_recv = nullptr;   // shared, requester: [W][S][ld] (slot order)
   float* grads_send = nullptr;  // requester: [W][S][ld]
-  float* grads_recv = nullptr;  // owner:     [W][cap][ld]
+  float* grads_recv = nullptr;  // shared, owner: [W][cap][ld] (cap <= S)
 };
+
+static void drop_dist_graphs(DistState* d) {
+  for (auto& g : d->graphs)
+    if (g.exec) (void)!hipGraphExecDestroy(g.exec);
+  d->graphs.clear();
+}
 
 void dist_free(DistState* d) {
   if (!d) return;
-  delete d->tr;
-  void* ptrs[] = {d->ids_send, d->ids_recv, d->aplan, d->d_cap, d->rows_send, d->rows_recv,
-                  d->grads_send, d->grads_recv};
+  drop_dist_graphs(d);
+  void* shared[] = {d->ids_recv, d->vals, d->rows_recv, d->grads_recv};
+  for (void* p : shared) d->tr->free_shared(p);
+  void* ptrs[] = {d->ids_send, d->aplan[0], d->aplan[1], d->d_cap, d->rows_send, d->grads_send};
   for (void* p : ptrs)
-    if (p) hipFree(p);
+    if (p) (void)!hipFree(p);
+  delete d->tr;
   delete d;
+}
+
+static int64_t dist_chunk_steps(const bprmf_handle* h) {
+  return std::max<int64_t>(1, (int64_t(1) << 20) / h->cfg.batch_size);
 }
 
 static int dist_attach(bprmf_handle* h, Transport* tr) {
@@ -169,16 +318,27 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   }
   auto* d = new DistState();
   d->tr = tr;
+  tr->self_exchange = getenv("BPRMF_DIST_SELF_EXCHANGE") != nullptr;
   h->dist = d;
   const int64_t W = h->cfg.world, B = h->cfg.batch_size;
   const int64_t iloc = (h->cfg.item_num + W - 1) / W;
   d->S = (int)std::min<int64_t>(2 * B, iloc);
+  d->nmax = dist_chunk_steps(h);
   const int64_t rows = W * d->S * h->geom.ld;
+  const int64_t ids = W * d->nmax * d->S;
+  void* p = nullptr;
+  if (int r = tr->alloc_shared(h, X_ROWS, sizeof(float) * rows, &p)) return r;
+  d->rows_recv = static_cast<float*>(p);
+  if (int r = tr->alloc_shared(h, X_GRADS, sizeof(float) * rows, &p)) return r;
+  d->grads_recv = static_cast<float*>(p);
+  if (int r = tr->alloc_shared(h, X_IDS, sizeof(int32_t) * 2 * ids, &p)) return r;
+  d->ids_recv = static_cast<int32_t*>(p);
+  if (int r = tr->alloc_shared(h, X_MAX, sizeof(int32_t) * 2 * W, &p)) return r;
+  d->vals = static_cast<int32_t*>(p);
   if (int r = dalloc(&d->d_cap, 1)) return r;
+  if (int r = dalloc(&d->ids_send, ids)) return r;
   if (int r = dalloc(&d->rows_send, rows)) return r;
-  if (int r = dalloc(&d->rows_recv, rows)) return r;
   if (int r = dalloc(&d->grads_send, rows)) return r;
-  if (int r = dalloc(&d->grads_recv, rows)) return r;
   // rows past a peer's request count are sent but never read; keep them finite
   HIPCHK(hipMemsetAsync(d->rows_send, 0, sizeof(float) * rows, h->stream));
   HIPCHK(hipMemsetAsync(d->grads_send, 0, sizeof(float) * rows, h->stream));
@@ -186,26 +346,100 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   return 0;
 }
 
-static int ensure_plan_bufs(bprmf_handle* h, int64_t n, int cap) {
+static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   DistState* d = h->dist;
   const int64_t W = h->cfg.world;
-  const int64_t ids = W * n * cap, ap = ids * W;
-  if (ids > d->ids_n) {
-    if (d->ids_send) HIPCHK(hipFree(d->ids_send));
-    if (d->ids_recv) HIPCHK(hipFree(d->ids_recv));
-    d->ids_send = d->ids_recv = nullptr;
-    d->ids_n = 0;
-    if (int r = dalloc(&d->ids_send, ids)) return r;
-    if (int r = dalloc(&d->ids_recv, ids)) return r;
-    d->ids_n = ids;
+  const int64_t ap = n * W * std::max(cap, 1) * W;
+  if (ap <= d->aplan_n[par]) return 0;
+  if (d->aplan[par]) HIPCHK(hipFree(d->aplan[par]));
+  d->aplan[par] = nullptr;
+  d->aplan_n[par] = 0;
+  if (int r = dalloc(&d->aplan[par], ap)) return r;
+  d->aplan_n[par] = ap;
+  return 0;
+}
+
+// The per-step launches and exchanges of a chunk of n steps (plan of `cap` rows per peer):
+// enqueued eagerly or captured into a hipGraph by dist_chunk.
+static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
+                         const int32_t* aplan, bool prof_kernels) {
+  DistState* d = h->dist;
+  const int B = h->cfg.batch_size, W = h->cfg.world;
+  const int ld = h->geom.ld;
+  const BatchBuf bb{h->d_batch, B};
+  // this rank's own requests bypass the transport (gather into its slots, apply in place)
+  const int self = d->tr->self_exchange ? -1 : h->cfg.rank;
+  const int64_t R = h->cfg.rank;
+  const size_t row_bytes = sizeof(float) * (size_t)cap * ld;
+  std::vector<const void*> sp(W);
+  std::vector<void*> rp(W);
+  for (int64_t k = 0; k < n; ++k) {
+    const BatchView v = bb.view(k);
+    const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
+    {
+      ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
+      HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase,
+                               d->rows_send, self, d->rows_recv + R * d->S * ld, h->stream));
+    }
+    for (int p = 0; p < W; ++p) {
+      sp[p] = p == self ? nullptr : d->rows_send + (int64_t)p * cap * ld;
+      rp[p] = d->rows_recv + (int64_t)p * d->S * ld;
+    }
+    if (int r = d->tr->exchange(h, Xchg{X_ROWS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0}))
+      return r;
+    {
+      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
+      HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
+                       h->d_contrib, h->d_ugrad, d->rows_recv, h->stream));
+    }
+    {
+      ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
+      HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                       h->d_ugrad, d->grads_send, h->stream));
+    }
+    for (int p = 0; p < W; ++p) {
+      sp[p] = p == self ? nullptr : d->grads_send + (int64_t)p * d->S * ld;
+      rp[p] = d->grads_recv + (int64_t)p * cap * ld;
+    }
+    if (int r = d->tr->exchange(h, Xchg{X_GRADS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0}))
+      return r;
+    {
+      ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
+      HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
+                              d->grads_recv, self, d->grads_send + R * d->S * ld, h->stream));
+    }
   }
-  if (ap > d->aplan_n) {
-    if (d->aplan) HIPCHK(hipFree(d->aplan));
-    d->aplan = nullptr;
-    d->aplan_n = 0;
-    if (int r = dalloc(&d->aplan, ap)) return r;
-    d->aplan_n = ap;
+  return 0;
+}
+
+static int launch_dist_graph(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
+                             const int32_t* aplan) {
+  DistState* d = h->dist;
+  const void* bufs[4] = {h->d_batch, ids_recv, aplan, h->d_contrib};
+  DistGraph* ge = nullptr;
+  for (auto& g : d->graphs)
+    if (g.n == n && g.cap == cap && std::equal(bufs, bufs + 4, g.bufs)) ge = &g;
+  if (!ge) {
+    if (d->graphs.size() >= 8) drop_dist_graphs(d);
+    DistGraph ng;
+    ng.n = n;
+    ng.cap = cap;
+    std::copy(bufs, bufs + 4, ng.bufs);
+    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = enqueue_steps(h, n, cap, ids_recv, aplan, false);
+    hipGraph_t graph = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+    if (rc || e2 != hipSuccess) {
+      if (graph) (void)!hipGraphDestroy(graph);
+      return rc ? rc : fail(BPRMF_E_HIP, "sharded step graph capture: %s", hipGetErrorString(e2));
+    }
+    const hipError_t e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
+    (void)!hipGraphDestroy(graph);
+    if (e != hipSuccess) return fail(BPRMF_E_HIP, "sharded step graph instantiate: %s", hipGetErrorString(e));
+    d->graphs.push_back(ng);
+    ge = &d->graphs.back();
   }
+  HIPCHK(hipGraphLaunch(ge->exec, h->stream));
   return 0;
 }
 
@@ -214,11 +448,13 @@ static int ensure_plan_bufs(bprmf_handle* h, int64_t n, int cap) {
 static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n,
                       const int32_t* ru, const int32_t* ri, const int32_t* rj) {
   DistState* d = h->dist;
-  const int B = h->cfg.batch_size, W = h->cfg.world, R = h->cfg.rank;
-  const int ld = h->geom.ld;
+  const int B = h->cfg.batch_size, W = h->cfg.world;
+  if (n > d->nmax) return fail(BPRMF_E_INVALID, "chunk of %lld steps > %lld", (long long)n, (long long)d->nmax);
   if ((int64_t)h->t + n >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   if (int r = ensure_seg(h, n)) return r;
   const BatchBuf bb{h->d_batch, B};
+  const int par = (int)(d->chunks & 1);
+  const int32_t seq = (int32_t)(d->chunks + 1);
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
   int64_t first_slot = 0, n_slots = n * B;
   if (!ru) {
@@ -235,61 +471,40 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   // exchange capacity of the chunk: the largest request count of any (rank, step, owner)
   HIPCHK(hipMemsetAsync(d->d_cap, 0, 4, h->stream));
   HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
-  if (int r = d->tr->max_i32(h, d->d_cap)) return r;
+  if (int r = d->tr->max_i32(h, d->d_cap, d->vals + par * W, seq)) return r;
   int32_t cap = 0;
   HIPCHK(hipMemcpyAsync(&cap, d->d_cap, 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  if (int r = check_err_flag(h)) return r;
   if (cap < 0 || cap > d->S) return fail(BPRMF_E_STATE, "exchange capacity %d outside [0, %d]", cap, d->S);
+  const bool graph = h->use_graphs && d->tr->capturable() && cap > 0;
+  if (graph) cap = std::min(d->S, (cap + 63) / 64 * 64);  // few distinct plans: graphs get reused
   d->cap = cap;
-  if (int r = ensure_plan_bufs(h, n, std::max(cap, 1))) return r;
-  std::vector<const void*> sp(W);
-  std::vector<void*> rp(W);
+  if (int r = ensure_aplan(h, par, n, cap)) return r;
+  int32_t* ids_recv = d->ids_recv + (int64_t)par * W * d->nmax * d->S;
+  int32_t* aplan = d->aplan[par];
   if (cap > 0) {
+    std::vector<const void*> sp(W);
+    std::vector<void*> rp(W);
     HIPCHK(dist_pack_ids(bb, n, W, cap, d->ids_send, h->stream));
     for (int p = 0; p < W; ++p) {
       sp[p] = d->ids_send + (int64_t)p * n * cap;
-      rp[p] = d->ids_recv + (int64_t)p * n * cap;
+      rp[p] = ids_recv + (int64_t)p * n * cap;
     }
-    if (int r = d->tr->exchange(h, sp.data(), rp.data(), sizeof(int32_t) * n * cap)) return r;
-    HIPCHK(dist_owner_plan(d->ids_recv, n, W, cap, d->aplan, h->stream));
+    const bool se = d->tr->self_exchange;
+    d->tr->self_exchange = false;  // the request lists always include the self block
+    const int r = d->tr->exchange(h, Xchg{X_IDS, sp.data(), rp.data(), sizeof(int32_t) * n * cap,
+                                          nullptr, 0, seq});
+    d->tr->self_exchange = se;
+    if (r) return r;
+    HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, h->stream));
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));
-  const size_t row_bytes = sizeof(float) * (size_t)cap * ld;
-  for (int64_t k = 0; k < n; ++k) {
-    const BatchView v = bb.view(k);
-    const bool sampled = ((h->t + k) % kProfStride) == 0;
-    {
-      ProfScope ps(h, BPRMF_KPROF_OWNER, sampled && !ea);
-      HIPCHK(dist_owner_gather(h->geom, h->Q, d->ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase,
-                               d->rows_send, R, d->rows_recv + (int64_t)R * d->S * ld, h->stream));
-    }
-    for (int p = 0; p < W; ++p) {
-      sp[p] = p == R ? nullptr : d->rows_send + (int64_t)p * cap * ld;
-      rp[p] = d->rows_recv + (int64_t)p * d->S * ld;
-    }
-    if (int r = d->tr->exchange(h, sp.data(), rp.data(), row_bytes)) return r;
-    {
-      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled && !ea);
-      HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                       h->d_contrib, h->d_ugrad, d->rows_recv, h->stream));
-    }
-    {
-      ProfScope ps(h, BPRMF_KPROF_APPLY, sampled && !ea);
-      HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                       h->d_ugrad, d->grads_send, h->stream));
-    }
-    for (int p = 0; p < W; ++p) {
-      sp[p] = p == R ? nullptr : d->grads_send + (int64_t)p * d->S * ld;
-      rp[p] = d->grads_recv + (int64_t)p * cap * ld;
-    }
-    if (int r = d->tr->exchange(h, sp.data(), rp.data(), row_bytes)) return r;
-    {
-      ProfScope ps(h, BPRMF_KPROF_OWNER, sampled && !ea);
-      HIPCHK(dist_owner_apply(h->geom, h->Q, d->ids_recv, d->aplan, n, W, cap, (int)k, h->hp,
-                              h->d_tbase, d->grads_recv, R, d->grads_send + (int64_t)R * d->S * ld,
-                              h->stream));
-    }
+  if (graph) {
+    if (int r = launch_dist_graph(h, n, cap, ids_recv, aplan)) return r;
+  } else {
+    if (int r = enqueue_steps(h, n, cap, ids_recv, aplan, !ea)) return r;
   }
   if (ea) {
     hipEvent_t eb = prof_event(h);
@@ -300,11 +515,8 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     }
   }
   h->t += (int32_t)n;
+  ++d->chunks;
   return 0;
-}
-
-static int64_t dist_chunk_steps(const bprmf_handle* h) {
-  return std::max<int64_t>(1, (int64_t(1) << 20) / h->cfg.batch_size);
 }
 
 }  // namespace bprmf
@@ -337,6 +549,53 @@ int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id) {
   return dist_attach(h, tr);
 }
 
+int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
+  if (!h || !blob) return fail(BPRMF_E_INVALID, "null argument");
+  if (int r = set_dev(h)) return r;
+  static_assert(sizeof(hipIpcMemHandle_t) * kIpcHandles <= BPRMF_IPC_BLOB_BYTES, "blob size");
+  auto* tr = new IpcTransport();
+  tr->world = h->cfg.world;
+  tr->rank = h->cfg.rank;
+  const size_t flag_bytes = sizeof(int32_t) * X_KINDS * kMaxWorld;
+  hipError_t e = hipExtMallocWithFlags(&tr->local[X_KINDS], flag_bytes, hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMalloc((void**)&tr->done, sizeof(uint32_t) * X_KINDS);
+  if (e == hipSuccess) e = hipMemset(tr->local[X_KINDS], 0, flag_bytes);
+  if (e == hipSuccess) e = hipMemset(tr->done, 0, sizeof(uint32_t) * X_KINDS);
+  if (e != hipSuccess) {
+    delete tr;
+    return fail(BPRMF_E_HIP, "ipc transport buffers: %s", hipGetErrorString(e));
+  }
+  if (int r = dist_attach(h, tr)) return r;
+  memset(blob, 0, BPRMF_IPC_BLOB_BYTES);
+  for (int b = 0; b < kIpcHandles; ++b) {
+    hipIpcMemHandle_t hd;
+    HIPCHK(hipIpcGetMemHandle(&hd, tr->local[b]));
+    memcpy(blob + b * sizeof hd, &hd, sizeof hd);
+  }
+  return 0;
+}
+
+int bprmf_dist_init_ipc(bprmf_handle* h, const uint8_t* blobs) {
+  if (!h || !blobs) return fail(BPRMF_E_INVALID, "null argument");
+  auto* tr = h->dist ? dynamic_cast<IpcTransport*>(h->dist->tr) : nullptr;
+  if (!tr) return fail(BPRMF_E_STATE, "call bprmf_dist_ipc_export first");
+  if (tr->opened) return fail(BPRMF_E_STATE, "ipc transport already initialised");
+  if (int r = set_dev(h)) return r;
+  for (int b = 0; b < kIpcHandles; ++b) tr->remote[b].assign(tr->world, nullptr);
+  for (int p = 0; p < tr->world; ++p)
+    for (int b = 0; b < kIpcHandles; ++b) {
+      if (p == tr->rank) {
+        tr->remote[b][p] = tr->local[b];
+        continue;
+      }
+      hipIpcMemHandle_t hd;
+      memcpy(&hd, blobs + (size_t)p * BPRMF_IPC_BLOB_BYTES + b * sizeof hd, sizeof hd);
+      HIPCHK(hipIpcOpenMemHandle(&tr->remote[b][p], hd, hipIpcMemLazyEnablePeerAccess));
+    }
+  tr->opened = true;
+  return 0;
+}
+
 int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (int r = set_dev(h)) return r;
@@ -364,7 +623,8 @@ int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group) {
 int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
                            bprmf_stats* st) {
   if (!h || first_step < 0 || n_steps < 0) return fail(BPRMF_E_INVALID, "bad arguments");
-  if (!h->dist) return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
+  if (!h->dist || !h->dist->tr->ready())
+    return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
   if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
   if (int r = begin_call(h)) return r;
   const int64_t chunk = dist_chunk_steps(h);
@@ -382,7 +642,8 @@ int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, 
 int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
                             int64_t n_steps, bprmf_stats* st) {
   if (!h || n_steps < 0 || (n_steps > 0 && (!u || !i || !j))) return fail(BPRMF_E_INVALID, "bad arguments");
-  if (!h->dist) return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
+  if (!h->dist || !h->dist->tr->ready())
+    return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
   const int64_t B = h->cfg.batch_size, n = n_steps * B, W = h->cfg.world, R = h->cfg.rank;
   int64_t valid = 0;
   for (int64_t k = 0; k < n; ++k) {

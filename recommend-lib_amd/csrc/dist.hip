@@ -13,6 +13,8 @@
 // K1/K2 (step.hip, sharded instantiations) -> exchange of per-slot gradients ->
 // k_owner_apply (fixed-order sum, lazy decay + SGD, one writer per row).
 // Reference semantics: the same SGD step as BPRMFRecommender.py:172-176 on the union batch.
+#include <algorithm>
+
 #include "device_common.h"
 
 namespace bprmf {
@@ -166,6 +168,134 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
                     fmaf(-lr, fmaf(wd, v.z, g[s].z), v.z), fmaf(-lr, fmaf(wd, v.w, g[s].w), v.w)));
   }
   if (sub == 0) Q.stamp[row] = t;
+}
+
+// ---- IPC transport: blocks pushed straight into the peers' buffers over xGMI ----------------
+// Per-peer blocks of `bytes` (a multiple of 4) are copied into a.dst[p] (a peer's buffer mapped
+// through hipIpc, or this rank's own buffer for the self block); every block fences at system
+// scope (waits for its stores' acknowledgements), and the last block to finish stores the
+// exchange's sequence number into each peer's flag for this rank.  seq = *tbase + k + 1 (per-step exchanges: graph-safe) or `seq`.
+__global__ void k_ipc_push(PushArgs a, int world, int64_t bytes, const int32_t* __restrict__ tbase,
+                           int k, int32_t seq, uint32_t* __restrict__ done) {
+  const int64_t n16 = bytes / 16, per = n16 + (bytes % 16) / 4, total = per * world;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(x / per);
+    const int64_t u = x - p * per;
+    if (!a.src[p]) continue;
+    if (u < n16)
+      reinterpret_cast<float4*>(a.dst[p])[u] = reinterpret_cast<const float4*>(a.src[p])[u];
+    else
+      reinterpret_cast<int32_t*>(a.dst[p])[4 * n16 + (u - n16)] =
+          reinterpret_cast<const int32_t*>(a.src[p])[4 * n16 + (u - n16)];
+  }
+  // The destinations are uncached (peer landing buffers, or this rank's own buffer for the self
+  // block, which the next kernel reads after the kernel boundary): waiting for the stores'
+  // acknowledgements makes them visible; a system-scope fence would also write back the whole
+  // L2 of this XCD, once per block.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // every block's stores are acknowledged
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int32_t s = tbase ? *tbase + k + 1 : seq;
+      for (int p = 0; p < world; ++p)
+        if (a.flag[p]) __hip_atomic_store(a.flag[p], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// wait until every peer's flag for this exchange reached its sequence number.  A wait that
+// outlives ~10 s (a peer died) raises err bit 4 and gives up instead of hanging the queue.
+__global__ void k_ipc_wait(const int32_t* flags, int world, int self, const int32_t* __restrict__ tbase,
+                           int k, int32_t seq, int32_t* __restrict__ err) {
+  const int32_t s = tbase ? *tbase + k + 1 : seq;
+  const int p = threadIdx.x;
+  if (p < world && p != self) {
+    int64_t spins = 0;
+    // relaxed: the flag and the data it guards live in uncached memory, so no cache needs
+    // invalidating (an acquire at system scope would invalidate this XCD's L2 every poll)
+    while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > 150000000) {
+        atomicOr(err, 4);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// receive side of a row/id exchange: per peer, wait for its flag, then copy its block from the
+// uncached landing buffer into the cached working buffer the step kernels read (rows read many
+// times, e.g. a hot item by every triplet that references it, must not be served uncached).
+// blocks_per_peer blocks per peer; a block waits only for its own peer.
+__global__ void k_ipc_recv(PushArgs a, int world, int self, int64_t bytes, int blocks_per_peer,
+                           const int32_t* flags, const int32_t* __restrict__ tbase, int k,
+                           int32_t seq, int32_t* __restrict__ err) {
+  const int p = blockIdx.x / blocks_per_peer;
+  if (p >= world || p == self || !a.src[p]) return;
+  const int32_t s = tbase ? *tbase + k + 1 : seq;
+  if (threadIdx.x == 0) {
+    int64_t spins = 0;
+    while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > 150000000) {
+        atomicOr(err, 4);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t n16 = bytes / 16, per = n16 + (bytes % 16) / 4;
+  const int64_t stride = (int64_t)blocks_per_peer * blockDim.x;
+  for (int64_t u = (blockIdx.x % blocks_per_peer) * (int64_t)blockDim.x + threadIdx.x; u < per;
+       u += stride) {
+    if (u < n16)
+      reinterpret_cast<float4*>(a.dst[p])[u] = reinterpret_cast<const float4*>(a.src[p])[u];
+    else
+      reinterpret_cast<int32_t*>(a.dst[p])[4 * n16 + (u - n16)] =
+          reinterpret_cast<const int32_t*>(a.src[p])[4 * n16 + (u - n16)];
+  }
+}
+
+hipError_t ipc_recv(const PushArgs& a, int world, int self, int64_t bytes, const int32_t* flags,
+                    const int32_t* tbase, int k, int32_t seq, int32_t* err, hipStream_t s) {
+  const int64_t units = bytes / 16 + (bytes % 16) / 4;
+  const int bpp = (int)std::max<int64_t>(1, std::min<int64_t>(256, (units + 4 * kBlock - 1) / (4 * kBlock)));
+  k_ipc_recv<<<(unsigned)(bpp * world), kBlock, 0, s>>>(a, world, self, bytes, bpp, flags, tbase, k,
+                                                        seq, err);
+  return hipGetLastError();
+}
+
+__global__ void k_max_vals(const int32_t* __restrict__ vals, int world, int32_t* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    int32_t m = 0;
+    for (int p = 0; p < world; ++p) m = max(m, vals[p]);
+    *out = m;
+  }
+}
+
+hipError_t ipc_push(const PushArgs& a, int world, int64_t bytes, const int32_t* tbase, int k,
+                    int32_t seq, uint32_t* done, hipStream_t s) {
+  // at most 160 blocks: each block ends with one increment of the shared `done` counter, and
+  // same-address atomics serialise (~13 ns each); 160 x 256 lanes x 16 B keeps the links busy
+  const int64_t units = (bytes / 16 + (bytes % 16) / 4) * world;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(160, (units + kBlock - 1) / kBlock));
+  k_ipc_push<<<blocks, kBlock, 0, s>>>(a, world, bytes, tbase, k, seq, done);
+  return hipGetLastError();
+}
+
+hipError_t ipc_wait(const int32_t* flags, int world, int self, const int32_t* tbase, int k,
+                    int32_t seq, int32_t* err, hipStream_t s) {
+  k_ipc_wait<<<1, 64, 0, s>>>(flags, world, self, tbase, k, seq, err);
+  return hipGetLastError();
+}
+
+hipError_t max_vals(const int32_t* vals, int world, int32_t* out, hipStream_t s) {
+  k_max_vals<<<1, 64, 0, s>>>(vals, world, out);
+  return hipGetLastError();
 }
 
 #define BPRMF_DISPATCH4D(geom, BODY)                               \

@@ -140,6 +140,18 @@ hipError_t add_rows(const Geom& g, Table W, const int32_t* rows, const float* gr
 hipError_t apply_rows(const Geom& g, Table W, const int32_t* rows, int64_t n, const Hyper& hp,
                       int32_t t, hipStream_t s);
 // --- sharded runner (dist.hip; layouts in dist.hip's header comment) ---
+struct PushArgs {  // one IPC exchange: per peer, source block, destination, flag to raise
+  const void* src[kMaxWorld];
+  void* dst[kMaxWorld];
+  int32_t* flag[kMaxWorld];
+};
+hipError_t ipc_push(const PushArgs& a, int world, int64_t bytes, const int32_t* tbase, int k,
+                    int32_t seq, uint32_t* done, hipStream_t s);
+hipError_t ipc_wait(const int32_t* flags, int world, int self, const int32_t* tbase, int k,
+                    int32_t seq, int32_t* err, hipStream_t s);
+hipError_t ipc_recv(const PushArgs& a, int world, int self, int64_t bytes, const int32_t* flags,
+                    const int32_t* tbase, int k, int32_t seq, int32_t* err, hipStream_t s);
+hipError_t max_vals(const int32_t* vals, int world, int32_t* out, hipStream_t s);
 hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s);
 hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
                          hipStream_t s);

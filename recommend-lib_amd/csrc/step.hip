@@ -178,14 +178,15 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
   }
 }
 
-template <int G4, int S, bool SH>
-__global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp,
-                                                      int ld, const int32_t* __restrict__ tbase,
-                                                      int step, const float* __restrict__ contrib,
-                                                      const float* __restrict__ ugrad,
-                                                      int long_blocks, int item_blocks,
-                                                      float* __restrict__ grads) {
-  constexpr int NG = kBlock / G4;
+// KB threads per block: 1024 (512 for rows over 1 KB) so a hot item's workgroup has 16-32 lane
+// groups fetching its references in parallel
+template <int G4, int S, bool SH, int KB>
+__global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp, int ld,
+                                                  const int32_t* __restrict__ tbase, int step,
+                                                  const float* __restrict__ contrib,
+                                                  const float* __restrict__ ugrad, int long_blocks,
+                                                  int item_blocks, float* __restrict__ grads) {
+  constexpr int NG = KB / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
   const int32_t t = *tbase + step + 1;
@@ -237,20 +238,24 @@ __global__ __launch_bounds__(kBlock) void k_item_step(BatchView bv, Table P, Tab
           if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
       }
     }
+    // fixed-shape tree over the groups' partial sums (deterministic order)
 #pragma unroll
     for (int k = 0; k < S; ++k) part[grp][sub + G4 * k] = g[k];
     __syncthreads();
+#pragma unroll
+    for (int half = NG / 2; half >= 1; half >>= 1) {
+      if (grp < half) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const float4 a = part[grp][sub + G4 * k], o = part[grp + half][sub + G4 * k];
+          part[grp][sub + G4 * k] = make_float4(a.x + o.x, a.y + o.y, a.z + o.z, a.w + o.w);
+        }
+      }
+      __syncthreads();
+    }
     if (grp == 0) {
 #pragma unroll
-      for (int k = 0; k < S; ++k) {
-        float4 acc = part[0][sub + G4 * k];
-#pragma unroll 4
-        for (int q = 1; q < NG; ++q) {
-          const float4 o = part[q][sub + G4 * k];
-          acc = make_float4(acc.x + o.x, acc.y + o.y, acc.z + o.z, acc.w + o.w);
-        }
-        g[k] = acc;
-      }
+      for (int k = 0; k < S; ++k) g[k] = part[0][sub + G4 * k];
       finish_item<G4, S, SH>(Q, item, r0.w, g, hp, ld, t, sub, grads);
     }
     return;
@@ -335,15 +340,16 @@ hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
                      float* grads, hipStream_t s) {
   const int long_blocks = item_long_blocks(B);
   BPRMF_DISPATCH4(g, ({
-    constexpr int NG = kBlock / G4_;
+    constexpr int KB = S_ == 1 ? 1024 : 512;
+    constexpr int NG = KB / G4_;
     const int item_blocks = (int)((2LL * B + NG - 1) / NG);
     const int user_blocks = (int)((B / 2 + NG - 1) / NG);  // multi-triplet users <= B/2
     const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks);
     if (grads)
-      k_item_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
+      k_item_step<G4_, S_, true, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
                                                            ugrad, long_blocks, item_blocks, grads);
     else
-      k_item_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
+      k_item_step<G4_, S_, false, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
                                                             contrib, ugrad, long_blocks,
                                                             item_blocks, nullptr);
   }));

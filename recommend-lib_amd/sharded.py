@@ -66,6 +66,15 @@ class TorchComm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 
+    def all_gather_bytes(self, data, device):
+        """every rank's bytes (equal lengths), in rank order."""
+        import torch
+        dev = torch.device("cpu") if self.backend == "gloo" else device
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [bytes(x.cpu().numpy().tobytes()) for x in out]
+
     def broadcast_bytes(self, data, device):
         """rank 0's bytes to every rank (the RCCL unique id of the library's communicator)."""
         import torch
@@ -197,6 +206,13 @@ class HipShard:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         _lib.check(self.L.bprmf_dist_init_rccl(self.h, ctypes.addressof(buf)))
 
+    def runner_ipc(self, all_gather_bytes):
+        blob = (ctypes.c_uint8 * _lib.IPC_BLOB_BYTES)()
+        _lib.check(self.L.bprmf_dist_ipc_export(self.h, ctypes.addressof(blob)))
+        blobs = b"".join(all_gather_bytes(bytes(blob)))
+        allb = (ctypes.c_uint8 * len(blobs)).from_buffer_copy(blobs)
+        _lib.check(self.L.bprmf_dist_init_ipc(self.h, ctypes.addressof(allb)))
+
     def runner_loopback(self, key):
         _lib.check(self.L.bprmf_dist_init_loopback(self.h, int(key)))
 
@@ -248,7 +264,8 @@ class ShardedBPRMF:
         self.chunk_steps = int(chunk_steps)
         self.steps_per_epoch = None
         self._plan = None  # (epoch, first_step, n, send_counts, recv_counts)
-        self.runner = None  # attach_runner(): "rccl" | "loopback"
+        self.runner = None  # attach_runner(): "ipc" | "rccl" | "loopback"
+        self.transport_error = None
 
     # -- data -----------------------------------------------------------------------------------
     def set_train(self, positives):
@@ -295,8 +312,10 @@ class ShardedBPRMF:
 
     # -- the library-driven runner: whole chunks of steps, exchanges issued from C++ -------------
     def attach_runner(self, transport="rccl", key=0):
-        """transport "rccl": the library's own RCCL communicator (rank 0 makes the unique id, the
-        process group broadcasts it); "loopback": in-process shards sharing group `key` (tests)."""
+        """transport "ipc": kernels write each peer's block straight into its buffers (hipIpc
+        mappings exchanged over the process group; one process per GPU, one node); "rccl": the
+        library's own RCCL communicator (rank 0 makes the unique id, the process group broadcasts
+        it); "loopback": in-process shards sharing group `key` (tests)."""
         if transport == "rccl":
             uid = bytes(128)
             if self.rank == 0:
@@ -305,6 +324,19 @@ class ShardedBPRMF:
                 uid = bytes(buf)
             uid = self.comm.broadcast_bytes(uid, self.device)
             self.b.runner_rccl(uid)
+        elif transport == "ipc":
+            self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
+        elif transport == "auto":  # ipc where every rank can map its peers, else rccl
+            ok = 1
+            try:
+                self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
+            except Exception as e:  # noqa: BLE001 (reported, then the fallback is agreed on)
+                self.transport_error = str(e)
+                ok = 0
+            if -self.comm.allreduce_max(-ok, self.device) == 1:
+                transport = "ipc"
+            else:
+                return self.attach_runner("rccl")
         elif transport == "loopback":
             self.b.runner_loopback(key)
         else:

@@ -1,0 +1,125 @@
+"""GPU: the library's IPC transport (kernels writing straight into the peers' buffers, flags for
+completion) between two PROCESSES sharing the box's one GPU (tests/ipc_worker.py, gloo process
+group for the handle exchange).  The sharded result equals the dense oracle on the union batches
+and, bit for bit, the in-process loopback transport."""
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import bpr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_workers(tmp_path, spec, mode, world=2):
+    spec_path = str(tmp_path / f"spec_{mode}.npz")
+    np.savez(spec_path, **spec)
+    port = _free_port()
+    procs, outs = [], []
+    for r in range(world):
+        out = str(tmp_path / f"out_{mode}_{r}.npz")
+        outs.append(out)
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE=str(world), LOCAL_RANK="0", IPC_SPEC=spec_path)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ipc_worker.py"),
+                                       out, mode], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    logs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=300)
+            logs.append(o)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, o in zip(procs, logs):
+        assert p.returncode == 0, o[-3000:]
+    return [dict(np.load(o)) for o in outs]
+
+
+def _loopback(rl, world, spec, mode, key):
+    sh = rl.sharded
+    grp = sh.ThreadGroup(world)
+    out, errs = [None] * world, []
+    U, I, D, B = (int(spec[k]) for k in ("U", "I", "D", "B"))
+
+    def run(r):
+        try:
+            m = sh.ShardedBPRMF(U, I, D, lr=float(spec["lr"]), wd=float(spec["wd"]), batch_size=B,
+                                seed=int(spec["seed"]), device=0, comm=sh.ThreadComm(grp, r))
+            if mode == "replay":
+                m.set_weights(sh.shard_rows(spec["P0"], r, world), sh.shard_rows(spec["Q0"], r, world))
+                m.attach_runner("loopback", key=key)
+                batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]
+                m.train_replay(batches)
+                m.train_replay(batches)
+            else:
+                S = m.set_train(spec["pos"])
+                m.attach_runner("loopback", key=key)
+                m.train_steps(0, 0, S)
+                m.train_steps(1, 0, 5)
+            out[r] = m.get_weights()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    return out
+
+
+def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path):
+    U, I, D, GB, steps = 301, 157, 128, 512, 6
+    g = np.random.default_rng(11)
+    u = g.integers(0, U, (steps, GB)).astype(np.int32)
+    i = g.integers(0, I, (steps, GB)).astype(np.int32)
+    j = g.integers(0, I, (steps, GB)).astype(np.int32)
+    i[:, :40] = 7  # a hot item
+    spec = dict(U=U, I=I, D=D, B=GB, lr=0.05, wd=0.01, seed=3, u=u, i=i, j=j,
+                P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
+                Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
+    res = _run_workers(tmp_path, spec, "replay")
+    sh = rl.sharded
+    P = sh.unshard_rows([r["P"] for r in res], U)
+    Q = sh.unshard_rows([r["Q"] for r in res], I)
+    Pr, Qr = spec["P0"].copy(), spec["Q0"].copy()
+    loss = 0.0
+    for _ in range(2):
+        for k in range(steps):
+            loss += O.bpr_step_dense(Pr, Qr, u[k], i[k], j[k], 0.05, 0.01)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+    assert sum(int(r["triplets"]) for r in res) == 2 * steps * GB
+    got = sum(float(r["loss"]) for r in res)
+    assert abs(got - loss) <= 1e-4 * abs(loss)
+    lb = _loopback(rl, 2, spec, "replay", key=4001)
+    for r in range(2):
+        assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])
+
+
+def test_ipc_sampler_training_equals_loopback(rl, golden, tmp_path):
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    spec = dict(U=int(f["U"]), I=int(f["I"]), D=64, B=1024, lr=0.01, wd=0.001, seed=9, pos=pos)
+    res = _run_workers(tmp_path, spec, "sampler")
+    lb = _loopback(rl, 2, spec, "sampler", key=4002)
+    for r in range(2):
+        assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])

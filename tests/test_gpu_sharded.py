@@ -202,7 +202,8 @@ def test_runner_sampler_matches_python_orchestration_and_is_reproducible(rl, gol
 
 def test_runner_rccl_transport_one_rank(rl):
     """The RCCL transport (library-owned communicator, unique id broadcast by the process group)
-    at world 1 gives the loopback transport's result bit for bit."""
+    at world 1, graph-captured or eager, with or without RCCL carrying the self blocks, gives the
+    loopback transport's result bit for bit."""
     import os
     import torch
     import torch.distributed as dist
@@ -217,15 +218,30 @@ def test_runner_rccl_transport_one_rank(rl):
     own = not dist.is_initialized()
     if own:
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    # rccl: steps replayed from a captured hipGraph; rccl + self exchange: this rank's own blocks
+    # go through RCCL send/recv inside the captured graph; loopback: eager, device copies
+    cases = [("rccl", {}), ("rccl", {"BPRMF_DIST_SELF_EXCHANGE": "1"}), ("loopback", {}),
+             ("rccl", {"BPRMF_NO_GRAPH": "1"})]
     try:
-        for transport in ("rccl", "loopback"):
-            m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=256, device=0)
-            m.set_weights(P0, Q0)
-            m.attach_runner(transport, key=3001)
+        for transport, env in cases:
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            try:
+                m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=256, device=0)
+                m.set_weights(P0, Q0)
+                m.attach_runner(transport, key=3001)
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k)
+                    else:
+                        os.environ[k] = v
             m.train_replay(batches)
+            m.train_replay(batches)  # second call: the cached graph is replayed
             res.append(m.get_weights())
     finally:
         if own:
             dist.destroy_process_group()
-    for x, y in zip(*res):
-        assert np.array_equal(x, y)
+    for r in res[1:]:
+        for x, y in zip(res[0], r):
+            assert np.array_equal(x, y)

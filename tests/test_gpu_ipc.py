@@ -86,7 +86,8 @@ def _loopback(rl, world, spec, mode, key):
     return out
 
 
-def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world):
     U, I, D, GB, steps = 301, 157, 128, 512, 6
     g = np.random.default_rng(11)
     u = g.integers(0, U, (steps, GB)).astype(np.int32)
@@ -96,7 +97,7 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path):
     spec = dict(U=U, I=I, D=D, B=GB, lr=0.05, wd=0.01, seed=3, u=u, i=i, j=j,
                 P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
                 Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
-    res = _run_workers(tmp_path, spec, "replay")
+    res = _run_workers(tmp_path, spec, "replay", world)
     sh = rl.sharded
     P = sh.unshard_rows([r["P"] for r in res], U)
     Q = sh.unshard_rows([r["Q"] for r in res], I)
@@ -110,8 +111,8 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path):
     assert sum(int(r["triplets"]) for r in res) == 2 * steps * GB
     got = sum(float(r["loss"]) for r in res)
     assert abs(got - loss) <= 1e-4 * abs(loss)
-    lb = _loopback(rl, 2, spec, "replay", key=4001)
-    for r in range(2):
+    lb = _loopback(rl, world, spec, "replay", key=4000 + world)
+    for r in range(world):
         assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])
 
 
@@ -120,6 +121,6 @@ def test_ipc_sampler_training_equals_loopback(rl, golden, tmp_path):
     pos = f["positives"].astype(np.int64)
     spec = dict(U=int(f["U"]), I=int(f["I"]), D=64, B=1024, lr=0.01, wd=0.001, seed=9, pos=pos)
     res = _run_workers(tmp_path, spec, "sampler")
-    lb = _loopback(rl, 2, spec, "sampler", key=4002)
+    lb = _loopback(rl, 2, spec, "sampler", key=4010)
     for r in range(2):
         assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])

@@ -133,6 +133,15 @@ int bprmf_score(bprmf_handle* h, const int32_t* u, const int32_t* i, int64_t n, 
 int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const int64_t* j,
                       int64_t n, float* pred_i, float* pred_j);
 
+/* ---- ranking ------------------------------------------------------- */
+/* Per user r: score its candidates items[offsets[r] .. offsets[r+1]) as bprmf_score does and
+ * return the positions (within the list) of the k best, score descending, ties by the later
+ * position first (np.argsort(pred)[::-1][:k], BPRMFRecommender.py:196-207; torch.topk of
+ * util/metrics.py:53-54); -1 / -inf past the list's end.  out_pos, out_score: [n_users, k]. */
+int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offsets,
+                     const int32_t* items, int64_t n_users, int32_t k, int32_t* out_pos,
+                     float* out_score);
+
 /* ---- measurement -------------------------------------------------------------------------- */
 /* Enable (1) / disable (0) and reset per-kernel event timing; read the sums since enabling. */
 int bprmf_profile(bprmf_handle* h, int32_t enable);

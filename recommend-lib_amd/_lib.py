@@ -76,6 +76,7 @@ SIGNATURES = {
     "bprmf_dist_apply_items": [_P, _P, _P, _I64],
     "bprmf_dist_end_step": [_P, ctypes.POINTER(ctypes.c_double)],
     "bprmf_dist_sample_dev": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
+    "bprmf_topk_lists": [_P, _P, _P, _P, _I64, ctypes.c_int32, _P, _P],
     "bprmf_dist_unique_id": [_P],
     "bprmf_dist_init_rccl": [_P, _P],
     "bprmf_dist_init_loopback": [_P, _I64],

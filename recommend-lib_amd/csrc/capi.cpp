@@ -687,6 +687,49 @@ int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const
   return check_err_flag(h);
 }
 
+int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offsets,
+                     const int32_t* items, int64_t n_users, int32_t k, int32_t* out_pos,
+                     float* out_score) {
+  if (!h || n_users < 0 || k <= 0 || (n_users > 0 && (!users || !offsets || !items || !out_pos || !out_score)))
+    return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_UNSUPPORTED, "top-k needs an unsharded handle");
+  if (k > 256) return fail(BPRMF_E_UNSUPPORTED, "k must be <= 256");
+  if (n_users == 0) return 0;
+  if (offsets[0] != 0) return fail(BPRMF_E_INVALID, "offsets[0] must be 0");
+  for (int64_t r = 0; r < n_users; ++r) {
+    if (offsets[r + 1] < offsets[r]) return fail(BPRMF_E_INVALID, "offsets must be non-decreasing");
+    if (users[r] < 0 || users[r] >= h->cfg.user_num) return fail(BPRMF_E_RANGE, "Invalid user code");
+  }
+  const int64_t m = offsets[n_users];
+  for (int64_t x = 0; x < m; ++x)
+    if (items[x] < 0 || items[x] >= h->cfg.item_num) return fail(BPRMF_E_RANGE, "Invalid item code");
+  if (int r = set_dev(h)) return r;
+  // one device block: users | offsets (8-aligned) | items | out_pos | out_score
+  const int64_t w_users = (n_users + 1) & ~1LL, w_offs = 2 * (n_users + 1);
+  const int64_t words = w_users + w_offs + m + 2 * n_users * (int64_t)k;
+  int32_t* buf = nullptr;
+  if (int r = dalloc(&buf, words)) return r;
+  int32_t* d_users = buf;
+  int64_t* d_offs = reinterpret_cast<int64_t*>(buf + w_users);
+  int32_t* d_items = buf + w_users + w_offs;
+  int32_t* d_pos = d_items + m;
+  float* d_score = reinterpret_cast<float*>(d_pos + n_users * (int64_t)k);
+  int rc = 0;
+  hipError_t e = hipMemcpyAsync(d_users, users, 4 * n_users, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_offs, offsets, 8 * (n_users + 1), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess && m) e = hipMemcpyAsync(d_items, items, 4 * m, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess)
+    e = topk_lists(h->geom, d_users, d_offs, d_items, n_users, k, h->P, h->Q, h->hp, h->t, d_pos,
+                   d_score, h->d_err, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_pos, d_pos, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_score, d_score, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "topk_lists: %s", hipGetErrorString(e));
+  hipFree(buf);
+  if (rc) return rc;
+  return check_err_flag(h);
+}
+
 int bprmf_profile(bprmf_handle* h, int32_t enable) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (int r = set_dev(h)) return r;

@@ -130,6 +130,10 @@ hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, T
 hipError_t forward64(const Geom& g, const int64_t* u, const int64_t* i, const int64_t* j,
                      int64_t n, Table P, Table Q, const Hyper& hp, int32_t T, float* oi, float* oj,
                      int32_t* err, hipStream_t s);
+// per-user top-k positions of candidate lists items[offs[r]..offs[r+1]) of users[r] (topk.hip)
+hipError_t topk_lists(const Geom& g, const int32_t* users, const int64_t* offs, const int32_t* items,
+                      int64_t n_users, int k, Table P, Table Q, const Hyper& hp, int32_t T,
+                      int32_t* out_pos, float* out_score, int32_t* err, hipStream_t s);
 // bring every row of a table to step T (before get_weights)
 hipError_t flush(const Geom& g, Table W, const Hyper& hp, int32_t T, hipStream_t s);
 // --- sharded step phases ---

@@ -2,8 +2,9 @@
 
 `metric_eval` / `_bpr_topk` keep the reference batch protocol (util/metrics.py:46-66,88-94):
 each loader batch is one user's [ground truth, negatives...]; the ground truth is item_i[0].
-`evaluate_topk` is the final KPI of BPRMFRecommender.py:196-229 with every candidate scored on
-the GPU in one launch instead of one scalar forward per candidate (the reference's 43 s loop).
+`evaluate_topk` is the final KPI of BPRMFRecommender.py:196-229 with every candidate scored AND
+ranked on the GPU in one launch (bprmf_topk_lists) instead of one scalar forward per candidate
+(the reference's 43 s loop); `metric_eval` ranks all loader batches in one launch the same way.
 The scalar metric functions restate util/metrics.py:99-195 (NumPy-2 safe: no np.asfarray).
 """
 from collections import defaultdict
@@ -23,6 +24,20 @@ def _ndcg(gt_item, pred_items):
 
 def _bpr_topk(model, test_loader, top_k):
     import torch
+    if hasattr(model, "topk_lists"):  # every batch ranked on the device in one launch
+        users, lists = [], []
+        for user, item_i, _ in test_loader:
+            users.append(int(torch.as_tensor(user).reshape(-1)[0]))
+            lists.append(torch.as_tensor(item_i).reshape(-1).cpu().numpy())
+        if not users:
+            return np.mean([]), np.mean([])
+        pos, _ = model.topk_lists(users, lists, top_k)
+        HR, NDCG = [], []
+        for l, p in zip(lists, pos):
+            recommends = l[p[p >= 0]].tolist()
+            HR.append(_hit(int(l[0]), recommends))
+            NDCG.append(_ndcg(int(l[0]), recommends))
+        return np.mean(HR), np.mean(NDCG)
     HR, NDCG = [], []
     for user, item_i, item_j in test_loader:
         prediction_i, _ = model(user, item_i, item_j)
@@ -107,7 +122,8 @@ def evaluate_topk(model, test_data, test_ur, topk=10):
 
     test_data: [[u, i], ...] candidates (load_mat test_data); test_ur: {u: set(gt items)}.
     Candidates are grouped per user exactly as the reference does (a set per user, listed in set
-    order), all scored in one device launch, then ranked with the same np.argsort(...)[::-1][:k].
+    order), then scored and ranked on the device in one launch with np.argsort(...)[::-1][:k]'s
+    order (score descending, ties by the later position).
     Returns dict(precision, recall, map, ndcg, hr, mrr).
     """
     test_u_is = defaultdict(set)
@@ -115,17 +131,11 @@ def evaluate_topk(model, test_data, test_ur, topk=10):
         test_u_is[int(ele[0])].add(int(ele[1]))
     users = list(test_u_is.keys())
     lists = [list(test_u_is[u]) for u in users]
-    flat_u = np.concatenate([np.full(len(l), u, dtype=np.int32) for u, l in zip(users, lists)]) \
-        if users else np.zeros(0, np.int32)
-    flat_i = np.concatenate([np.asarray(l, dtype=np.int32) for l in lists]) if users else np.zeros(0, np.int32)
-    scores = model.score(flat_u, flat_i) if len(flat_u) else np.zeros(0, np.float32)
     preds = {}
-    off = 0
-    for u, l in zip(users, lists):
-        s = scores[off:off + len(l)]
-        off += len(l)
-        rec_idx = np.argsort(s)[::-1][:topk]
-        preds[u] = [1 if e in test_ur[u] else 0 for e in np.array(l)[rec_idx]]
+    if users:
+        pos, _ = model.topk_lists(users, lists, topk)  # scoring + ranking on the device
+        for u, l, p in zip(users, lists, pos):
+            preds[u] = [1 if e in test_ur[u] else 0 for e in np.array(l)[p[p >= 0]]]
     rel = list(preds.values())
     return dict(
         precision=float(np.mean([precision_at_k(r, topk) for r in rel])),

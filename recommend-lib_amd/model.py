@@ -257,6 +257,30 @@ class BPRMF:
         _lib.check(self._L.bprmf_score(self._h, _lib.ptr(u), _lib.ptr(i), len(u), _lib.ptr(out)))
         return out
 
+    def topk_lists(self, users, lists, k):
+        """Per user, the k best of its candidate list (one device launch for all users): positions
+        into the list and scores, score descending, ties by the later position first (what
+        np.argsort(pred)[::-1][:k] ranks, BPRMFRecommender.py:196-207); -1 / -inf past the end.
+        users: [n]; lists: n sequences of item ids (or (offsets[n+1], flat items))."""
+        u = np.ascontiguousarray(np.asarray(users).reshape(-1), dtype=np.int32)
+        if isinstance(lists, tuple) and len(lists) == 2:
+            offs = np.ascontiguousarray(lists[0], dtype=np.int64)
+            flat = np.ascontiguousarray(lists[1], dtype=np.int32)
+        else:
+            lens = np.fromiter((len(x) for x in lists), dtype=np.int64, count=len(lists))
+            offs = np.zeros(len(lists) + 1, dtype=np.int64)
+            np.cumsum(lens, out=offs[1:])
+            flat = (np.concatenate([np.asarray(x, dtype=np.int32).reshape(-1) for x in lists])
+                    if len(lists) else np.zeros(0, np.int32))
+            flat = np.ascontiguousarray(flat, dtype=np.int32)
+        if len(offs) != len(u) + 1:
+            raise ValueError("one candidate list per user")
+        pos = np.empty((len(u), int(k)), dtype=np.int32)
+        sc = np.empty((len(u), int(k)), dtype=np.float32)
+        _lib.check(self._L.bprmf_topk_lists(self._h, _lib.ptr(u), _lib.ptr(offs), _lib.ptr(flat),
+                                            len(u), int(k), _lib.ptr(pos), _lib.ptr(sc)))
+        return pos, sc
+
     def forward(self, user, item_i, item_j=None):
         """BPR.forward (BPRMFRecommender.py:42-50): int64 tensors (0-d or [B]) -> fp32 (pred_i, pred_j).
         CUDA inputs stay on the GPU; CPU inputs are scored on the GPU and returned on CPU."""

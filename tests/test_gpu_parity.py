@@ -370,3 +370,34 @@ def test_ml20m_shape_properties(rl):
     assert s2["loss"] < s1["loss"]
     P, Q = m.get_weights()
     assert np.isfinite(P).all() and np.isfinite(Q).all()
+
+
+# ---- device ranking (bprmf_topk_lists) ----------------------------------
+@pytest.mark.parametrize("d,k", [(32, 10), (128, 10), (64, 256), (256, 1)])
+def test_topk_lists_matches_argsort_of_device_scores(rl, d, k):
+    U, I = 97, 6011
+    g = np.random.default_rng(d + k)
+    m = rl.BPRMF(U, I, d, seed=1)
+    m.set_weights((0.1 * g.standard_normal((U, d))).astype(np.float32),
+                  (0.1 * g.standard_normal((I, d))).astype(np.float32))
+    users = g.integers(0, U, 40)
+    lens = [0, 1, 5, 999, 1000, 2047, 5000] + list(g.integers(1, 1500, 33))
+    lists = [g.integers(0, I, n) for n in lens]
+    lists[3][10:20] = lists[3][5]  # duplicated candidates: equal scores, later position first
+    pos, sc = m.topk_lists(users, lists, k)
+    for r, (u, l) in enumerate(zip(users, lists)):
+        s = m.score(np.full(len(l), u), l) if len(l) else np.zeros(0, np.float32)
+        order = np.lexsort((-np.arange(len(l)), -s.astype(np.float64)))[:k]
+        want = np.full(k, -1)
+        want[:len(order)] = order
+        assert np.array_equal(pos[r], want), (r, len(l))
+        assert np.array_equal(sc[r][:len(order)], s[order])
+        assert np.all(np.isneginf(sc[r][len(order):]))
+
+
+def test_topk_lists_rejects_bad_ids(rl):
+    m = rl.BPRMF(10, 20, 8)
+    with pytest.raises(ValueError):
+        m.topk_lists([3], [[1, 25]], 2)
+    with pytest.raises(ValueError):
+        m.topk_lists([11], [[1, 2]], 2)

@@ -60,15 +60,17 @@ typedef struct {
 } bprmf_stats;
 
 /* live kernel timing (HIP events around every launch of each kind while enabled) */
-/* kinds: sample/build, step kernel 1 (users), step kernel 2 (items), owner-side item update, and
- * whole steps replayed from a captured graph (count = steps, ms = their summed device time) */
+/* kinds: sample/build, step kernel 1 (users), step kernel 2 (items), owner-side item update,
+ * whole steps replayed from a captured graph (count = steps, ms = their summed device time), and
+ * full-catalogue top-k launches */
 enum {
   BPRMF_KPROF_SAMPLE = 0,
   BPRMF_KPROF_FWD_SCATTER = 1,
   BPRMF_KPROF_APPLY = 2,
   BPRMF_KPROF_OWNER = 3,
   BPRMF_KPROF_STEPS = 4,
-  BPRMF_KPROF_KINDS = 5
+  BPRMF_KPROF_TOPK = 5,
+  BPRMF_KPROF_KINDS = 6
 };
 typedef struct {
   int64_t count[8];     /* launches (steps for BPRMF_KPROF_STEPS) recorded per kind */
@@ -141,6 +143,13 @@ int bprmf_forward_dev(bprmf_handle* h, const int64_t* u, const int64_t* i, const
 int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offsets,
                      const int32_t* items, int64_t n_users, int32_t k, int32_t* out_pos,
                      float* out_score);
+
+/* Per user: the k best items of the WHOLE catalogue (the serving form of predict): scores on f32
+ * MFMA (exact f32 products and sums, k-ordered fmaf chain), exclude_train != 0 skips the user's
+ * training positives; score descending, ties by the smaller item; -1 / -inf when fewer remain.
+ * factor_num <= 128, k <= 32.  out_items, out_scores: [n_users, k]. */
+int bprmf_topk_all(bprmf_handle* h, const int32_t* users, int64_t n_users, int32_t k,
+                   int32_t exclude_train, int32_t* out_items, float* out_scores);
 
 /* ---- measurement -------------------------------------------------------------------------- */
 /* Enable (1) / disable (0) and reset per-kernel event timing; read the sums since enabling. */

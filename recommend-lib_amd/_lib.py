@@ -36,7 +36,7 @@ class Stats(ctypes.Structure):
 class KProf(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int64 * 8), ("ms", ctypes.c_double * 8)]
 
-    KINDS = ("sample", "user_step", "item_step", "owner_apply", "step_graph")
+    KINDS = ("sample", "user_step", "item_step", "owner_apply", "step_graph", "topk_all")
 
     def as_dict(self):
         return {k: dict(count=int(self.count[n]), ms=float(self.ms[n])) for n, k in enumerate(self.KINDS)}
@@ -77,6 +77,7 @@ SIGNATURES = {
     "bprmf_dist_end_step": [_P, ctypes.POINTER(ctypes.c_double)],
     "bprmf_dist_sample_dev": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
     "bprmf_topk_lists": [_P, _P, _P, _P, _I64, ctypes.c_int32, _P, _P],
+    "bprmf_topk_all": [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P],
     "bprmf_dist_unique_id": [_P],
     "bprmf_dist_init_rccl": [_P, _P],
     "bprmf_dist_init_loopback": [_P, _I64],

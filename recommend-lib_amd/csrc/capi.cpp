@@ -730,6 +730,40 @@ int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offse
   return check_err_flag(h);
 }
 
+int bprmf_topk_all(bprmf_handle* h, const int32_t* users, int64_t n_users, int32_t k,
+                   int32_t exclude_train, int32_t* out_items, float* out_scores) {
+  if (!h || n_users < 0 || k <= 0 || (n_users > 0 && (!users || !out_items || !out_scores)))
+    return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.world != 1) return fail(BPRMF_E_UNSUPPORTED, "top-k needs an unsharded handle");
+  if (k > 32) return fail(BPRMF_E_UNSUPPORTED, "k must be <= 32");
+  if (h->geom.ld > 128) return fail(BPRMF_E_UNSUPPORTED, "full-catalogue top-k supports factor_num <= 128");
+  if (exclude_train && !h->d_indptr) return fail(BPRMF_E_STATE, "exclude_train needs bprmf_set_train");
+  for (int64_t r = 0; r < n_users; ++r)
+    if (users[r] < 0 || users[r] >= h->cfg.user_num) return fail(BPRMF_E_RANGE, "Invalid user code");
+  if (n_users == 0) return 0;
+  if (int r = set_dev(h)) return r;
+  const int64_t words = ((n_users + 3) & ~3LL) + 2 * n_users * (int64_t)k;
+  int32_t* buf = nullptr;
+  if (int r = dalloc(&buf, words)) return r;
+  int32_t* d_users = buf;
+  int32_t* d_items = buf + ((n_users + 3) & ~3LL);
+  float* d_scores = reinterpret_cast<float*>(d_items + n_users * (int64_t)k);
+  int rc = 0;
+  hipError_t e = hipMemcpyAsync(d_users, users, 4 * n_users, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    ProfScope ps(h, BPRMF_KPROF_TOPK);
+    e = topk_all(h->geom, d_users, n_users, k, h->P, h->Q, h->hp, h->t,
+                 exclude_train ? h->d_indptr : nullptr, exclude_train ? h->d_indices : nullptr,
+                 d_items, d_scores, h->stream);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out_items, d_items, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_scores, d_scores, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "topk_all: %s", hipGetErrorString(e));
+  hipFree(buf);
+  return rc;
+}
+
 int bprmf_profile(bprmf_handle* h, int32_t enable) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (int r = set_dev(h)) return r;

@@ -134,6 +134,11 @@ hipError_t forward64(const Geom& g, const int64_t* u, const int64_t* i, const in
 hipError_t topk_lists(const Geom& g, const int32_t* users, const int64_t* offs, const int32_t* items,
                       int64_t n_users, int k, Table P, Table Q, const Hyper& hp, int32_t T,
                       int32_t* out_pos, float* out_score, int32_t* err, hipStream_t s);
+// per-user top-k items of the whole catalogue (f32 MFMA scores), optionally skipping the user's
+// training positives (indptr/indices: the handle's CSR); ld <= 128, k <= 32 (topk.hip)
+hipError_t topk_all(const Geom& g, const int32_t* users, int64_t n_users, int k, Table P, Table Q,
+                    const Hyper& hp, int32_t T, const int64_t* indptr, const int32_t* indices,
+                    int32_t* out_items, float* out_scores, hipStream_t s);
 // bring every row of a table to step T (before get_weights)
 hipError_t flush(const Geom& g, Table W, const Hyper& hp, int32_t T, hipStream_t s);
 // --- sharded step phases ---

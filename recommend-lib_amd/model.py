@@ -281,6 +281,17 @@ class BPRMF:
                                             len(u), int(k), _lib.ptr(pos), _lib.ptr(sc)))
         return pos, sc
 
+    def topk_all(self, users, k, exclude_train=True):
+        """The k best items of the whole catalogue per user (scores on f32 MFMA), skipping the
+        user's training positives unless exclude_train=False: (items [n, k], scores [n, k]),
+        score descending, ties by the smaller item; -1 / -inf when fewer items remain."""
+        u = np.ascontiguousarray(np.asarray(users).reshape(-1), dtype=np.int32)
+        items = np.empty((len(u), int(k)), dtype=np.int32)
+        sc = np.empty((len(u), int(k)), dtype=np.float32)
+        _lib.check(self._L.bprmf_topk_all(self._h, _lib.ptr(u), len(u), int(k),
+                                          1 if exclude_train else 0, _lib.ptr(items), _lib.ptr(sc)))
+        return items, sc
+
     def forward(self, user, item_i, item_j=None):
         """BPR.forward (BPRMFRecommender.py:42-50): int64 tensors (0-d or [B]) -> fp32 (pred_i, pred_j).
         CUDA inputs stay on the GPU; CPU inputs are scored on the GPU and returned on CPU."""

@@ -401,3 +401,63 @@ def test_topk_lists_rejects_bad_ids(rl):
         m.topk_lists([3], [[1, 25]], 2)
     with pytest.raises(ValueError):
         m.topk_lists([11], [[1, 2]], 2)
+
+
+def _check_topk_all(items, scores, S, k, tol):
+    """items/scores from the device vs exact float64 scores S [n, I] (-inf = excluded)."""
+    for r in range(S.shape[0]):
+        s = S[r]
+        finite = np.isfinite(s)
+        nvalid = int(finite.sum())
+        kk = min(k, nvalid)
+        it, sc = items[r], scores[r]
+        assert np.all(it[kk:] == -1) and np.all(np.isneginf(sc[kk:])), r
+        got = it[:kk]
+        assert np.all(got >= 0) and len(set(got.tolist())) == kk
+        assert np.all(finite[got]), "an excluded item was returned"
+        np.testing.assert_allclose(sc[:kk], s[got], rtol=0, atol=tol)
+        assert np.all(np.diff(sc[:kk]) <= 0)
+        kth = np.sort(s[finite])[::-1][kk - 1] if kk else np.inf
+        assert np.all(s[got] >= kth - tol)  # nothing clearly worse than the true k-th best
+        must = np.flatnonzero(s > kth + tol)  # everything clearly better is there
+        assert set(must.tolist()) <= set(got.tolist())
+
+
+@pytest.mark.parametrize("d,k,exclude", [(8, 10, True), (32, 1, False), (64, 32, True),
+                                         (128, 10, True), (128, 32, False)])
+def test_topk_all_matches_float64_ranking(rl, d, k, exclude):
+    U, I = 150, 5003
+    g = np.random.default_rng(7 * d + k)
+    m = rl.BPRMF(U, I, d, seed=3)
+    P = (0.2 * g.standard_normal((U, d))).astype(np.float32)
+    Q = (0.2 * g.standard_normal((I, d))).astype(np.float32)
+    m.set_weights(P, Q)
+    pos = np.stack([g.integers(0, U, 4000), g.integers(0, I, 4000)], 1)
+    pos[:200, 0] = 5  # a heavy user
+    m.set_train(pos)
+    users = np.concatenate([np.arange(U), [5, 5, 0]])
+    items, scores = m.topk_all(users, k, exclude_train=exclude)
+    S = P[users].astype(np.float64) @ Q.T.astype(np.float64)
+    if exclude:
+        for r, u in enumerate(users):
+            S[r, pos[pos[:, 0] == u, 1]] = -np.inf
+    tol = 2e-6 * (np.abs(P[users]).astype(np.float64) @ np.abs(Q.T).astype(np.float64)).max()
+    _check_topk_all(items, scores, S, k, tol)
+
+
+def test_topk_all_after_training_uses_lazy_decay(rl, golden):
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    U, I = int(f["U"]), int(f["I"])
+    m = rl.BPRMF(U, I, 32, batch_size=4096, seed=5)
+    m.set_train(pos)
+    m.train_epoch()
+    m.train_steps(1, 0, 7)  # stamps now differ row to row
+    P, Q = m.get_weights()
+    users = np.arange(U)
+    items, scores = m.topk_all(users, 10)
+    S = P.astype(np.float64) @ Q.T.astype(np.float64)
+    for u in range(U):
+        S[u, pos[pos[:, 0] == u, 1]] = -np.inf
+    tol = 4e-6 * (np.abs(P).astype(np.float64) @ np.abs(Q.T).astype(np.float64)).max()
+    _check_topk_all(items, scores, S, 10, tol)

@@ -22,6 +22,14 @@ sys.path.insert(0, ROOT)
 MFMA_F32_PEAK_TF = 157.3
 
 
+def blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max(int(x.get("num_threads", 1)) for x in threadpool_info()) or 1
+    except Exception:  # noqa: BLE001
+        return int(os.environ.get("OMP_NUM_THREADS", "1"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=138493)
@@ -72,7 +80,7 @@ def main():
                         "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TF, 4),
                         "flops_per_launch": flops},
            "cpu_baseline": {"value": round(n / cpu_s, 1), "unit": "users/s",
-                            "cores": os.cpu_count(), "kind": "numpy",
+                            "cores": blas_threads(), "kind": "numpy",
                             "sample": f"{n} users: f32 GEMM vs all {I} items + argpartition"},
            "topk_agreement_vs_cpu": round(agree, 4)}
     print(json.dumps(out), flush=True)

@@ -147,7 +147,8 @@ int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offse
 /* Per user: the k best items of the WHOLE catalogue (the serving form of predict): scores on f32
  * MFMA (exact f32 products and sums, k-ordered fmaf chain), exclude_train != 0 skips the user's
  * training positives; score descending, ties by the smaller item; -1 / -inf when fewer remain.
- * factor_num <= 128, k <= 32.  out_items, out_scores: [n_users, k]. */
+ * factor_num <= 128, k <= 32.  out_items, out_scores: [n_users, k].  Like bprmf_get_weights,
+ * it first brings both tables to the current step (applies the pending weight decay). */
 int bprmf_topk_all(bprmf_handle* h, const int32_t* users, int64_t n_users, int32_t k,
                    int32_t exclude_train, int32_t* out_items, float* out_scores);
 

@@ -100,102 +100,100 @@ __global__ __launch_bounds__(kTopkThreads) void k_topk_lists(
 }
 
 // ---- full-catalogue top-K: scores of every (user, item) on f32 MFMA, selection on the fly ----
+// The tables are flushed to the current step first (bprmf_topk_all), so rows are read as stored.
 // Workgroup = 4 waves x 16 users; all waves sweep the item catalogue in tiles of 32 items staged
-// in LDS (double-buffered, the next tile's global loads in flight during the current tile's
-// MFMAs).  Per wave and tile: 16 x 32 scores = two v_mfma_f32_16x16x4_f32 accumulators over
-// ld/4 k-steps.  Operand map (16x16x4 f32: A[l&15][k=l>>4], B[k=l>>4][l&15]): lane group
-// g = l>>4 holds the float4 at k = 16t + 4g of its row; element e of step t is one MFMA, so k
-// runs in the order (t, e, g) and the result is that f32 fmaf chain (exact f32, no reduced
-// precision).  Selection: every lane compares its 8 scores with its rows' current K-th best
-// (registers); candidates (rare after the first tiles) are inserted one lane at a time into the
-// row's K-entry list in LDS.  Ties: the earlier (smaller) item wins, the sweep is in item order.
+// in LDS (the next tile's global loads in flight in registers during the current tile's MFMAs).
+// Per wave and tile: 16 x 32 scores = two v_mfma_f32_16x16x4_f32 accumulators over ld/4
+// k-steps (two independent chains cover the 40-cycle dependent latency).  Operand map (16x16x4
+// f32: A[l&15][k=l>>4], B[k=l>>4][l&15]): lane group g = l>>4 holds the float4 at k = 16t + 4g
+// of its row; element e of step t is one MFMA, so k runs in the order (t, e, g) and each score
+// is that f32 fmaf chain (exact f32, no reduced precision).
+// Selection: each lane compares its 8 scores with its rows' current k-th best (registers) and
+// queues the few that beat it in its row's LDS queue; then the 16 row-owner lanes insert their
+// queues into their rows' k-entry lists in parallel.  Ties: the earlier (smaller) item wins, the
+// sweep is in item order.
 constexpr int kAllUsersPerWave = 16;
 constexpr int kAllWaves = 4;
 constexpr int kAllTile = 32;
 constexpr int kAllMaxK = 32;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int LDT>  // LDT = ceil(ld / 16) k-steps of 16 (1..8: ld <= 128; LDS 50 KB at 8)
+template <int LDT>  // LDT = ceil(ld / 16) k-steps of 16 (1..8: ld <= 128)
 __global__ __launch_bounds__(256) void k_topk_all(
-    const int32_t* __restrict__ users, int64_t n_users, int k, Table P, Table Q, Hyper hp, int ld,
-    int32_t T, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const int32_t* __restrict__ users, int64_t n_users, int k, const float* __restrict__ PW,
+    int64_t p_rows, const float* __restrict__ QW, int64_t q_rows, int ld,
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     int32_t* __restrict__ out_items, float* __restrict__ out_scores) {
   constexpr int LDP = 16 * LDT + 4;  // LDS row stride (floats): conflict-free float4 reads
-  __shared__ float4 s_tile[2][kAllTile][LDP / 4];
-  __shared__ float s_ls[kAllWaves][kAllUsersPerWave][kAllMaxK];
-  __shared__ int32_t s_li[kAllWaves][kAllUsersPerWave][kAllMaxK];
-  __shared__ int32_t s_cnt[kAllWaves][kAllUsersPerWave];
-  __shared__ int32_t s_worst[kAllWaves][kAllUsersPerWave];
-  __shared__ float s_tau[kAllWaves][kAllUsersPerWave];
-  __shared__ uint32_t s_mask[kAllWaves][kAllUsersPerWave];
+  constexpr int UW = kAllUsersPerWave;
+  __shared__ float4 s_tile[kAllTile][LDP / 4];
+  __shared__ float s_ls[kAllWaves][UW][kAllMaxK];
+  __shared__ int32_t s_li[kAllWaves][UW][kAllMaxK];
+  __shared__ float s_qs[kAllWaves][UW][kAllTile];  // this tile's candidates per row
+  __shared__ int32_t s_qi[kAllWaves][UW][kAllTile];
+  __shared__ int32_t s_qn[kAllWaves][UW];
+  __shared__ float s_tau[kAllWaves][UW];
+  __shared__ uint32_t s_mask[kAllWaves][UW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = lane & 15, g = lane >> 4;
-  const int64_t ub = (int64_t)blockIdx.x * (kAllWaves * kAllUsersPerWave) + w * kAllUsersPerWave;
-  // A operand: this lane's row (user ub + row), float4 at k = 16t + 4g, with its pending decay
+  const int64_t ub = (int64_t)blockIdx.x * (kAllWaves * UW) + w * UW;
+  // A operand: user row ub + row, float4 at k = 16t + 4g
   float4 a4[LDT];
   {
     const int64_t r = ub + row;
-    const bool ok = r < n_users && (uint64_t)users[r] < (uint64_t)P.rows;
+    const bool ok = r < n_users && (uint64_t)users[r] < (uint64_t)p_rows;
     const int64_t u = ok ? users[r] : 0;
-    const float fu = ok ? decay_pow(hp.log2a, T - P.stamp[u]) : 0.f;
 #pragma unroll
     for (int t = 0; t < LDT; ++t) {
       const int kk = 16 * t + 4 * g;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok && kk < ld) v = *reinterpret_cast<const float4*>(P.W + u * ld + kk);
-      a4[t] = make_float4(v.x * fu, v.y * fu, v.z * fu, v.w * fu);
+      a4[t] = (ok && kk < ld) ? *reinterpret_cast<const float4*>(PW + u * ld + kk)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  // per-row selection state (lanes 0..15 own rows) and the exclusion cursor
+  // row-owner lanes (0..15): list state in registers + LDS, exclusion cursor
+  int cnt = 0, worst = 0;
   int64_t pnext = 0, pend = 0;
   int32_t pval = INT32_MAX;
-  if (lane < kAllUsersPerWave) {
-    s_cnt[w][lane] = 0;
+  if (lane < UW) {
+    s_qn[w][lane] = 0;
     s_tau[w][lane] = -INFINITY;
-    s_worst[w][lane] = 0;
     const int64_t r = ub + lane;
-    if (indptr && r < n_users && (uint64_t)users[r] < (uint64_t)P.rows) {
+    if (indptr && r < n_users && (uint64_t)users[r] < (uint64_t)p_rows) {
       pnext = indptr[users[r]];
       pend = indptr[users[r] + 1];
       pval = pnext < pend ? indices[pnext] : INT32_MAX;
     }
   }
-  float tau[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  // tile loader: 32 items x ld floats, as float4s, each scaled by its item's pending decay
+  float tau[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // rows 4g + r
+  // tile loader: 32 items x ld floats as float4s
   constexpr int PER = (kAllTile * 4 * LDT + 255) / 256;  // float4s per thread
-  const int q4 = ld / 4;  // float4s per row
+  const int q4 = ld / 4;
   float4 nxt[PER];
   auto load_tile = [&](int64_t i0) {
 #pragma unroll
     for (int m = 0; m < PER; ++m) {
       const int x = threadIdx.x + 256 * m, it = x / (4 * LDT), c = x % (4 * LDT);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int64_t item = i0 + it;
-      if (it < kAllTile && c < q4 && item < Q.rows) {
-        v = *reinterpret_cast<const float4*>(Q.W + item * ld + 4 * c);
-        const float fi = decay_pow(hp.log2a, T - Q.stamp[item]);
-        v = make_float4(v.x * fi, v.y * fi, v.z * fi, v.w * fi);
-      }
-      nxt[m] = v;
+      nxt[m] = (it < kAllTile && c < q4 && item < q_rows)
+                   ? *reinterpret_cast<const float4*>(QW + item * ld + 4 * c)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store_tile = [&](int b) {
+  auto store_tile = [&]() {
 #pragma unroll
     for (int m = 0; m < PER; ++m) {
       const int x = threadIdx.x + 256 * m, it = x / (4 * LDT), c = x % (4 * LDT);
-      if (it < kAllTile) s_tile[b][it][c] = nxt[m];
+      if (it < kAllTile) s_tile[it][c] = nxt[m];
     }
   };
-  const int64_t ntiles = (Q.rows + kAllTile - 1) / kAllTile;
+  const int64_t ntiles = (q_rows + kAllTile - 1) / kAllTile;
   load_tile(0);
-  store_tile(0);
+  store_tile();
   __syncthreads();
   for (int64_t tile = 0; tile < ntiles; ++tile) {
-    const int b = (int)(tile & 1);
     const int64_t i0 = tile * kAllTile;
     if (tile + 1 < ntiles) load_tile(i0 + kAllTile);
-    // exclusion mask of this tile for the wave's rows
-    if (lane < kAllUsersPerWave) {
+    if (lane < UW) {  // exclusion mask of this tile for the owner's row
       uint32_t msk = 0;
       while (pval < i0 + kAllTile) {
         if (pval >= i0) msk |= 1u << (pval - i0);
@@ -207,8 +205,8 @@ __global__ __launch_bounds__(256) void k_topk_all(
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < LDT; ++t) {
-      const float4 b0 = s_tile[b][row][4 * t + g];
-      const float4 b1 = s_tile[b][16 + row][4 * t + g];
+      const float4 b0 = s_tile[row][4 * t + g];
+      const float4 b1 = s_tile[16 + row][4 * t + g];
       acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t].x, b0.x, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t].x, b1.x, acc1, 0, 0, 0);
       acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t].y, b0.y, acc0, 0, 0, 0);
@@ -218,64 +216,66 @@ __global__ __launch_bounds__(256) void k_topk_all(
       acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t].w, b0.w, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[t].w, b1.w, acc1, 0, 0, 0);
     }
-    __builtin_amdgcn_wave_barrier();
-    // lane holds C[row 4g + r][col]: col = lane & 15 (acc0) and 16 + (lane & 15) (acc1)
-    float sc[8];
+    __syncthreads();  // every wave is done reading s_tile: refill it
+    if (tile + 1 < ntiles) store_tile();
+    // lane holds C[row 4g + r][item (lane & 15)] (acc0) and [item 16 + (lane & 15)] (acc1)
     bool cand = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t msk = s_mask[w][4 * g + r];
-      const int c0 = row, c1 = 16 + row;
-      const bool v0 = i0 + c0 < Q.rows && !((msk >> c0) & 1u);
-      const bool v1 = i0 + c1 < Q.rows && !((msk >> c1) & 1u);
-      sc[r] = v0 ? acc0[r] : -INFINITY;
-      sc[4 + r] = v1 ? acc1[r] : -INFINITY;
-      cand |= sc[r] > tau[r] || sc[4 + r] > tau[r];
-    }
-    uint64_t pending = __ballot(cand);
-    if (pending) {
-      while (pending) {  // one lane at a time inserts its candidates into its rows' lists
-        const int src = __builtin_ctzll(pending);
-        pending &= pending - 1;
-        if (lane == src) {
+      const int ur = 4 * g + r;
+      const uint32_t msk = s_mask[w][ur];
 #pragma unroll
-          for (int x = 0; x < 8; ++x) {
-            const int ur = 4 * g + (x & 3);
-            const float v = sc[x];
-            if (!(v > s_tau[w][ur])) continue;
-            const int32_t item = (int32_t)(i0 + (x < 4 ? row : 16 + row));
-            int c = s_cnt[w][ur];
-            int slot;
-            if (c < k) {
-              slot = c;
-              s_cnt[w][ur] = ++c;
-            } else {
-              slot = s_worst[w][ur];
+      for (int c = 0; c < 2; ++c) {
+        const int col = 16 * c + row;
+        const float x = (i0 + col < q_rows && !((msk >> col) & 1u)) ? (c ? acc1[r] : acc0[r])
+                                                                      : -INFINITY;
+        if (x > tau[r]) {
+          const int q = atomicAdd(&s_qn[w][ur], 1);
+          s_qs[w][ur][q] = x;
+          s_qi[w][ur][q] = (int32_t)(i0 + col);
+          cand = true;
+        }
+      }
+    }
+    if (__ballot(cand)) {
+      __builtin_amdgcn_wave_barrier();
+      if (lane < UW) {  // the owner inserts its row's queue (rows in parallel)
+        const int nq = s_qn[w][lane];
+        float tl = s_tau[w][lane];
+        for (int q = 0; q < nq; ++q) {
+          const float v = s_qs[w][lane][q];
+          if (!(v > tl)) continue;
+          const int32_t item = s_qi[w][lane][q];
+          int slot;
+          if (cnt < k) {
+            slot = cnt++;
+          } else {
+            slot = worst;
+          }
+          s_ls[w][lane][slot] = v;
+          s_li[w][lane][slot] = item;
+          if (cnt == k) {  // full: find the worst entry (lowest score, then largest item)
+            int wi = 0;
+            for (int y = 1; y < k; ++y) {
+              const float a = s_ls[w][lane][y], bb = s_ls[w][lane][wi];
+              if (a < bb || (a == bb && s_li[w][lane][y] > s_li[w][lane][wi])) wi = y;
             }
-            s_ls[w][ur][slot] = v;
-            s_li[w][ur][slot] = item;
-            if (c == k) {  // list full: the worst entry (lowest score, then largest item)
-              int wi = 0;
-              for (int y = 1; y < k; ++y) {
-                const float a = s_ls[w][ur][y], bb = s_ls[w][ur][wi];
-                if (a < bb || (a == bb && s_li[w][ur][y] > s_li[w][ur][wi])) wi = y;
-              }
-              s_worst[w][ur] = wi;
-              s_tau[w][ur] = s_ls[w][ur][wi];
-            }
+            worst = wi;
+            tl = s_ls[w][lane][wi];
           }
         }
-        __builtin_amdgcn_wave_barrier();
+        s_qn[w][lane] = 0;
+        s_tau[w][lane] = tl;
       }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int r = 0; r < 4; ++r) tau[r] = s_tau[w][4 * g + r];
     }
-    if (tile + 1 < ntiles) store_tile(b ^ 1);
-    __syncthreads();
+    __syncthreads();  // the refilled tile is complete
   }
-  // results: lanes 0..15 sort their row's list (score desc, item asc) and write it
-  if (lane < kAllUsersPerWave && ub + lane < n_users) {
-    const int c = s_cnt[w][lane];
+  // results: the owner lanes sort their row's list (score desc, item asc) and write it
+  if (lane < UW && ub + lane < n_users) {
+    const int c = cnt;
     float* ls = s_ls[w][lane];
     int32_t* li = s_li[w][lane];
     for (int x = 1; x < c; ++x) {
@@ -303,12 +303,15 @@ hipError_t topk_all(const Geom& g, const int32_t* users, int64_t n_users, int k,
                     int32_t* out_items, float* out_scores, hipStream_t s) {
   if (n_users <= 0) return hipSuccess;
   if (k <= 0 || k > kAllMaxK || g.ld > 128) return hipErrorInvalidValue;
+  // rows as stored: bring both tables to step T first (the lazy decay made explicit)
+  if (hipError_t e = flush(g, P, hp, T, s)) return e;
+  if (hipError_t e = flush(g, Q, hp, T, s)) return e;
   const unsigned blocks = (unsigned)((n_users + kAllWaves * kAllUsersPerWave - 1) / (kAllWaves * kAllUsersPerWave));
   const int ldt = (g.ld + 15) / 16;
 #define BPRMF_TOPK_ALL(L)                                                                    \
   case L:                                                                                  \
-    k_topk_all<L><<<blocks, 256, 0, s>>>(users, n_users, k, P, Q, hp, g.ld, T, indptr, indices, \
-                                         out_items, out_scores);                           \
+    k_topk_all<L><<<blocks, 256, 0, s>>>(users, n_users, k, P.W, P.rows, Q.W, Q.rows, g.ld, \
+                                         indptr, indices, out_items, out_scores);          \
     break;
   switch (ldt) {
     BPRMF_TOPK_ALL(1)

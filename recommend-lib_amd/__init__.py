@@ -1,5 +1,6 @@
 """recommend-lib_amd — MI355X-native BPR-MF training path (drop-in for the reference's
-BPRMFRecommender / util.data_loader.BPRData / util.metrics BPR parts).
+BPRMFRecommender / util.data_loader.BPRData / util.metrics BPR parts), plus the NCF path of
+SURVEY.md §8f (NCFRecommender / NCFData).
 
 The directory name is not a Python identifier; import it with
     importlib.import_module("recommend-lib_amd")
@@ -15,7 +16,10 @@ from .model import BPRMF
 from . import metrics
 from . import sharded
 from .sharded import ShardedBPRMF
+from . import ncf
+from .ncf import NCF, NCFData
 
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 
-__all__ = ["BPRMF", "BPR", "BPRData", "BprmfError", "metrics", "build", "LIB_PATH"]
+__all__ = ["BPRMF", "BPR", "BPRData", "NCF", "NCFData", "ShardedBPRMF", "BprmfError", "metrics",
+           "build", "LIB_PATH"]

@@ -1,4 +1,4 @@
-"""ctypes binding of libbprmf_amd.so (include/bprmf.h).
+"""ctypes binding of libbprmf_amd.so (include/bprmf.h, include/ncf.h).
 
 The HIP library is the only compute path: if it is missing or no GPU is visible, handle creation
 raises — there is no CPU fallback in the product.
@@ -23,6 +23,16 @@ class Config(ctypes.Structure):
                 ("num_ng", ctypes.c_int32), ("init_std", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("device", ctypes.c_int32), ("rank", ctypes.c_int32),
                 ("world", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+
+
+class NcfConfig(ctypes.Structure):  # ncf_config, include/ncf.h
+    _fields_ = [("user_num", ctypes.c_int64), ("item_num", ctypes.c_int64),
+                ("factor_num", ctypes.c_int32), ("num_layers", ctypes.c_int32),
+                ("model", ctypes.c_int32), ("batch_size", ctypes.c_int32),
+                ("num_ng", ctypes.c_int32), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("init_std", ctypes.c_float),
+                ("seed", ctypes.c_uint64), ("device", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 4)]
 
 
 class Stats(ctypes.Structure):
@@ -88,6 +98,22 @@ SIGNATURES = {
     "bprmf_row_stride": [_P, ctypes.POINTER(ctypes.c_int32)],
     "bprmf_profile": [_P, ctypes.c_int32],
     "bprmf_profile_read": [_P, ctypes.POINTER(KProf)],
+    # include/ncf.h
+    "ncf_create": [ctypes.POINTER(NcfConfig), ctypes.POINTER(ctypes.c_void_p)],
+    "ncf_destroy": [_P],
+    "ncf_param_count": [_P, ctypes.POINTER(ctypes.c_int32)],
+    "ncf_param_shape": [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
+    "ncf_set_param": [_P, ctypes.c_int32, _P],
+    "ncf_get_param": [_P, ctypes.c_int32, _P],
+    "ncf_set_train": [_P, _P, _P, _I64],
+    "ncf_epoch_size": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
+    "ncf_train_samples": [_P, _P, _P, _P, _I64, _P],
+    "ncf_train_steps": [_P, ctypes.c_uint32, _I64, _I64, _P],
+    "ncf_train_epoch": [_P, ctypes.c_uint32, _P],
+    "ncf_sample": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
+    "ncf_predict": [_P, _P, _P, _I64, _P],
+    "ncf_profile": [_P, ctypes.c_int32],
+    "ncf_profile_read": [_P, ctypes.POINTER(KProf)],
 }
 
 _lib = None

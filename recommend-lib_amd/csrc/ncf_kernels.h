@@ -1,0 +1,59 @@
+// ncf_kernels.h — host-side view of the NCF kernels (ncf.hip).  Internal to libbprmf_amd.so; the
+// public ABI is include/ncf.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace bprmf {
+namespace ncf {
+
+constexpr int kMaxLayers = 4;
+constexpr int kSamples = 16;         // samples per fwd/bwd workgroup (the MFMA M dimension)
+constexpr int kLossSlotsNcf = 256;   // per-workgroup loss partial slots (summed on the host)
+enum { kNeuMF = 0, kGMF = 1, kMLP = 2 };
+
+struct Dims {
+  int d, E, L, model, pred;            // factor_num, tower input width per side, layers, model
+  int nin[kMaxLayers], nout[kMaxLayers];
+  int64_t U, I;
+  // the flat (tower + predict) parameter block, in the reference's state_dict order
+  int flat_n, off_W[kMaxLayers], off_b[kMaxLayers], off_wp, off_bp;
+};
+
+struct Params {
+  float *Pg, *Qg, *Pm, *Qm;            // embed_{user,item}_{GMF,MLP}.weight
+  float *W[kMaxLayers], *b[kMaxLayers];  // MLP_layers.{3l+1}.weight [nout x nin] / bias
+  float *WT[kMaxLayers];               // W^T copies [nin x nout] for the backward
+  float *wp, *bp;                      // predict_layer.weight [pred] / bias [1]
+};
+
+struct Grads {  // dense gradient rows of the embedding tables + the step each row was touched
+  float *Pg, *Qg, *Pm, *Qm;
+  int32_t *touch_u, *touch_i;
+};
+
+struct AdamArgs {
+  float one_minus_b1, b2, one_minus_b2, eps, step_size, bc2_sqrt;
+};
+
+size_t fwdbwd_lds_bytes(const Dims& D);
+hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const int32_t* u,
+                  const int32_t* i, const float* y, int n, int32_t t, float* partial,
+                  double* loss, int32_t* err, hipStream_t s);
+hipError_t forward(const Dims& D, const Params& P, const int32_t* u, const int32_t* i, int n,
+                   float* z, int32_t* err, hipStream_t s);
+hipError_t adam_rows(float* W, float* M, float* V, float* Gr, const int32_t* touch, int64_t rows,
+                     int dim, int32_t t, const AdamArgs& a, hipStream_t s);
+hipError_t adam_flat(const Dims& D, const Params& P, float* F, float* M, float* V,
+                     const float* partial, int nparts, int lo, int hi, const AdamArgs& a,
+                     hipStream_t s);
+hipError_t transpose(const Dims& D, const Params& P, hipStream_t s);
+hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* u,
+                  int32_t* i, float* y, int32_t* err, hipStream_t s);
+hipError_t init(float* W, int64_t n, int kind, float param, uint32_t k0, uint32_t k1, uint32_t tag,
+                hipStream_t s);
+
+}  // namespace ncf
+}  // namespace bprmf

@@ -10,10 +10,12 @@ from conftest import ROOT
 
 
 def _declared():
-    with open(os.path.join(ROOT, "include", "bprmf.h")) as f:
-        src = f.read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(bprmf_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in ("bprmf.h", "ncf.h"):
+        with open(os.path.join(ROOT, "include", h)) as f:
+            src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+        names |= set(re.findall(r"\b((?:bprmf|ncf)_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol(rl):
@@ -46,3 +48,6 @@ def test_config_layout_matches_header(rl):
     # int64,int64,int32,float,float,int32,int32,float,uint64,int32,int32,int32,int32[4]
     assert ctypes.sizeof(rl._lib.Config) == 8 + 8 + 4 + 4 + 4 + 4 + 4 + 4 + 8 + 4 + 4 + 4 + 16 + 4
     assert ctypes.sizeof(rl._lib.Stats) == 32
+    # int64 x2, int32 x5, float x5, uint64 (offset 56), int32, int32[4] -> 84, padded to 88
+    assert ctypes.sizeof(rl._lib.NcfConfig) == 88
+    assert rl._lib.NcfConfig.seed.offset == 56

@@ -112,6 +112,7 @@ SIGNATURES = {
     "ncf_train_epoch": [_P, ctypes.c_uint32, _P],
     "ncf_sample": [_P, ctypes.c_uint32, _I64, _I64, _P, _P, _P],
     "ncf_predict": [_P, _P, _P, _I64, _P],
+    "ncf_active_rows": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
     "ncf_profile": [_P, ctypes.c_int32],
     "ncf_profile_read": [_P, ctypes.POINTER(KProf)],
 }

@@ -54,23 +54,35 @@ static __host__ __device__ inline Lds lds_plan(const Dims& D) {
 size_t fwdbwd_lds_bytes(const Dims& D) { return sizeof(float) * (size_t)lds_plan(D).total; }
 
 // y[16 x 16 tile] = X[16 x K] (LDS, stride ldx) . W[n0.., :]^T (global, W[n][k], stride K):
-// 16x16x4 f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (K % 4 == 0).
+// 16x16x4 f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (K % 4 == 0).  The W rows
+// come from L2/HBM: eight k-steps of loads are issued before their 32 MFMAs, so one latency is
+// paid per eight steps, not per step.
 static __device__ __forceinline__ f32x4 tile_xwt(const float* X, int ldx, const float* W, int K,
                                                  int n0, int nmax, int lane) {
+  constexpr int U = 8;
   const int r = lane & 15, g = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const bool nok = n0 + r < nmax;
-  for (int t = 0; 16 * t < K; ++t) {
-    const int k = 16 * t + 4 * g;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-    if (k < K) {
-      a = *reinterpret_cast<const float4*>(X + r * ldx + k);
-      if (nok) b = ld4(W + (int64_t)(n0 + r) * K + k);
+  const float* wr = W + (int64_t)(n0 + r) * K;
+  for (int t0 = 0; 16 * t0 < K; t0 += U) {
+    float4 a[U], b[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int k = 16 * (t0 + q) + 4 * g;
+      b[q] = (nok && k < K) ? ld4(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int k = 16 * (t0 + q) + 4 * g;
+      a[q] = k < K ? *reinterpret_cast<const float4*>(X + r * ldx + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].x, b[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].y, b[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].z, b[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].w, b[q].w, acc, 0, 0, 0);
+    }
   }
   return acc;
 }

@@ -572,6 +572,18 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
   return ncf_check_err(h);
 }
 
+int ncf_active_rows(ncf_handle* h, int64_t* users, int64_t* items) {
+  if (!h || !users || !items) return fail(BPRMF_E_INVALID, "null argument");
+  if (int r = ncf_dev(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> tu(h->D.U), ti(h->D.I);
+  HIPCHK(hipMemcpy(tu.data(), h->G.touch_u, 4 * h->D.U, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ti.data(), h->G.touch_i, 4 * h->D.I, hipMemcpyDeviceToHost));
+  *users = std::count_if(tu.begin(), tu.end(), [](int32_t x) { return x >= 0; });
+  *items = std::count_if(ti.begin(), ti.end(), [](int32_t x) { return x >= 0; });
+  return 0;
+}
+
 int ncf_profile(ncf_handle* h, int32_t enable) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (int r = ncf_dev(h)) return r;

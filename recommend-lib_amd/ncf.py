@@ -185,6 +185,12 @@ class NCF:
 
     __call__ = forward
 
+    def active_rows(self):
+        """(users, items) whose embedding rows Adam moves every step (ever touched)."""
+        u, i = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self._L.ncf_active_rows(self._h, ctypes.byref(u), ctypes.byref(i)))
+        return u.value, i.value
+
     def profile(self, enable=True):
         _lib.check(self._L.ncf_profile(self._h, 1 if enable else 0))
 

@@ -2,9 +2,11 @@
 //
 // One handle per GPU (one process per GPU under torch.distributed.run).  The runner drives whole
 // chunks of steps from C++: no Python per step.  Transports:
-//   ipc       a push kernel writes each peer's block straight into the peer's buffer (mapped with
-//             hipIpc; xGMI peer writes) and raises a per-source flag; a one-block wait kernel
-//             spins on this rank's flags.  A few us per exchange, no host in the loop.
+//   ipc       kernels write each peer's block straight into the peer's buffer (mapped with
+//             hipIpc; xGMI peer writes) and raise a per-source flag.  Per step, the owners'
+//             gather writes the rows into the requesters' landing buffers itself and K1 waits on
+//             its row flags; K2's gradients go out with one push kernel and the owners' apply
+//             waits on its gradient flags: 5 kernels per step, no host in the loop.
 //   rccl      an RCCL communicator owned by the handle (ncclCommInitRank from a unique id the
 //             caller broadcasts); per-peer blocks move with grouped ncclSend/ncclRecv over xGMI.
 //   loopback  handles of one process exchanging through a shared table + device copies (the
@@ -153,6 +155,33 @@ struct IpcTransport final : Transport {
   }
   void free_shared(void* p) override { (void)p; }  // owned (and freed) by the transport
   int32_t* flags() const { return static_cast<int32_t*>(local[X_KINDS]); }
+  // per-step fusion (enqueue_steps): the owners' gather writes rows straight into the peers' row
+  // landing buffers, K1 reads them there after waiting on its flags, and the apply waits on the
+  // gradient flags itself; only the gradient push remains a separate kernel
+  bool fused() const { return opened && !self_exchange && world > 1; }
+  float* landing(int kind) const { return static_cast<float*>(local[kind]); }
+  void* peer_landing(int kind, int p) const { return remote[kind][p]; }
+  int32_t* peer_flag(int kind, int p) const {
+    return static_cast<int32_t*>(remote[X_KINDS][p]) + kind * kMaxWorld + rank;
+  }
+  const int32_t* my_flags(int kind) const { return flags() + kind * kMaxWorld; }
+  // the push half of an exchange: every peer's block into its landing buffer + its flag
+  int push(bprmf_handle* h, const Xchg& x) {
+    PushArgs a{};
+    const char* base = static_cast<const char*>(recv_base[x.kind]);
+    const ptrdiff_t off = static_cast<const char*>(x.recv[rank]) - base;  // this rank's block
+    for (int p = 0; p < world; ++p) {
+      a.src[p] = x.send[p];
+      if (p == rank) {
+        a.dst[p] = x.recv[p];
+      } else {
+        a.dst[p] = static_cast<char*>(remote[x.kind][p]) + off;
+        a.flag[p] = peer_flag(x.kind, p);
+      }
+    }
+    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, done + x.kind, h->stream));
+    return 0;
+  }
   int exchange(bprmf_handle* h, const Xchg& x) override {
     if (!x.bytes) return 0;
     if (world == 1) {  // no peers: only a self block, if the caller did not place it
@@ -371,6 +400,21 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
   const int self = d->tr->self_exchange ? -1 : h->cfg.rank;
   const int64_t R = h->cfg.rank;
   const size_t row_bytes = sizeof(float) * (size_t)cap * ld;
+  auto* ipc = dynamic_cast<IpcTransport*>(d->tr);
+  const bool fused = ipc && ipc->fused();
+  float* rows_in = fused ? ipc->landing(X_ROWS) : d->rows_recv;  // what K1 reads, by slot
+  PushArgs gd{};  // where the gather puts the row of position (p, idx): gd.dst[p] + idx * ld
+  for (int p = 0; p < W; ++p) {
+    if (p == self || (fused && p == R)) {
+      gd.dst[p] = rows_in + R * d->S * ld;  // this rank's own slots
+    } else if (fused) {
+      gd.dst[p] = static_cast<float*>(ipc->peer_landing(X_ROWS, p)) + R * d->S * ld;
+      gd.flag[p] = ipc->peer_flag(X_ROWS, p);
+    } else {
+      gd.dst[p] = d->rows_send + (int64_t)p * cap * ld;
+    }
+  }
+  const PeerWait pw{fused ? ipc->my_flags(X_ROWS) : nullptr, W, (int)R, h->d_err};
   std::vector<const void*> sp(W);
   std::vector<void*> rp(W);
   for (int64_t k = 0; k < n; ++k) {
@@ -378,19 +422,21 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
     {
       ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
-      HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase,
-                               d->rows_send, self, d->rows_recv + R * d->S * ld, h->stream));
+      HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase, gd,
+                               fused ? ipc->done + X_ROWS : nullptr, h->stream));
     }
-    for (int p = 0; p < W; ++p) {
-      sp[p] = p == self ? nullptr : d->rows_send + (int64_t)p * cap * ld;
-      rp[p] = d->rows_recv + (int64_t)p * d->S * ld;
+    if (!fused) {
+      for (int p = 0; p < W; ++p) {
+        sp[p] = p == self ? nullptr : d->rows_send + (int64_t)p * cap * ld;
+        rp[p] = d->rows_recv + (int64_t)p * d->S * ld;
+      }
+      if (int r = d->tr->exchange(h, Xchg{X_ROWS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0}))
+        return r;
     }
-    if (int r = d->tr->exchange(h, Xchg{X_ROWS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0}))
-      return r;
     {
       ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
       HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
-                       h->d_contrib, h->d_ugrad, d->rows_recv, h->stream));
+                       h->d_contrib, h->d_ugrad, rows_in, h->stream, pw));
     }
     {
       ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
@@ -401,12 +447,13 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
       sp[p] = p == self ? nullptr : d->grads_send + (int64_t)p * d->S * ld;
       rp[p] = d->grads_recv + (int64_t)p * cap * ld;
     }
-    if (int r = d->tr->exchange(h, Xchg{X_GRADS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0}))
-      return r;
+    const Xchg xg{X_GRADS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0};
+    if (int r = fused ? (row_bytes ? ipc->push(h, xg) : 0) : d->tr->exchange(h, xg)) return r;
     {
       ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
       HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
-                              d->grads_recv, self, d->grads_send + R * d->S * ld, h->stream));
+                              d->grads_recv, self, d->grads_send + R * d->S * ld,
+                              fused ? ipc->my_flags(X_GRADS) : nullptr, h->d_err, h->stream));
     }
   }
   return 0;

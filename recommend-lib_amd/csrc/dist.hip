@@ -83,31 +83,46 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
   }
 }
 
-// owner: rows requested by every peer for step k, brought to step t-1, packed [world][cap][ld];
-// this rank's own requests go straight to their slots (self_rows, no exchange copy)
+// owner: rows requested by every peer for step k, brought to step t-1: the row of position
+// (p, idx) goes to dst.to[p] + idx * ld (packed send blocks, this rank's own slots, or -- IPC
+// transport -- straight into peer p's landing buffer).  With dst.done set (IPC), the grid is a
+// bounded grid-stride loop and the last workgroup to finish raises each peer's row flag to the
+// step number once every workgroup's stores are acknowledged.
 template <int G4, int S>
 __global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t* __restrict__ ids_recv,
                                                         int64_t n, int world, int cap, int k,
                                                         Hyper hp, int ld,
                                                         const int32_t* __restrict__ tbase,
-                                                        float* __restrict__ rows_send, int self,
-                                                        float* __restrict__ self_rows) {
+                                                        PushArgs dst, uint32_t* __restrict__ done) {
+  constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
-  const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
-  if (x >= (int64_t)world * cap) return;
-  const int p = (int)(x / cap), idx = (int)(x % cap);
-  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
-  if ((uint32_t)row >= (uint32_t)Q.rows) return;
   const int32_t t = *tbase + k + 1;
-  const float* w = Q.W + (int64_t)row * ld + 4 * sub;
-  float4 v[S];
+  for (int64_t x = blockIdx.x * (int64_t)NG + threadIdx.x / G4; x < (int64_t)world * cap;
+       x += (int64_t)gridDim.x * NG) {
+    const int p = (int)(x / cap), idx = (int)(x % cap);
+    const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+    if ((uint32_t)row >= (uint32_t)Q.rows) continue;
+    const float* w = Q.W + (int64_t)row * ld + 4 * sub;
+    float4 v[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
-  const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[row]);
-  float* o = (p == self ? self_rows + (int64_t)idx * ld : rows_send + x * ld) + 4 * sub;
+    for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
+    const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[row]);
+    float* o = static_cast<float*>(dst.dst[p]) + (int64_t)idx * ld + 4 * sub;
 #pragma unroll
-  for (int s = 0; s < S; ++s)
-    st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
+    for (int s = 0; s < S; ++s)
+      st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
+  }
+  if (!done) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int p = 0; p < world; ++p)
+        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // owner: for each distinct row of step k (its leader position) sum the peers' gradients in peer
@@ -118,9 +133,12 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
                                                        int world, int cap, int k, Hyper hp, int ld,
                                                        const int32_t* __restrict__ tbase,
                                                        const float* __restrict__ grads_recv, int self,
-                                                       const float* __restrict__ self_grads) {
+                                                       const float* __restrict__ self_grads,
+                                                       const int32_t* __restrict__ wait_flags,
+                                                       int32_t* __restrict__ err) {
   const int sub = threadIdx.x & (G4 - 1);
   const int64_t x = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;  // p * cap + idx
+  wait_peer_flags(wait_flags, world, self, *tbase + k + 1, err);  // IPC: the peers' gradients
   if (x >= (int64_t)world * cap) return;
   const int32_t* rec = aplan + ((int64_t)k * world * cap + x) * world;
   const int32_t r0 = rec[0];
@@ -336,13 +354,14 @@ hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int ca
 }
 
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
-                             int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
-                             int self, float* self_rows, hipStream_t s) {
+                             int cap, int k, const Hyper& hp, const int32_t* tbase,
+                             const PushArgs& dst, uint32_t* done, hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
-    const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
+    unsigned blocks = blocks_for((int64_t)world * cap * G4_);
+    if (done) blocks = std::min(blocks, 160u);  // one `done` increment per workgroup
     k_owner_gather<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, n, world, cap, k, hp, g.ld,
-                                                      tbase, rows_send, self, self_rows);
+                                                      tbase, dst, done);
   }));
   return hipGetLastError();
 }
@@ -350,12 +369,14 @@ hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, in
 hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                             int64_t n, int world, int cap, int k, const Hyper& hp,
                             const int32_t* tbase, const float* grads_recv, int self,
-                            const float* self_grads, hipStream_t s) {
+                            const float* self_grads, const int32_t* wait_flags, int32_t* err,
+                            hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
     const unsigned blocks = blocks_for((int64_t)world * cap * G4_);
     k_owner_apply<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, aplan, n, world, cap, k, hp,
-                                                     g.ld, tbase, grads_recv, self, self_grads);
+                                                     g.ld, tbase, grads_recv, self, self_grads,
+                                                     wait_flags, err);
   }));
   return hipGetLastError();
 }

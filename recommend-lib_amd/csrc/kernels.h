@@ -112,12 +112,18 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s);
+// sharded K1 over the IPC transport: wait for the peers' row flags first (flags == null: none)
+struct PeerWait {
+  const int32_t* flags = nullptr;
+  int world = 1, self = 0;
+  int32_t* err = nullptr;
+};
 // K1, one lane group per triplet: c*P_u -> contrib[p]; single-triplet users updated in place,
 // the others' per-triplet gradients -> ugrad[p].  item_rows != null: sharded K1 (item rows by
 // slot from the exchange buffer)
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
-                     const float* item_rows, hipStream_t s);
+                     const float* item_rows, hipStream_t s, const PeerWait& pw = PeerWait{});
 // K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
 // grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items)
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
@@ -166,12 +172,16 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
                          hipStream_t s);
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
                            hipStream_t s);
+// row of position (p, idx) -> dst.dst[p] + idx * ld; done != null: bounded grid, the last
+// workgroup raises dst.flag[p] (IPC) to the step number
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
-                             int cap, int k, const Hyper& hp, const int32_t* tbase, float* rows_send,
-                             int self, float* self_rows, hipStream_t s);
+                             int cap, int k, const Hyper& hp, const int32_t* tbase,
+                             const PushArgs& dst, uint32_t* done, hipStream_t s);
+// wait_flags != null (IPC): every workgroup first waits for the peers' gradient flags
 hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                             int64_t n, int world, int cap, int k, const Hyper& hp,
                             const int32_t* tbase, const float* grads_recv, int self,
-                            const float* self_grads, hipStream_t s);
+                            const float* self_grads, const int32_t* wait_flags, int32_t* err,
+                            hipStream_t s);
 
 }  // namespace bprmf

@@ -54,9 +54,11 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
                                                       int step, double* loss,
                                                       float* __restrict__ contrib,
                                                       float* __restrict__ ugrad,
-                                                      const float* __restrict__ item_rows) {
+                                                      const float* __restrict__ item_rows,
+                                                      PeerWait pw) {
   const int sub = threadIdx.x & (G4 - 1);
   const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
+  if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
   // independent loads: the record (allocated for every p < B), the triplet count, the step base
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[p];
   const int n = bv.meta[0];
@@ -320,15 +322,15 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
 
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
-                     const float* item_rows, hipStream_t s) {
+                     const float* item_rows, hipStream_t s, const PeerWait& pw) {
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
     if (item_rows)
       k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
-                                                           contrib, ugrad, item_rows);
+                                                           contrib, ugrad, item_rows, pw);
     else
       k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
-                                                            contrib, ugrad, nullptr);
+                                                            contrib, ugrad, nullptr, pw);
   }));
   return hipGetLastError();
 }

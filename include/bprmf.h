@@ -212,6 +212,40 @@ int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, 
 int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
                             int64_t n_steps, bprmf_stats* stats);
 
+/* ---- ingestion: ratings files -> dense-coded rows (util/data_loader.py:27-146, :410-548) ---- */
+/* Host-only (no GPU).  Lines "<user> <sep> <item> <sep> <rating> <sep> <timestamp>" with any
+ * separator run ('\t' ml-100k u.data, '::' ml-1m/ml-10m ratings.dat, ',' ml-20m ratings.csv; a
+ * header line is skipped).  Rows with rating >= min_rating are kept (load_rate :35/:39/:43: 4 for
+ * ml-1m/10m/20m, 0 for ml-100k); core > 0 applies prepro='5core'/'10core' (:122-144, one pass:
+ * rows whose user and item both have >= core ratings); rows are ordered by (user, item, timestamp)
+ * (:118) and ids coded densely in ascending raw order (load_mat :447-448, pd.Categorical codes).
+ * threads <= 0: all hardware threads. */
+typedef struct bprmf_dataset bprmf_dataset;
+enum { BPRMF_SPLIT_LOO_TIME = 0, BPRMF_SPLIT_FO_TIME = 1 };
+int bprmf_dataset_load(const char* path, float min_rating, int32_t core, int32_t threads,
+                       bprmf_dataset** out);
+int bprmf_dataset_info(bprmf_dataset* d, int64_t* n, int64_t* user_num, int64_t* item_num);
+/* any pointer may be NULL; users/items/ratings/timestamps [n], user_ids [user_num], item_ids
+ * [item_num] (code -> raw id) */
+int bprmf_dataset_copy(bprmf_dataset* d, int32_t* users, int32_t* items, float* ratings,
+                       int64_t* timestamps, int64_t* user_ids, int64_t* item_ids);
+/* is_test[n] per row: LOO_TIME = _split_loo(by_time=1) (:410-414, each user's latest row, ties to
+ * the first in row order); FO_TIME = _split_fo(by_time=1) (:422-427, rows past the first
+ * ceil(n (1 - test_frac)) in time order; equal timestamps in row order, where the reference
+ * shuffles) */
+int bprmf_dataset_split(bprmf_dataset* d, int32_t method, double test_frac, uint8_t* is_test);
+/* Test lists (load_mat's test_data, :453-492) as (user, item) rows.  LOO_TIME: per user
+ * ascending, the test item then `count` distinct items the user never rated, ascending
+ * (_negative_sampling :430-439, count = 999; BPRMF_E_NO_NEGATIVE when fewer exist, as
+ * random.sample raises).  FO_TIME: per test user in order of first test timestamp, the test items
+ * plus never-rated candidates up to `count` in all (or `count` of the test items), ascending.
+ * Draws are a function of (seed, user).  Call with users == NULL to get the row count in *n_out;
+ * otherwise *n_out is the capacity in and the count out. */
+int bprmf_dataset_candidates(bprmf_dataset* d, const uint8_t* is_test, int32_t method,
+                             int32_t count, uint64_t seed, int64_t* n_out, int32_t* users,
+                             int32_t* items);
+int bprmf_dataset_free(bprmf_dataset* d);
+
 #ifdef __cplusplus
 }
 #endif

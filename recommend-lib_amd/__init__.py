@@ -18,8 +18,10 @@ from . import sharded
 from .sharded import ShardedBPRMF
 from . import ncf
 from .ncf import NCF, NCFData
+from . import ingest
+from .ingest import load_rate, load_mat
 
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 
 __all__ = ["BPRMF", "BPR", "BPRData", "NCF", "NCFData", "ShardedBPRMF", "BprmfError", "metrics",
-           "build", "LIB_PATH"]
+           "ingest", "load_rate", "load_mat", "build", "LIB_PATH"]

@@ -96,6 +96,14 @@ SIGNATURES = {
     "bprmf_dist_train_steps": [_P, ctypes.c_uint32, _I64, _I64, _P],
     "bprmf_dist_train_replay": [_P, _P, _P, _P, _I64, _P],
     "bprmf_row_stride": [_P, ctypes.POINTER(ctypes.c_int32)],
+    "bprmf_dataset_load": [ctypes.c_char_p, ctypes.c_float, ctypes.c_int32, ctypes.c_int32,
+                           ctypes.POINTER(ctypes.c_void_p)],
+    "bprmf_dataset_info": [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+    "bprmf_dataset_copy": [_P, _P, _P, _P, _P, _P, _P],
+    "bprmf_dataset_split": [_P, ctypes.c_int32, ctypes.c_double, _P],
+    "bprmf_dataset_candidates": [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                 ctypes.POINTER(_I64), _P, _P],
+    "bprmf_dataset_free": [_P],
     "bprmf_profile": [_P, ctypes.c_int32],
     "bprmf_profile_read": [_P, ctypes.POINTER(KProf)],
     # include/ncf.h

@@ -380,49 +380,55 @@ extern "C" {
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done);
 
-// The 2*nb step launches of a chunk (user_step k, item_step k; k < nb) captured once into a
-// hipGraph and replayed: every argument is fixed (batch k's records at a fixed offset, t read from
-// d_tbase), so a replay costs one host call instead of 2*nb launches.
+// The step launches of a chunk (user_step k, item_step k; k < nb) in blocks of kGraphSteps steps:
+// block j is captured once into a hipGraph and replayed for every chunk that reaches it (every
+// argument is fixed: batch k's records sit at a fixed offset of the batch buffer, t is read from
+// d_tbase), so replays cost one host call per block and no chunk length ever triggers a capture
+// again; the last nb % kGraphSteps steps are launched directly.
 static void drop_graphs(bprmf_handle* h) {
   for (auto& ge : h->graphs)
     if (ge.exec) hipGraphExecDestroy(ge.exec);
   h->graphs.clear();
 }
 
-static int launch_step_graph(bprmf_handle* h, int64_t nb) {
-  StepGraph* ge = nullptr;
-  for (auto& g : h->graphs)
-    if (g.nb == nb) ge = &g;
-  if (!ge) {
-    if (h->graphs.size() >= 8) drop_graphs(h);
-    StepGraph ng;
-    ng.nb = nb;
-    const int B = h->cfg.batch_size;
-    const BatchBuf bb{h->d_batch, B};
-    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    hipError_t e = hipSuccess;
-    for (int64_t k = 0; k < nb && e == hipSuccess; ++k) {
-      const BatchView v = bb.view(k);
-      e = user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss, h->d_contrib,
-                    h->d_ugrad, nullptr, h->stream);
-      if (e == hipSuccess)
-        e = item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                      h->d_ugrad, nullptr, h->stream);
-    }
-    hipGraph_t graph = nullptr;
-    const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
-    if (e != hipSuccess || e2 != hipSuccess) {
-      if (graph) hipGraphDestroy(graph);
-      return fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e != hipSuccess ? e : e2));
-    }
-    e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
-    hipGraphDestroy(graph);
-    if (e != hipSuccess) return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
-    h->graphs.push_back(ng);
-    ge = &h->graphs.back();
+static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
+  const int B = h->cfg.batch_size;
+  const BatchBuf bb{h->d_batch, B};
+  for (int64_t k = k0; k < k1; ++k) {
+    const BatchView v = bb.view(k);
+    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss, h->d_contrib,
+                     h->d_ugrad, nullptr, h->stream));
+    HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->d_ugrad,
+                     nullptr, h->stream));
   }
-  HIPCHK(hipGraphLaunch(ge->exec, h->stream));
   return 0;
+}
+
+static int launch_step_graph(bprmf_handle* h, int64_t nb) {
+  for (int64_t j = 0; (j + 1) * kGraphSteps <= nb; ++j) {
+    StepGraph* ge = nullptr;
+    for (auto& g : h->graphs)
+      if (g.nb == j) ge = &g;
+    if (!ge) {
+      StepGraph ng;
+      ng.nb = j;
+      HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+      const int rc = step_launches(h, j * kGraphSteps, (j + 1) * kGraphSteps);
+      hipGraph_t graph = nullptr;
+      const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+      if (rc || e2 != hipSuccess) {
+        if (graph) hipGraphDestroy(graph);
+        return rc ? rc : fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e2));
+      }
+      const hipError_t e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
+      hipGraphDestroy(graph);
+      if (e != hipSuccess) return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
+      h->graphs.push_back(ng);
+      ge = &h->graphs.back();
+    }
+    HIPCHK(hipGraphLaunch(ge->exec, h->stream));
+  }
+  return step_launches(h, nb / kGraphSteps * kGraphSteps, nb);
 }
 
 // One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler

@@ -304,7 +304,8 @@ struct DistState {
   int64_t aplan_n[2] = {0, 0};
   int32_t* ids_send = nullptr;     // [W][n][cap]
   int32_t* ids_recv = nullptr;     // shared, 2 parities x [W][nmax][S]
-  int32_t* aplan[2] = {nullptr, nullptr};  // [n][W][cap][W] per parity
+  int32_t* aplan[2] = {nullptr, nullptr};  // per parity: aplan [n][W][cap][W], then gdep
+                                           // [n][W][cap][W], then gfree [n][W][cap]
   int32_t* vals = nullptr;         // shared, 2 parities x [W] (capacity max)
   int32_t* d_cap = nullptr;
   float* rows_send = nullptr;   // owner:     [W][cap][ld]
@@ -378,7 +379,7 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   DistState* d = h->dist;
   const int64_t W = h->cfg.world;
-  const int64_t ap = n * W * std::max(cap, 1) * W;
+  const int64_t ap = n * W * std::max(cap, 1) * (2 * W + 1);
   if (ap <= d->aplan_n[par]) return 0;
   if (d->aplan[par]) HIPCHK(hipFree(d->aplan[par]));
   d->aplan[par] = nullptr;
@@ -417,14 +418,17 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
   const PeerWait pw{fused ? ipc->my_flags(X_ROWS) : nullptr, W, (int)R, h->d_err};
   std::vector<const void*> sp(W);
   std::vector<void*> rp(W);
+  const int64_t WC = (int64_t)W * cap;
+  const int32_t* gdep = aplan + n * WC * W;
+  const int32_t* gfree = gdep + n * WC * W;
+  {  // the chunk's first rows; later steps' rows come with the previous step's apply
+    ProfScope ps(h, BPRMF_KPROF_OWNER, prof_kernels && (h->t % kProfStride) == 0);
+    HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, 0, h->hp, h->d_tbase, gd,
+                             fused ? ipc->done + X_ROWS : nullptr, h->stream));
+  }
   for (int64_t k = 0; k < n; ++k) {
     const BatchView v = bb.view(k);
     const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
-    {
-      ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
-      HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase, gd,
-                               fused ? ipc->done + X_ROWS : nullptr, h->stream));
-    }
     if (!fused) {
       for (int p = 0; p < W; ++p) {
         sp[p] = p == self ? nullptr : d->rows_send + (int64_t)p * cap * ld;
@@ -451,9 +455,15 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     if (int r = fused ? (row_bytes ? ipc->push(h, xg) : 0) : d->tr->exchange(h, xg)) return r;
     {
       ProfScope ps(h, BPRMF_KPROF_OWNER, sampled);
-      HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
-                              d->grads_recv, self, d->grads_send + R * d->S * ld,
-                              fused ? ipc->my_flags(X_GRADS) : nullptr, h->d_err, h->stream));
+      const int32_t* wf = fused ? ipc->my_flags(X_GRADS) : nullptr;
+      const float* own = d->grads_send + R * d->S * ld;
+      if (k + 1 < n)  // apply step k, gather step k+1
+        HIPCHK(dist_owner_step(h->geom, h->Q, ids_recv, aplan, gdep, gfree, n, W, cap, (int)k, h->hp,
+                               h->d_tbase, d->grads_recv, self, own, wf, h->d_err, gd,
+                               fused ? ipc->done + X_ROWS : nullptr, h->stream));
+      else
+        HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
+                                d->grads_recv, self, own, wf, h->d_err, h->stream));
     }
   }
   return 0;
@@ -544,7 +554,8 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
                                           nullptr, 0, seq});
     d->tr->self_exchange = se;
     if (r) return r;
-    HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, h->stream));
+    HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, aplan + n * W * (int64_t)cap * W,
+                           aplan + 2 * n * W * (int64_t)cap * W, h->stream));
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));

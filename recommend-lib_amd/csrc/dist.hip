@@ -57,19 +57,33 @@ static __device__ __forceinline__ int find_row(const int32_t* __restrict__ list,
 // apply plan: aplan[k][p][idx][q] = q*cap + (position of row in peer q's list of step k), -1 if q
 // does not request it; a position whose row an earlier peer also requests (or a pad) gets
 // aplan[..][0] = -2 (not a leader: skipped by k_owner_apply).
+// Gather plan of the fused owner step (k_owner_step: apply step k, then gather step k+1):
+// gdep[k][p][idx][q] = position of the leader's row in peer q's list of step k+1, -1 if q does not
+// request it then (the leader serves those positions from the row it just wrote); gfree[k][p][idx]
+// = 1 when position (p, idx) of step k holds a row that step k-1 did not apply (k = 0: every row),
+// gathered on its own.
 __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
-                             int32_t* __restrict__ aplan) {
+                             int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
+                             int32_t* __restrict__ gfree) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= n * world * (int64_t)cap) return;
   const int idx = (int)(x % cap);
   const int p = (int)((x / cap) % world);
   const int64_t k = x / ((int64_t)cap * world);
   int32_t* rec = aplan + x * world;
+  int32_t* dep = gdep + x * world;
+  for (int q = 0; q < world; ++q) dep[q] = -1;
   const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+  gfree[x] = 0;
   if (row < 0) {
     rec[0] = -2;
     return;
   }
+  bool free_row = true;
+  if (k > 0)
+    for (int q = 0; q < world && free_row; ++q)
+      if (find_row(ids_recv + ((int64_t)q * n + k - 1) * cap, cap, (uint32_t)row) >= 0) free_row = false;
+  gfree[x] = free_row ? 1 : 0;
   for (int q = 0; q < p; ++q)
     if (find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row) >= 0) {
       rec[0] = -2;
@@ -80,6 +94,7 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
     if (q == p) pos = idx;
     else if (q > p) pos = find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row);
     rec[q] = pos < 0 ? -1 : q * cap + pos;
+    if (k + 1 < n) dep[q] = find_row(ids_recv + ((int64_t)q * n + k + 1) * cap, cap, (uint32_t)row);
   }
 }
 
@@ -186,6 +201,114 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
                     fmaf(-lr, fmaf(wd, v.z, g[s].z), v.z), fmaf(-lr, fmaf(wd, v.w, g[s].w), v.w)));
   }
   if (sub == 0) Q.stamp[row] = t;
+}
+
+// Fused owner step: apply step k (as k_owner_apply) and gather step k+1 (as k_owner_gather) in one
+// launch.  A row step k applies is served to step k+1's requesters by its leader, from the value
+// it just stored (gdep); rows step k does not apply are gathered by their own groups (gfree).  No
+// row is both read by a free gather and written by an apply, so the groups are independent.
+// With done set (IPC), a bounded grid-stride grid and the last workgroup raises the peers' row
+// flags to step k+1.
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_owner_step(Table Q, const int32_t* __restrict__ ids_recv,
+                                                      const int32_t* __restrict__ aplan,
+                                                      const int32_t* __restrict__ gdep,
+                                                      const int32_t* __restrict__ gfree, int64_t n,
+                                                      int world, int cap, int k, Hyper hp, int ld,
+                                                      const int32_t* __restrict__ tbase,
+                                                      const float* __restrict__ grads_recv, int self,
+                                                      const float* __restrict__ self_grads,
+                                                      const int32_t* __restrict__ wait_flags,
+                                                      int32_t* __restrict__ err, PushArgs dst,
+                                                      uint32_t* __restrict__ done) {
+  constexpr int NG = kBlock / G4;
+  const int sub = threadIdx.x & (G4 - 1);
+  const int32_t t = *tbase + k + 1;
+  wait_peer_flags(wait_flags, world, self, t, err);  // IPC: the peers' gradients of step k
+  const int64_t WC = (int64_t)world * cap;
+  const float lr = hp.lr, wd = hp.wd;
+  for (int64_t x = blockIdx.x * (int64_t)NG + threadIdx.x / G4; x < 2 * WC; x += (int64_t)gridDim.x * NG) {
+    if (x < WC) {  // apply: the leader position of a row of step k
+      const int32_t* rec = aplan + ((int64_t)k * WC + x) * world;
+      const int32_t r0 = rec[0];
+      if (r0 == -2) continue;
+      const int p = (int)(x / cap), idx = (int)(x % cap);
+      const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
+      float* w = Q.W + (int64_t)row * ld + 4 * sub;
+      float4 cur[S], g[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        cur[s] = ld4(w + 4 * G4 * s);
+        g[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const int32_t stamp = Q.stamp[row];
+      for (int q0 = 0; q0 < world; q0 += 8) {  // peers' rows in flight, summed in peer order
+        int32_t pos[8];
+        float4 gr[8][S];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          pos[m] = q0 + m < world ? (q0 + m == 0 ? r0 : rec[q0 + m]) : -1;
+          if (pos[m] >= 0) {
+            const int q = pos[m] / cap, i = pos[m] - q * cap;
+            const float* gp = (q == self ? self_grads + (int64_t)i * ld : grads_recv + (int64_t)pos[m] * ld) + 4 * sub;
+#pragma unroll
+            for (int s = 0; s < S; ++s) gr[m][s] = ld4(gp + 4 * G4 * s);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          if (pos[m] >= 0) {
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+              g[s] = make_float4(g[s].x + gr[m][s].x, g[s].y + gr[m][s].y, g[s].z + gr[m][s].z,
+                                 g[s].w + gr[m][s].w);
+          }
+      }
+      const float f = decay_pow(hp.log2a, t - 1 - stamp);
+      float4 nv[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const float4 v = make_float4(cur[s].x * f, cur[s].y * f, cur[s].z * f, cur[s].w * f);
+        nv[s] = make_float4(fmaf(-lr, fmaf(wd, v.x, g[s].x), v.x), fmaf(-lr, fmaf(wd, v.y, g[s].y), v.y),
+                            fmaf(-lr, fmaf(wd, v.z, g[s].z), v.z), fmaf(-lr, fmaf(wd, v.w, g[s].w), v.w));
+        st4(w + 4 * G4 * s, nv[s]);
+      }
+      if (sub == 0) Q.stamp[row] = t;
+      const int32_t* dep = gdep + ((int64_t)k * WC + x) * world;
+      for (int q = 0; q < world; ++q) {  // step k+1's requests of this row: the new value
+        const int32_t i2 = dep[q];
+        if (i2 < 0) continue;
+        float* o = static_cast<float*>(dst.dst[q]) + (int64_t)i2 * ld + 4 * sub;
+#pragma unroll
+        for (int s = 0; s < S; ++s) st4(o + 4 * G4 * s, nv[s]);
+      }
+    } else {  // gather: a position of step k+1 whose row step k does not apply
+      const int64_t y = x - WC;
+      if (!gfree[(int64_t)(k + 1) * WC + y]) continue;
+      const int q = (int)(y / cap), idx = (int)(y % cap);
+      const int32_t row = ids_recv[((int64_t)q * n + k + 1) * cap + idx];
+      const float* w = Q.W + (int64_t)row * ld + 4 * sub;
+      float4 v[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
+      const float f = decay_pow(hp.log2a, t - Q.stamp[row]);  // brought to step (t + 1) - 1
+      float* o = static_cast<float*>(dst.dst[q]) + (int64_t)idx * ld + 4 * sub;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
+    }
+  }
+  if (!done) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int p = 0; p < world; ++p)
+        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ---- IPC transport: blocks pushed straight into the peers' buffers over xGMI ----------------
@@ -347,9 +470,26 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
 }
 
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           hipStream_t s) {
+                           int32_t* gdep, int32_t* gfree, hipStream_t s) {
   if (n <= 0 || cap <= 0) return hipSuccess;
-  k_owner_plan<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap, aplan);
+  k_owner_plan<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap, aplan,
+                                                                      gdep, gfree);
+  return hipGetLastError();
+}
+
+hipError_t dist_owner_step(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
+                           const int32_t* gdep, const int32_t* gfree, int64_t n, int world, int cap,
+                           int k, const Hyper& hp, const int32_t* tbase, const float* grads_recv,
+                           int self, const float* self_grads, const int32_t* wait_flags,
+                           int32_t* err, const PushArgs& dst, uint32_t* done, hipStream_t s) {
+  if (cap <= 0) return hipSuccess;
+  BPRMF_DISPATCH4D(g, ({
+    unsigned blocks = blocks_for(2LL * world * cap * G4_);
+    if (done) blocks = std::min(blocks, 160u);  // one `done` increment per workgroup
+    k_owner_step<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, aplan, gdep, gfree, n, world, cap,
+                                                    k, hp, g.ld, tbase, grads_recv, self,
+                                                    self_grads, wait_flags, err, dst, done);
+  }));
   return hipGetLastError();
 }
 

@@ -20,8 +20,9 @@ int fail(int code, const char* fmt, ...);
     if (e_ != hipSuccess) return bprmf::fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
 
-struct StepGraph {  // a captured chunk of step launches (launch_step_graph)
-  int64_t nb = 0;
+constexpr int64_t kGraphSteps = 64;  // steps per captured step graph (launch_step_graph)
+struct StepGraph {  // a captured block of step launches (launch_step_graph)
+  int64_t nb = 0;   // the block's index j: steps [j * kGraphSteps, (j + 1) * kGraphSteps) of a chunk
   hipGraphExec_t exec = nullptr;
 };
 constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step

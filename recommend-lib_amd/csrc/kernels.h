@@ -171,7 +171,13 @@ hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStre
 hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
                          hipStream_t s);
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           hipStream_t s);
+                           int32_t* gdep, int32_t* gfree, hipStream_t s);
+// apply step k and gather step k+1 in one launch (dist.hip k_owner_step)
+hipError_t dist_owner_step(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
+                           const int32_t* gdep, const int32_t* gfree, int64_t n, int world, int cap,
+                           int k, const Hyper& hp, const int32_t* tbase, const float* grads_recv,
+                           int self, const float* self_grads, const int32_t* wait_flags,
+                           int32_t* err, const PushArgs& dst, uint32_t* done, hipStream_t s);
 // row of position (p, idx) -> dst.dst[p] + idx * ld; done != null: bounded grid, the last
 // workgroup raises dst.flag[p] (IPC) to the step number
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,

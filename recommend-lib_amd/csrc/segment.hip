@@ -308,7 +308,9 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
   const int64_t iloc = (i_rows + world - 1) / world;
   if ((uint64_t)iloc * (uint64_t)world >= 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const int ub = bits_for(u_rows), ib = bits_for(iloc * world);
+  // one value above every valid key: an empty position (kNone) must sort after all of them, and
+  // the sorts see only these low bits of it
+  const int ub = bits_for(u_rows + 1), ib = bits_for(iloc * world + 1);
   if (B <= kBuildThreads * 4)
     k_build_batches<4><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,

@@ -20,6 +20,10 @@
 
 #include "device_common.h"
 
+#ifndef UB_MASK
+#define UB_MASK 0
+#endif
+
 namespace bprmf {
 
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -77,10 +81,14 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
       vi[k] = ld4(qi + 4 * G4 * k);
       vj[k] = ld4(qj + 4 * G4 * k);
     }
+#if UB_MASK & 1
+    const float fi = 1.f, fj = 1.f, fu = 1.f;
+#else
     const int32_t su = P.stamp[u];
     const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
     const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
     const float fu = decay_pow(hp.log2a, t - 1 - su);
+#endif
     float di = 0.f, dj = 0.f;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -98,11 +106,17 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
     float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
     for (int k = 0; k < S; ++k) st4(cb + 4 * G4 * k, scale4(pu[k], c));
+#if UB_MASK & 2
+    if (false) {
+#else
     if (r.w) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
+#endif
 #pragma unroll
       for (int k = 0; k < S; ++k)
         st4(pw + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
+#if !(UB_MASK & 4)
       if (sub == 0) P.stamp[u] = t;
+#endif
     } else {  // K2 sums the segment's gradients in position order
       float* ub = ugrad + (int64_t)p * ld + 4 * sub;
 #pragma unroll

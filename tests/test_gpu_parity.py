@@ -98,6 +98,28 @@ def test_step_vs_oracle_all_geometries(rl, d):
     np.testing.assert_allclose(Qg, Q, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("U,I", [(8, 16), (2, 4), (64, 32)])
+def test_power_of_two_tables_with_partial_batches_vs_oracle(rl, U, I):
+    """Partial batches (empty tail positions) on tables whose row counts are powers of two, where
+    an empty position's radix-sort key is only one past the last row id."""
+    g = np.random.default_rng(U * 100 + I)
+    d, B = 8, 64
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    m = _model(rl, U, I, d, B, lr=0.05, wd=0.01)
+    m.set_weights(P0, Q0)
+    P, Q = P0.copy(), Q0.copy()
+    for n in (B + 23, 5, 2 * B - 1):  # every call ends in a partial batch
+        u, i, j = g.integers(0, U, n), g.integers(0, I, n), g.integers(0, I, n)
+        u[-1] = U - 1  # the last row is always present
+        m.train_triplets(u, i, j)
+        for s in range(0, n, B):
+            O.bpr_step_dense(P, Q, u[s:s + B], i[s:s + B], j[s:s + B], 0.05, 0.01)
+    Pg, Qg = m.get_weights()
+    np.testing.assert_allclose(Pg, P, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Qg, Q, rtol=1e-5, atol=1e-6)
+
+
 def test_large_batch_atomic_path_vs_oracle(rl):
     """batch_size > kMaxSegBatch (8192) takes the f32-atomic path (fwd_scatter + apply_refs)."""
     g = np.random.default_rng(8)

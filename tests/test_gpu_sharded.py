@@ -64,6 +64,36 @@ def test_sharded_replay_equals_single_gpu_global_batch(rl, world):
     np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("Uu,Ii", [(16, 32), (4, 8)])
+def test_sharded_replay_power_of_two_shards(rl, Uu, Ii):
+    """Two shards whose local user counts are powers of two: each shard's batch has empty slots
+    (the other shard's triplets) in the middle, whose sort key must order after every local user
+    (regression: with log2(rows) sort bits it collided with the last user and split its segment)."""
+    g = np.random.default_rng(Uu)
+    world, GB, steps, d = 2, 64, 5, 8
+    P0 = (0.1 * g.standard_normal((Uu, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((Ii, d))).astype(np.float32)
+    batches = [(g.integers(0, Uu, GB), g.integers(0, Ii, GB), g.integers(0, Ii, GB)) for _ in range(steps)]
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(Uu, Ii, d, lr=0.05, wd=0.01, batch_size=GB, device=0, comm=comm)
+        m.set_weights(sh.shard_rows(P0, r, world), sh.shard_rows(Q0, r, world))
+        m.plan_replay(batches)
+        for k in range(steps):
+            m.step_replay(k)
+        return m.get_weights()
+
+    parts = _run_threads(rl, world, fn)
+    P = sh.unshard_rows([p[0] for p in parts], Uu)
+    Q = sh.unshard_rows([p[1] for p in parts], Ii)
+    Pr, Qr = P0.copy(), Q0.copy()
+    for u, i, j in batches:
+        O.bpr_step_dense(Pr, Qr, u, i, j, 0.05, 0.01)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+
+
 def test_sharded_sampler_training(rl, golden):
     """Sampler mode over 2 shards: each shard's batches are its own users' triplets, bit-exact with
     the oracle sampler for that shard; training reduces the loss."""

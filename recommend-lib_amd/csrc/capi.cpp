@@ -184,7 +184,7 @@ int bprmf_destroy(bprmf_handle* h) {
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err,
-                  h->d_batch, h->d_contrib, h->d_ugrad, h->d_tbase};
+                  h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -363,6 +363,7 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   if (!h->d_contrib) {
     if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
     if (int r = dalloc(&h->d_ugrad, B * h->geom.ld)) return r;
+    if (int r = dalloc(&h->d_xloss, B)) return r;
     if (int r = dalloc(&h->d_tbase, 1)) return r;
   }
   if (n_batches <= h->batch_cap) return 0;
@@ -396,10 +397,10 @@ static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
   const BatchBuf bb{h->d_batch, B};
   for (int64_t k = k0; k < k1; ++k) {
     const BatchView v = bb.view(k);
-    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss, h->d_contrib,
+    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss, h->d_contrib,
                      h->d_ugrad, nullptr, h->stream));
     HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->d_ugrad,
-                     nullptr, h->stream));
+                     nullptr, h->stream, h->d_xloss, h->d_loss));
   }
   return 0;
 }
@@ -484,13 +485,13 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
       const bool sampled = ((h->t + k) % kProfStride) == 0;
       {
         ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
-        HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
+        HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss,
                          h->d_contrib, h->d_ugrad, nullptr, h->stream));
       }
       {
         ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
         HIPCHK(item_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                         h->d_ugrad, nullptr, h->stream));
+                         h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss));
       }
     }
   }
@@ -892,7 +893,7 @@ int bprmf_dist_user_step(bprmf_handle* h, int64_t k, const float* item_rows) {
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
   ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER);
   HIPCHK(user_step(h->geom, bb.view(k), h->cfg.batch_size, h->P, h->Q, h->hp, h->d_tbase, 0,
-                   h->d_loss, h->d_contrib, h->d_ugrad, item_rows, h->stream));
+                   h->d_xloss, h->d_contrib, h->d_ugrad, item_rows, h->stream));
   return 0;
 }
 
@@ -902,7 +903,7 @@ int bprmf_dist_item_grads(bprmf_handle* h, int64_t k, float* grads) {
   const BatchBuf bb{h->d_batch, h->cfg.batch_size};
   ProfScope ps(h, BPRMF_KPROF_APPLY);
   HIPCHK(item_step(h->geom, bb.view(k), h->cfg.batch_size, h->P, h->Q, h->hp, h->d_tbase, 0,
-                   h->d_contrib, h->d_ugrad, grads, h->stream));
+                   h->d_contrib, h->d_ugrad, grads, h->stream, h->d_xloss, h->d_loss));
   return 0;
 }
 

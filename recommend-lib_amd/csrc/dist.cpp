@@ -439,13 +439,13 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     }
     {
       ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
-      HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_loss,
+      HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss,
                        h->d_contrib, h->d_ugrad, rows_in, h->stream, pw));
     }
     {
       ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
       HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                       h->d_ugrad, d->grads_send, h->stream));
+                       h->d_ugrad, d->grads_send, h->stream, h->d_xloss, h->d_loss));
     }
     for (int p = 0; p < W; ++p) {
       sp[p] = p == self ? nullptr : d->grads_send + (int64_t)p * d->S * ld;

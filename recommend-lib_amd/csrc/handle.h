@@ -53,6 +53,7 @@ struct bprmf_handle {
   int64_t batch_cap = 0;
   float* d_contrib = nullptr;  // [B, ld] c*P_u per triplet (K1 -> K2)
   float* d_ugrad = nullptr;    // [B, ld] user gradient per triplet of multi-triplet users
+  float* d_xloss = nullptr;    // [B] x per triplet (K1 -> K2's loss workgroup)
   int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;

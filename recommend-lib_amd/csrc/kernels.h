@@ -119,16 +119,19 @@ struct PeerWait {
   int32_t* err = nullptr;
 };
 // K1, one lane group per triplet: c*P_u -> contrib[p]; single-triplet users updated in place,
-// the others' per-triplet gradients -> ugrad[p].  item_rows != null: sharded K1 (item rows by
+// the others' per-triplet gradients -> ugrad[p]; x = <P_u,Q_i> - <P_u,Q_j> -> xloss[p] (if set).  item_rows != null: sharded K1 (item rows by
 // slot from the exchange buffer)
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
+                     const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw = PeerWait{});
 // K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
-// grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items)
+// grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items).
+// loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
+// left in xloss[B], to loss[0] (fixed-order f64 tree)
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
-                     float* grads, hipStream_t s);
+                     float* grads, hipStream_t s, const float* xloss = nullptr,
+                     double* loss = nullptr);
 int item_long_blocks(int B);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,

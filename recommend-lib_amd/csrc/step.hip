@@ -20,10 +20,6 @@
 
 #include "device_common.h"
 
-#ifndef UB_MASK
-#define UB_MASK 0
-#endif
-
 namespace bprmf {
 
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -55,7 +51,7 @@ static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, floa
 template <int G4, int S, bool SH>
 __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
                                                       int ld, const int32_t* __restrict__ tbase,
-                                                      int step, double* loss,
+                                                      int step, float* __restrict__ xloss,
                                                       float* __restrict__ contrib,
                                                       float* __restrict__ ugrad,
                                                       const float* __restrict__ item_rows,
@@ -67,7 +63,6 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[p];
   const int n = bv.meta[0];
   const int32_t t = *tbase + step + 1;
-  float lsum = 0.f;
   if (p < n) {
     const int32_t i = r.x, j = r.y, u = r.z;
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
@@ -81,14 +76,10 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
       vi[k] = ld4(qi + 4 * G4 * k);
       vj[k] = ld4(qj + 4 * G4 * k);
     }
-#if UB_MASK & 1
-    const float fi = 1.f, fj = 1.f, fu = 1.f;
-#else
     const int32_t su = P.stamp[u];
     const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
     const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
     const float fu = decay_pow(hp.log2a, t - 1 - su);
-#endif
     float di = 0.f, dj = 0.f;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -102,28 +93,21 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
     dj = group_sum<G4>(dj);
     const float x = di - dj;
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
-    if (sub == 0 && loss) lsum = softplus(-x);
+    if (sub == 0 && xloss) xloss[p] = x;  // K2 sums the loss terms
     float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
     for (int k = 0; k < S; ++k) st4(cb + 4 * G4 * k, scale4(pu[k], c));
-#if UB_MASK & 2
-    if (false) {
-#else
     if (r.w) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
-#endif
 #pragma unroll
       for (int k = 0; k < S; ++k)
         st4(pw + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
-#if !(UB_MASK & 4)
       if (sub == 0) P.stamp[u] = t;
-#endif
     } else {  // K2 sums the segment's gradients in position order
       float* ub = ugrad + (int64_t)p * ld + 4 * sub;
 #pragma unroll
       for (int k = 0; k < S; ++k) st4(ub + 4 * G4 * k, scale4(sub4(vi[k], vj[k]), -c));
     }
   }
-  if (loss) wave_add_loss(loss, lsum);
 }
 
 template <int G4, int S>
@@ -201,13 +185,32 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   const int32_t* __restrict__ tbase, int step,
                                                   const float* __restrict__ contrib,
                                                   const float* __restrict__ ugrad, int long_blocks,
-                                                  int item_blocks, float* __restrict__ grads) {
+                                                  int item_blocks, float* __restrict__ grads,
+                                                  const float* __restrict__ xloss,
+                                                  double* __restrict__ loss) {
   constexpr int NG = KB / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
   const int32_t t = *tbase + step + 1;
-  if ((int)blockIdx.x >= long_blocks + item_blocks) {  // users with several triplets
-    const int m = ((int)blockIdx.x - long_blocks - item_blocks) * NG + grp;
+  if (loss && blockIdx.x == 0) {  // the step's loss (first block: dispatched first, off the tail)
+    __shared__ double red[KB / 64];
+    const int n = bv.meta[0];
+    double acc = 0.0;
+    for (int p = threadIdx.x; p < n; p += KB) acc += (double)softplus(-xloss[p]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);  // fixed butterfly
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the only writer of this slot in the launch
+      double tot = 0.0;
+      for (int w = 0; w < KB / 64; ++w) tot += red[w];
+      loss[0] += tot;
+    }
+    return;
+  }
+  const int bid = (int)blockIdx.x - (loss ? 1 : 0);
+  if (bid >= long_blocks + item_blocks) {  // users with several triplets
+    const int m = (bid - long_blocks - item_blocks) * NG + grp;
     const int4 r0 = reinterpret_cast<const int4*>(bv.mrec + (int64_t)m * kRec)[0];
     const int n_multi = bv.meta[4];
     if (m >= n_multi) return;
@@ -224,11 +227,11 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     if (sub == 0) P.stamp[u] = t;
     return;
   }
-  if ((int)blockIdx.x < long_blocks) {
+  if (bid < long_blocks) {
     __shared__ float4 part[NG][G4 * S];
-    const int4 r0 = reinterpret_cast<const int4*>(bv.lrec + (int64_t)blockIdx.x * kRec)[0];
+    const int4 r0 = reinterpret_cast<const int4*>(bv.lrec + (int64_t)bid * kRec)[0];
     const int n_long = bv.meta[3];
-    if ((int)blockIdx.x >= n_long) return;  // uniform over the block
+    if (bid >= n_long) return;  // uniform over the block
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
     float4 g[S];
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     }
     return;
   }
-  const int s = (blockIdx.x - long_blocks) * NG + grp;
+  const int s = (bid - long_blocks) * NG + grp;
   const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
   const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
   const int n_iseg = bv.meta[2];
@@ -335,15 +338,15 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
   }
 
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
-                     const int32_t* tbase, int step, double* loss, float* contrib, float* ugrad,
+                     const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw) {
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
     if (item_rows)
-      k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
+      k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
                                                            contrib, ugrad, item_rows, pw);
     else
-      k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, loss,
+      k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
                                                             contrib, ugrad, nullptr, pw);
   }));
   return hipGetLastError();
@@ -353,21 +356,23 @@ int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg
 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
-                     float* grads, hipStream_t s) {
+                     float* grads, hipStream_t s, const float* xloss, double* loss) {
   const int long_blocks = item_long_blocks(B);
+  if (!xloss) loss = nullptr;
   BPRMF_DISPATCH4(g, ({
     constexpr int KB = S_ == 1 ? 1024 : 512;
     constexpr int NG = KB / G4_;
     const int item_blocks = (int)((2LL * B + NG - 1) / NG);
     const int user_blocks = (int)((B / 2 + NG - 1) / NG);  // multi-triplet users <= B/2
-    const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks);
+    const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks + (loss ? 1 : 0));
     if (grads)
       k_item_step<G4_, S_, true, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
-                                                           ugrad, long_blocks, item_blocks, grads);
+                                                           ugrad, long_blocks, item_blocks, grads,
+                                                           xloss, loss);
     else
       k_item_step<G4_, S_, false, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
                                                             contrib, ugrad, long_blocks,
-                                                            item_blocks, nullptr);
+                                                            item_blocks, nullptr, xloss, loss);
   }));
   return hipGetLastError();
 }

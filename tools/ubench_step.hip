@@ -254,6 +254,8 @@ int main(int argc, char** argv) {
   CK(hipMemset(contrib, 0, 4 * (int64_t)B * ld));
   CK(hipMemset(ugrad, 0, 4 * (int64_t)B * ld));
   CK(hipMalloc(&loss, 8 * kLossSlots));
+  float* xl;
+  CK(hipMalloc(&xl, 4 * (int64_t)B));
   CK(hipMemset(loss, 0, 8 * kLossSlots));
   SamplerArgs sa{};
   BatchBuf bb{dbatch, B};
@@ -337,19 +339,19 @@ int main(int argc, char** argv) {
     }
   }
   printf("K1 user_step:                     %7.2f us\n", time_loop(S, [&](int k) {
-           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, ugrad, nullptr, 0));
+           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, xl, contrib, ugrad, nullptr, 0));
          }));
   printf("K1 user_step, same batch:         %7.2f us\n", time_loop(S, [&](int k) {
-           CK(user_step(g, bb.view(0), B, P, Q, hp, dt, k, loss, contrib, ugrad, nullptr, 0));
+           CK(user_step(g, bb.view(0), B, P, Q, hp, dt, k, xl, contrib, ugrad, nullptr, 0));
          }));
   printf("K2 item_step, same batch:         %7.2f us\n", time_loop(S, [&](int k) {
-           CK(item_step(g, bb.view(0), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0));
+           CK(item_step(g, bb.view(0), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0, xl, loss));
          }));
   printf("K1 user_step (no loss):           %7.2f us\n", time_loop(S, [&](int k) {
            CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, nullptr, contrib, ugrad, nullptr, 0));
          }));
   printf("K2 item_step:                     %7.2f us\n", time_loop(S, [&](int k) {
-           CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0));
+           CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0, xl, loss));
          }));
   if (g.G4 == 32 && g.S == 1) {
     constexpr int KB = 1024, NG = KB / 32;
@@ -357,20 +359,20 @@ int main(int argc, char** argv) {
     const int ib = (2 * B + NG - 1) / NG, ubk = (B / 2 + NG - 1) / NG;
     printf("K2 long items only:               %7.2f us\n", time_loop(S, [&](int k) {
              k_item_step<32, 1, false, KB><<<lb, KB>>>(bb.view(k % S), P, Q, hp, ld, dt, k, contrib,
-                                                       ugrad, lb, ib, nullptr);
+                                                       ugrad, lb, ib, nullptr, nullptr, nullptr);
            }));
     printf("K2 short items only:              %7.2f us\n", time_loop(S, [&](int k) {
              k_item_step<32, 1, false, KB><<<ib, KB>>>(bb.view(k % S), P, Q, hp, ld, dt, k, contrib,
-                                                       ugrad, 0, ib, nullptr);
+                                                       ugrad, 0, ib, nullptr, nullptr, nullptr);
            }));
     printf("K2 multi-triplet users only:      %7.2f us\n", time_loop(S, [&](int k) {
              k_item_step<32, 1, false, KB><<<ubk, KB>>>(bb.view(k % S), P, Q, hp, ld, dt, k, contrib,
-                                                        ugrad, 0, 0, nullptr);
+                                                        ugrad, 0, 0, nullptr, nullptr, nullptr);
            }));
   }
   printf("K1+K2 step:                       %7.2f us\n", time_loop(S, [&](int k) {
-           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, ugrad, nullptr, 0));
-           CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0));
+           CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, xl, contrib, ugrad, nullptr, 0));
+           CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, 0, xl, loss));
          }));
   if (g.G4 == 32 && g.S == 1) {
     const unsigned nb = (unsigned)(B / (kBlock / 32));
@@ -379,9 +381,9 @@ int main(int argc, char** argv) {
            k_k1x<FL><<<nb, kBlock, 0, st>>>(bb.view(k % S), P, Q, hp, ld, dt, k, loss, contrib, ugrad); }));
     K1X(63) K1X(62) K1X(61) K1X(59) K1X(55) K1X(47) K1X(31) K1X(16) K1X(0)
     printf("graph K1 product:                 %7.2f us\n", graph_time(64, [&](int k, hipStream_t st) {
-             CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, ugrad, nullptr, st)); }));
+             CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, xl, contrib, ugrad, nullptr, st)); }));
     printf("graph K2 product:                 %7.2f us\n", graph_time(64, [&](int k, hipStream_t st) {
-             CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, st)); }));
+             CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, st, xl, loss)); }));
     printf("graph empty 512x256:              %7.2f us\n", graph_time(64, [&](int k, hipStream_t st) {
              k_empty<<<nb, kBlock, 0, st>>>(); }));
   }
@@ -392,8 +394,8 @@ int main(int argc, char** argv) {
     hipGraphExec_t ge;
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
     for (int k = 0; k < nbg; ++k) {
-      CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, loss, contrib, ugrad, nullptr, st));
-      CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, st));
+      CK(user_step(g, bb.view(k % S), B, P, Q, hp, dt, k, xl, contrib, ugrad, nullptr, st));
+      CK(item_step(g, bb.view(k % S), B, P, Q, hp, dt, k, contrib, ugrad, nullptr, st, xl, loss));
     }
     CK(hipStreamEndCapture(st, &gr));
     CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));

@@ -110,18 +110,21 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
   }
 }
 
-template <int G4, int S>
-static __device__ __forceinline__ void apply_item(Table Q, int32_t item, const float4 (&g)[S],
-                                                  const Hyper& hp, int ld, int32_t t, int sub) {
-  float* w = Q.W + (int64_t)item * ld + 4 * sub;
+// an item row and its stamp, loaded as soon as the segment's record is known so the loads run
+// alongside the contribution gathers instead of after them (single GPU only; sharded K2 emits the
+// gradient and reads no item row)
+template <int G4, int S, bool SH>
+struct ItemRow {
   float4 x[S];
+  int32_t stamp = 0;
+  __device__ __forceinline__ void load(const Table& Q, int32_t item, int ld, int sub) {
+    if (SH) return;
+    const float* w = Q.W + (int64_t)item * ld + 4 * sub;
 #pragma unroll
-  for (int k = 0; k < S; ++k) x[k] = ld4(w + 4 * G4 * k);
-  const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[item]);
-#pragma unroll
-  for (int k = 0; k < S; ++k) st4(w + 4 * G4 * k, sgd4(scale4(x[k], f), g[k], hp.lr, hp.wd));
-  if (sub == 0) Q.stamp[item] = t;
-}
+    for (int k = 0; k < S; ++k) x[k] = ld4(w + 4 * G4 * k);
+    stamp = Q.stamp[item];
+  }
+};
 
 template <int G4, int S>
 static __device__ __forceinline__ void load_ref(float4 (&row)[S], const float* __restrict__ contrib,
@@ -138,17 +141,23 @@ static __device__ __forceinline__ void acc_ref(float4 (&g)[S], const float4 (&ro
   for (int k = 0; k < S; ++k) g[k] = fma4(sgn, row[k], g[k]);
 }
 
-// finish one item segment: apply (single GPU) or hand the gradient to the exchange (sharded)
+// finish one item segment: apply W = V - lr (g + wd V) to the preloaded row (single GPU) or hand
+// the gradient to the exchange (sharded)
 template <int G4, int S, bool SH>
 static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int slot,
-                                                   const float4 (&g)[S], const Hyper& hp, int ld,
-                                                   int32_t t, int sub, float* __restrict__ grads) {
+                                                   const float4 (&g)[S], const ItemRow<G4, S, SH>& row,
+                                                   const Hyper& hp, int ld, int32_t t, int sub,
+                                                   float* __restrict__ grads) {
   if (SH) {
     float* o = grads + (int64_t)slot * ld + 4 * sub;
 #pragma unroll
     for (int k = 0; k < S; ++k) st4(o + 4 * G4 * k, g[k]);
   } else {
-    apply_item<G4, S>(Q, item, g, hp, ld, t, sub);
+    float* w = Q.W + (int64_t)item * ld + 4 * sub;
+    const float f = decay_pow(hp.log2a, t - 1 - row.stamp);
+#pragma unroll
+    for (int k = 0; k < S; ++k) st4(w + 4 * G4 * k, sgd4(scale4(row.x[k], f), g[k], hp.lr, hp.wd));
+    if (sub == 0) Q.stamp[item] = t;
   }
 }
 
@@ -234,6 +243,8 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     if (bid >= n_long) return;  // uniform over the block
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
+    ItemRow<G4, S, SH> row;
+    if (grp == 0) row.load(Q, item, ld, sub);
     float4 g[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     if (grp == 0) {
 #pragma unroll
       for (int k = 0; k < S; ++k) g[k] = part[0][sub + G4 * k];
-      finish_item<G4, S, SH>(Q, item, r0.w, g, hp, ld, t, sub, grads);
+      finish_item<G4, S, SH>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
     }
     return;
   }
@@ -286,7 +297,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
   if (s >= n_iseg || r1.w) return;  // past the batch's items, or a workgroup-served hot item
   const int32_t item = r0.x;
   const int beg = r0.y, end = r0.z, len = end - beg;
-  float4 g[S], row[S];
+  ItemRow<G4, S, SH> row;
+  row.load(Q, item, ld, sub);
+  float4 g[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (len <= 4) {  // the common case: every ref inline, all rows requested before accumulating
@@ -317,8 +330,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
       }
     }
   }
-  (void)row;
-  finish_item<G4, S, SH>(Q, item, item, g, hp, ld, t, sub, grads);  // SH: item field = slot
+  finish_item<G4, S, SH>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
 }
 
 // Expand BODY for every instantiated float4 geometry (G4_, S_).

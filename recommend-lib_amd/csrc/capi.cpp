@@ -144,10 +144,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   }
   const int64_t ld = g.ld;
   TRY(dalloc(&h->P.W, h->U * ld));
-  TRY(dalloc(&h->P.G, h->U * ld));
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
-  TRY(dalloc(&h->Q.G, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
   TRY(dalloc(&h->d_loss, kLossSlots));
   TRY(dalloc(&h->d_err, 1));
@@ -158,8 +156,6 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     HIPCHK(hipMemsetAsync(p, 0, bytes, h->stream));
     return 0;
   };
-  TRY(memz(h->P.G, sizeof(float) * h->U * ld));
-  TRY(memz(h->Q.G, sizeof(float) * h->I * ld));
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
   TRY(memz(h->d_err, sizeof(int32_t)));
@@ -376,6 +372,22 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   return 0;
 }
 
+// gradient accumulators of the f32-atomic step (B > kMaxSegBatch) and of the Python-orchestrated
+// sharded owner apply, allocated on first use: the segmented steps never touch them, and at the
+// C5 shape (100M x 256 items) they would be another 102 GB of HBM
+int bprmf::ensure_grad(bprmf_handle* h) {
+  const int64_t ld = h->geom.ld;
+  if (!h->P.G) {
+    if (int r = dalloc(&h->P.G, h->U * ld)) return r;
+    if (h->U) HIPCHK(hipMemsetAsync(h->P.G, 0, sizeof(float) * h->U * ld, h->stream));
+  }
+  if (!h->Q.G) {
+    if (int r = dalloc(&h->Q.G, h->I * ld)) return r;
+    if (h->I) HIPCHK(hipMemsetAsync(h->Q.G, 0, sizeof(float) * h->I * ld, h->stream));
+  }
+  return 0;
+}
+
 extern "C" {
 
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
@@ -503,6 +515,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done) {
   const int64_t B = h->cfg.batch_size;
+  if (int r = ensure_grad(h)) return r;
   for (int64_t off = 0; off < n; off += B) {
     const int64_t nb = std::min(B, n - off);
     if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
@@ -910,6 +923,7 @@ int bprmf_dist_item_grads(bprmf_handle* h, int64_t k, float* grads) {
 int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n) {
   if (!h || n < 0 || (n > 0 && (!rows || !grads))) return fail(BPRMF_E_INVALID, "bad arguments");
   if (int r = set_dev(h)) return r;
+  if (int r = ensure_grad(h)) return r;
   ProfScope ps(h, BPRMF_KPROF_OWNER);
   HIPCHK(add_rows(h->geom, h->Q, rows, grads, n, h->d_err, h->stream));
   HIPCHK(apply_rows(h->geom, h->Q, rows, n, h->hp, h->t + 1, h->stream));

@@ -106,6 +106,7 @@ struct ProfScope {
 };
 int ensure_trip(bprmf_handle* h, int64_t n);
 int ensure_seg(bprmf_handle* h, int64_t n_batches);
+int ensure_grad(bprmf_handle* h);
 bool seg_mode(const bprmf_handle* h);
 int check_err_flag(bprmf_handle* h);
 SamplerArgs sampler_args(bprmf_handle* h);

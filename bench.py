@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-kernel event pass")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="steps per library call (0: up to the end of the epoch)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded RCCL path even at one rank (exercises it on one GPU)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "rccl"],

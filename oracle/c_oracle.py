@@ -78,3 +78,66 @@ class DenseTrainer:
 
 def threads():
     return int(lib().oracle_threads())
+
+
+# ---- rating SGD (oracle/mf_cpu.c: util/matrix_factorization.pyx SVD / RSVD) ----------------------
+_mf = None
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+def mf_lib():
+    global _mf
+    if _mf is None:
+        src = os.path.join(HERE, "mf_cpu.c")
+        so = os.path.join(HERE, "liboracle_mf.so")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(so)
+        L.oracle_svd_epochs.argtypes = [ctypes.c_int64, _i32p, _i32p, _f64p, ctypes.c_int,
+                                        ctypes.c_double, ctypes.c_int, _f64p, _f64p, _f64p, _f64p,
+                                        _f64p, _f64p, ctypes.c_int]
+        L.oracle_rsvd_epochs.argtypes = [ctypes.c_int64, _i32p, _i32p, _f64p, ctypes.c_int,
+                                         ctypes.c_double, ctypes.c_int, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_double, _f64p, _f64p, _f64p,
+                                         _f64p, ctypes.c_int]
+        _mf = L
+    return _mf
+
+
+def svd_epochs(u, i, r, P, Q, bu, bi, gm, biased, lr, reg, epochs):
+    """SVD.fit epochs on copies of the tables; returns (P, Q, bu, bi)."""
+    P, Q = np.array(P, np.float64, order="C"), np.array(Q, np.float64, order="C")
+    bu, bi = np.array(bu, np.float64), np.array(bi, np.float64)
+    mf_lib().oracle_svd_epochs(len(u), np.ascontiguousarray(u, np.int32),
+                               np.ascontiguousarray(i, np.int32), np.ascontiguousarray(r, np.float64),
+                               P.shape[1], float(gm), int(biased), np.asarray(lr, np.float64),
+                               np.asarray(reg, np.float64), P, Q, bu, bi, int(epochs))
+    return P, Q, bu, bi
+
+
+def rsvd_epochs(u, i, r, P, Q, bu, bi, gm, version, lr, reg, reg2, epochs):
+    """RSVD.fit epochs (as when verbose) on copies; returns (ui, vj, ci, dj)."""
+    P, Q = np.array(P, np.float64, order="C"), np.array(Q, np.float64, order="C")
+    bu, bi = np.array(bu, np.float64), np.array(bi, np.float64)
+    mf_lib().oracle_rsvd_epochs(len(u), np.ascontiguousarray(u, np.int32),
+                                np.ascontiguousarray(i, np.int32),
+                                np.ascontiguousarray(r, np.float64), P.shape[1], float(gm),
+                                int(version), float(lr), float(reg), float(reg2), P, Q, bu, bi,
+                                int(epochs))
+    return P, Q, bu, bi
+
+
+def mf_levels(u, i, U, I):
+    """The device's schedule (mf_capi.cpp:mf_set_train), restated: level(s) = 1 + the last level
+    of s's user or item among earlier samples; returns (order, offsets) of the stable sort by
+    level.  Running the samples in `order` must equal the sequential loop bit for bit."""
+    lu = np.full(U, -1, np.int64)
+    li = np.full(I, -1, np.int64)
+    lvl = np.empty(len(u), np.int64)
+    for s in range(len(u)):
+        a, b = int(u[s]), int(i[s])
+        lvl[s] = lu[a] = li[b] = max(lu[a], li[b]) + 1
+    order = np.argsort(lvl, kind="stable")
+    L = int(lvl.max()) + 1 if len(lvl) else 0
+    off = np.searchsorted(lvl[order], np.arange(L + 1))
+    return order, off

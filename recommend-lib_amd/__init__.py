@@ -1,6 +1,7 @@
 """recommend-lib_amd — MI355X-native BPR-MF training path (drop-in for the reference's
 BPRMFRecommender / util.data_loader.BPRData / util.metrics BPR parts), plus the NCF path of
-SURVEY.md §8f (NCFRecommender / NCFData).
+SURVEY.md §8f (NCFRecommender / NCFData), and the Cython rating-SGD models SVD / RSVD
+(util/matrix_factorization.pyx).
 
 The directory name is not a Python identifier; import it with
     importlib.import_module("recommend-lib_amd")
@@ -20,8 +21,10 @@ from . import ncf
 from .ncf import NCF, NCFData
 from . import ingest
 from .ingest import load_rate, load_mat
+from . import mf
+from .mf import SVD, RSVD
 
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 
 __all__ = ["BPRMF", "BPR", "BPRData", "NCF", "NCFData", "ShardedBPRMF", "BprmfError", "metrics",
-           "ingest", "load_rate", "load_mat", "build", "LIB_PATH"]
+           "ingest", "load_rate", "load_mat", "SVD", "RSVD", "build", "LIB_PATH"]

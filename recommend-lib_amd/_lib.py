@@ -123,6 +123,14 @@ SIGNATURES = {
     "ncf_active_rows": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
     "ncf_profile": [_P, ctypes.c_int32],
     "ncf_profile_read": [_P, ctypes.POINTER(KProf)],
+    # include/mf.h (mf_config / mf_stats: recommend-lib_amd/mf.py)
+    "mf_create": [_P, ctypes.POINTER(ctypes.c_void_p)],
+    "mf_destroy": [_P],
+    "mf_set_train": [_P, _P, _P, _P, _I64, ctypes.c_double],
+    "mf_set_weights": [_P, _P, _P, _P, _P],
+    "mf_get_weights": [_P, _P, _P, _P, _P],
+    "mf_fit": [_P, ctypes.c_int32, _P],
+    "mf_predict": [_P, _P, _P, _I64, _P],
 }
 
 _lib = None

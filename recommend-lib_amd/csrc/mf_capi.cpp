@@ -71,6 +71,7 @@ int mf_create(const mf_config* cfg, mf_handle** out) {
   *out = nullptr;
   if (cfg->user_num < 0 || cfg->item_num < 0 || cfg->n_factors <= 0)
     return fail(BPRMF_E_INVALID, "need user_num, item_num >= 0 and n_factors > 0");
+  if (cfg->n_factors > 1024) return fail(BPRMF_E_UNSUPPORTED, "n_factors must be <= 1024");
   if (cfg->model != MF_SVD && cfg->model != MF_RSVD) return fail(BPRMF_E_INVALID, "unknown model");
   if (cfg->model == MF_RSVD && cfg->variant != 1 && cfg->variant != 2)
     return fail(BPRMF_E_INVALID, "RSVD version must be 1 or 2");

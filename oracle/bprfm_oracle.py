@@ -3,7 +3,8 @@
 Model BPRFMRecommender.py:28-79, loop :203-227: two fields per side (user feature u, item feature
 U + x), values 1 (util/data_loader.py:574-627); per side
     fm   = 0.5 * ((e_u + e_x)^2 - (e_u^2 + e_x^2))                       (Bi-Interaction, :68-73)
-    y    = BatchNorm1d(fm) in training mode (batch mean, biased variance, eps 1e-5) if batch_norm
+    y    = BatchNorm1d(fm) in training mode (batch mean, biased variance, eps 1e-5) if batch_norm;
+           running mean / variance (unbiased) updated with momentum 0.1, side i then side j
     y    = Dropout(p)(y)                                                   (:51-52)
     pred = sum_k y + b_u + b_x + bias_                                     (:74-79)
 loss = -sum log sigmoid(pred_i - pred_j) (:220), dense gradients, Adagrad over every parameter
@@ -26,6 +27,8 @@ class State:
         self.bn = gamma is not None
         self.gamma = None if gamma is None else np.array(gamma, np.float64)
         self.beta = None if beta is None else np.array(beta, np.float64)
+        k = self.E.shape[1]
+        self.run_mean, self.run_var = np.zeros(k), np.ones(k)
         self.acc = {n: np.full_like(getattr(self, n), init_acc)
                     for n in ("E", "b", "bias_", "gamma", "beta") if getattr(self, n) is not None}
 
@@ -42,6 +45,9 @@ def _side(st, u, xf, mask):
         xhat = (fm - mean) * inv
         y = st.gamma * xhat + st.beta
         cache.update(xhat=xhat, inv=inv)
+        B = fm.shape[0]
+        st.run_mean = 0.9 * st.run_mean + 0.1 * mean
+        st.run_var = 0.9 * st.run_var + 0.1 * (var * B / (B - 1) if B > 1 else var)
     else:
         y = fm
     if mask is not None:
@@ -89,3 +95,14 @@ def step(st, U, u, i, j, lr, masks=None, grads_out=None):
         p = getattr(st, n)
         p -= lr * gr / (np.sqrt(st.acc[n]) + ADAGRAD_EPS)
     return loss
+
+
+def predict(st, u, x):
+    """model.eval() forward of one side (:61-79): BatchNorm on the running statistics."""
+    u, x = np.asarray(u, np.int64), np.asarray(x, np.int64)
+    a, c = st.E[u], st.E[x]
+    s = a + c
+    fm = 0.5 * (s * s - (a * a + c * c))
+    if st.bn:
+        fm = (fm - st.run_mean) / np.sqrt(st.run_var + BN_EPS) * st.gamma + st.beta
+    return fm.sum(1) + st.b[u] + st.b[x] + st.bias_[0]

@@ -1,4 +1,4 @@
-"""ctypes binding of libbprmf_amd.so (include/bprmf.h, include/ncf.h).
+"""ctypes binding of libbprmf_amd.so (include/bprmf.h, ncf.h, mf.h, bprfm.h).
 
 The HIP library is the only compute path: if it is missing or no GPU is visible, handle creation
 raises — there is no CPU fallback in the product.
@@ -131,7 +131,17 @@ SIGNATURES = {
     "mf_get_weights": [_P, _P, _P, _P, _P],
     "mf_fit": [_P, ctypes.c_int32, _P],
     "mf_predict": [_P, _P, _P, _I64, _P],
+    # include/bprfm.h (bprfm_config / bprfm_stats: recommend-lib_amd/bprfm.py)
+    "bprfm_create": [_P, ctypes.POINTER(ctypes.c_void_p)],
+    "bprfm_destroy": [_P],
+    "bprfm_set_weights": [_P, _P, _P, _P, _P, _P, _P, _P],
+    "bprfm_get_weights": [_P, _P, _P, _P, _P, _P, _P, _P],
+    "bprfm_train": [_P, _P, _P, _P, _I64, ctypes.c_int32, _P],
+    "bprfm_dropout_mask": [_P, ctypes.c_int32, _P],
+    "bprfm_predict": [_P, _P, _P, _I64, _P],
+    "bprfm_steps": [_P],
 }
+RESTYPES = {"bprmf_last_error": ctypes.c_char_p, "bprfm_steps": ctypes.c_int64}
 
 _lib = None
 
@@ -154,7 +164,7 @@ def load():
     for name, args in SIGNATURES.items():
         f = getattr(L, name)
         f.argtypes = args
-        f.restype = ctypes.c_char_p if name == "bprmf_last_error" else ctypes.c_int
+        f.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = L
     return L
 

@@ -57,3 +57,6 @@ def test_oracle_matches_reference_steps(name):
     if st.bn:
         np.testing.assert_allclose(st.gamma, c["final_FM_layers_0_weight"], rtol=0, atol=PARAM_ATOL)
         np.testing.assert_allclose(st.beta, c["final_FM_layers_0_bias"], rtol=0, atol=PARAM_ATOL)
+        np.testing.assert_allclose(st.run_mean, c["final_FM_layers_0_running_mean"], rtol=1e-3,
+                                   atol=1e-7)
+        np.testing.assert_allclose(st.run_var, c["final_FM_layers_0_running_var"], rtol=1e-3)

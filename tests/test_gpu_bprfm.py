@@ -1,0 +1,195 @@
+"""GPU: the BPR-FM path (include/bprfm.h, bprfm.hip) through the BPRFM drop-in, against the
+reference module's own steps (tests/golden/bprfm_steps.npz, made by running BPRFMRecommender.BPRFM)
+and the float64 oracle (oracle/bprfm_oracle.py).
+
+Tolerances: float32 on both sides with different summation orders (the device scatters embedding
+gradients with float atomics), then Adagrad, whose first updates are ~lr * g / |g|: the parameter
+tolerance is the one the oracle itself needs against the reference (PARAM_ATOL,
+tests/test_bprfm_oracle.py).  Losses agree to LOSS_RTOL.  Dropout is replayed exactly: the
+device's keep-scales of a step come back from bprfm_dropout_mask and go into the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import bprfm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+F = np.load(os.path.join(GOLDEN, "bprfm_steps.npz"))
+CASES = [str(c) for c in F["cases"]]
+PARAM_ATOL = 5e-4
+LOSS_RTOL = 1e-4
+PRED_ATOL = 1e-5
+# Large tables over several steps: a gradient element that nearly cancels (a heavy user's many
+# terms, a hot item's +/- references) sits where Adagrad's g / sqrt(1e-8 + g^2) is steepest, so
+# float32 sum-order noise there moves the update by up to ~1e-3 (6 of 512 000 elements in the
+# 3-step k = 64 case).  Those elements may exceed PARAM_ATOL, no more than OUTLIER_FRAC of them and
+# none by more than OUTLIER_CAP.
+OUTLIER_FRAC = 1e-4
+OUTLIER_CAP = 4e-3
+
+
+def case(name):
+    return {k[len(name) + 1:]: F[k] for k in F.files if k.startswith(name + "_")}
+
+
+def init_sd(c):
+    sd = {"embeddings.weight": c["init_embeddings_weight"], "biases.weight": c["init_biases_weight"],
+          "bias_": c["init_bias_"]}
+    if int(c["bn"]):
+        for n in ("weight", "bias", "running_mean", "running_var"):
+            sd["FM_layers.0." + n] = c["init_FM_layers_0_" + n]
+    return sd
+
+
+def model_for(rl, c, p=0.0, max_batch=None):
+    U, I, k = int(c["U"]), int(c["I"]), int(c["k"])
+    m = rl.BPRFM(U + I, k, bool(c["bn"]), [p, 0.0], lr=float(c["lr"]),
+                 max_batch=max_batch or int(c["B"]), seed=7)
+    m.load_state_dict(init_sd(c))
+    return m
+
+
+def check_params(sd, E, b, bias_, gamma=None, beta=None, rm=None, rv=None, atol=PARAM_ATOL,
+                 outliers=False):
+    if outliers:
+        d = np.abs(sd["embeddings.weight"] - E)
+        assert (d > atol).mean() <= OUTLIER_FRAC, (d > atol).sum()
+        assert d.max() <= OUTLIER_CAP, d.max()
+    else:
+        np.testing.assert_allclose(sd["embeddings.weight"], E, rtol=0, atol=atol)
+    np.testing.assert_allclose(sd["biases.weight"].reshape(-1), np.reshape(b, -1), rtol=0, atol=atol)
+    np.testing.assert_allclose(sd["bias_"], np.reshape(bias_, -1), rtol=0, atol=0)
+    if gamma is not None:
+        np.testing.assert_allclose(sd["FM_layers.0.weight"], gamma, rtol=0, atol=atol)
+        np.testing.assert_allclose(sd["FM_layers.0.bias"], beta, rtol=0, atol=atol)
+        np.testing.assert_allclose(sd["FM_layers.0.running_mean"], rm, rtol=1e-3, atol=1e-7)
+        np.testing.assert_allclose(sd["FM_layers.0.running_var"], rv, rtol=1e-3)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_steps_match_reference_module(rl, name):
+    c = case(name)
+    m = model_for(rl, c)
+    U = int(c["U"])
+    for s in range(int(c["steps"])):
+        t = c["triplets"][s]
+        loss = m.train_triplets(t[0], U + t[1], U + t[2], batch_size=int(c["B"]))
+        assert loss == pytest.approx(float(c["loss"][s]), rel=LOSS_RTOL)
+    assert m.steps == int(c["steps"])
+    sd = m.state_dict()
+    bn = bool(c["bn"])
+    check_params(sd, c["final_embeddings_weight"], c["final_biases_weight"], c["final_bias_"],
+                 *(c["final_FM_layers_0_" + n] for n in ("weight", "bias", "running_mean",
+                                                         "running_var")) if bn else ())
+    if bn:
+        assert int(sd["FM_layers.0.num_batches_tracked"]) == int(c["final_FM_layers_0_num_batches_tracked"])
+
+
+def oracle_state(c):
+    bn = bool(c["bn"])
+    return O.State(c["init_embeddings_weight"], c["init_biases_weight"], c["init_bias_"],
+                   c["init_FM_layers_0_weight"] if bn else None,
+                   c["init_FM_layers_0_bias"] if bn else None)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("p", [0.5, 0.2])
+def test_dropout_steps_match_oracle_with_replayed_masks(rl, name, p):
+    c = case(name)
+    m = model_for(rl, c, p=p)
+    st = oracle_state(c)
+    U, B, k = int(c["U"]), int(c["B"]), int(c["k"])
+    for s in range(int(c["steps"])):
+        t = c["triplets"][s]
+        masks = m.dropout_mask(B)
+        assert masks.shape == (2, B, k)
+        keep = masks != 0
+        np.testing.assert_allclose(masks[keep], 1.0 / (1.0 - p), rtol=1e-6)
+        want = O.step(st, U, t[0], t[1], t[2], float(c["lr"]), masks=masks.astype(np.float64))
+        got = m.train_triplets(t[0], U + t[1], U + t[2], batch_size=B)
+        assert got == pytest.approx(want, rel=LOSS_RTOL)
+    sd = m.state_dict()
+    check_params(sd, st.E, st.b, st.bias_,
+                 *((st.gamma, st.beta, st.run_mean, st.run_var) if st.bn else ()))
+
+
+def test_dropout_keep_rate_and_fresh_draws_per_step(rl):
+    c = case("bn16")
+    m = model_for(rl, c, p=0.5, max_batch=4096)
+    a = m.dropout_mask(4096)
+    assert abs((a != 0).mean() - 0.5) < 0.01
+    assert set(np.unique(a).tolist()) == {0.0, 2.0}
+    U = int(c["U"])
+    t = c["triplets"][0]
+    m.train_triplets(t[0], U + t[1], U + t[2], batch_size=int(c["B"]))
+    b = m.dropout_mask(4096)
+    assert (a != b).mean() > 0.4  # a new step, new draws
+    assert np.array_equal(b, m.dropout_mask(4096))  # ...and deterministic for a step
+
+
+@pytest.mark.parametrize("bn", [True, False])
+def test_ragged_batches_and_larger_table(rl, bn):
+    """k = 64 (the reference default), 3000 users / 5000 items, 10 000 triplets in batches of
+    4096 (the last one ragged): every step against the oracle."""
+    g = np.random.default_rng(5)
+    U, I, k, B, n = 3000, 5000, 64, 4096, 10000
+    E = (0.01 * g.standard_normal((U + I, k))).astype(np.float32)
+    m = rl.BPRFM(U + I, k, bn, [0.0], lr=0.05, max_batch=B)
+    m.load_state_dict({"embeddings.weight": E})
+    st = O.State(E, np.zeros(U + I), np.zeros(1), np.ones(k) if bn else None,
+                 np.zeros(k) if bn else None)
+    u = g.integers(0, U, n)
+    u[:300] = 17  # a heavy user
+    i = U + g.integers(0, I, n)
+    j = U + g.integers(0, I, n)
+    i[100:400] = U + 4  # a hot item
+    want = 0.0
+    for beg in range(0, n, B):
+        sl = slice(beg, beg + B)
+        want += O.step(st, 0, u[sl], i[sl], j[sl], 0.05)
+    got = m.train_triplets(u, i, j, batch_size=B)
+    assert m.last_stats["steps"] == 3 and m.last_stats["triplets"] == n
+    assert got == pytest.approx(want, rel=LOSS_RTOL)
+    check_params(m.state_dict(), st.E, st.b, st.bias_,
+                 *((st.gamma, st.beta, st.run_mean, st.run_var) if bn else ()), outliers=True)
+    # model.eval() forward (running statistics, no dropout) on the device's own parameters
+    sd = m.state_dict()
+    ev = O.State(sd["embeddings.weight"], sd["biases.weight"], sd["bias_"],
+                 sd["FM_layers.0.weight"] if bn else None, sd["FM_layers.0.bias"] if bn else None)
+    if bn:
+        ev.run_mean, ev.run_var = sd["FM_layers.0.running_mean"], sd["FM_layers.0.running_var"]
+    q = np.stack([g.integers(0, U, 500), U + g.integers(0, I, 500)], 1)
+    pi, pj = m(q, np.ones((500, 2)), q[::-1], np.ones((500, 2)))
+    np.testing.assert_allclose(pi, O.predict(ev, q[:, 0], q[:, 1]), rtol=1e-4, atol=PRED_ATOL)
+    np.testing.assert_allclose(pj, O.predict(ev, q[::-1, 0], q[::-1, 1]), rtol=1e-4, atol=PRED_ATOL)
+
+
+def test_bad_inputs_fail_loudly(rl):
+    m = rl.BPRFM(100, 8, True, [0.0], max_batch=64)
+    with pytest.raises(ValueError):
+        m.train_triplets([0], [5], [100])  # feature 100 of 100
+    with pytest.raises(ValueError):
+        m.train_triplets([0, 1], [5, 6], [7, 8], batch_size=65)
+    with pytest.raises(ValueError):
+        m.predict(np.array([[0, -1]]))
+    with pytest.raises(ValueError):
+        m.predict(np.array([[0, 1]]), np.array([[1, 0.5]]))
+    assert m.train_triplets([], [], []) == 0.0 and m.steps == 0
+    with pytest.raises((ValueError, rl.BprmfError)):
+        rl.BPRFM(100, 65, True, [0.0])
+    with pytest.raises(ValueError):
+        rl.BPRFM(100, 8, True, [1.0])
+
+
+def test_fit_epoch_over_bprfm_data(rl):
+    import pandas as pd
+    df = pd.DataFrame({"user": [0, 0, 1, 2, 2, 2], "item": [0, 1, 1, 2, 3, 0]})
+    d = rl.BPRFMData(df, {"user": 0, "item": 3}, {x: x for x in range(7)}, 4, num_ng=3,
+                     is_training=True)
+    m = rl.BPRFM(7, 8, True, [0.5], max_batch=8)
+    np.random.seed(3)
+    loss = m.fit_epoch(d, batch_size=8)
+    assert np.isfinite(loss) and m.steps == 3 and m.last_stats["triplets"] == 18

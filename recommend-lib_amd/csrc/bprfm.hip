@@ -10,16 +10,19 @@
 //
 // Layout: G lanes per triplet (G = next_pow2(k) <= 64), one factor per lane; TPB = 256 / G
 // triplets per workgroup.  Kernels of one step (BN on):
-//   k_fm_fwd    fm rows of both sides -> X; per-workgroup sums of fm and fm^2 (double)
-//   k_fm_stats  batch mean / 1/sqrt(var + eps) per side (fixed-order sum of the partials), and the
-//               running statistics (momentum 0.1, unbiased variance; i side, then j side)
-//   k_fm_mid    y, dropout, pred, loss, c = sigmoid(-(pred_i - pred_j)); per-workgroup sums of
-//               gy and gy * xhat per side (the BatchNorm backward's batch terms)
+//   k_fm_fwd    fm rows of both sides -> X; per-workgroup sums of fm and fm^2 (double; at most
+//               512 workgroups striding over the batch)
+//   k_fm_stats  batch mean / 1/sqrt(var + eps) per side (fixed-order sum of the partials, one
+//               workgroup per 4 factors), and the running statistics (momentum 0.1, unbiased variance; i side,
+//               then j side)
+//   k_fm_mid    y, dropout, pred, c = sigmoid(-(pred_i - pred_j)); per-workgroup sums of gy and
+//               gy * xhat per side (the BatchNorm backward's batch terms)
 //   k_fm_stats2 fixed-order sums of those; dgamma, dbeta
 //   k_fm_back   BatchNorm and Bi-Interaction backward, gradient rows added into G (f32 atomics)
-//   k_fm_apply  Adagrad on every touched row (claimed once per step by its stamp), G re-zeroed;
-//               gamma / beta
-// BN off: k_fm_fwd computes pred and the backward itself, then k_fm_apply.
+//   k_fm_apply  Adagrad on every touched row (small tables: a sweep over the rows the backward
+//               stamped; else claimed once per step by swapping its stamp), G re-zeroed;
+//               gamma / beta; the step's loss (workgroup 0)
+// BN off: k_fm_plain computes pred and the backward itself, then k_fm_apply.
 // The user feature's bias enters pred_i and pred_j with one value, so its gradient is exactly
 // zero (the reference's autograd cancels it exactly too): nothing is added to it, and Adagrad on a
 // zero gradient leaves the value exactly; bias_ likewise is never touched.
@@ -84,8 +87,9 @@ static __device__ __forceinline__ void add_row(float* __restrict__ G, int64_t ro
   atomicAdd(G + row * ld + e, v);
 }
 
+// BN off: the whole step's forward and backward, one lane group per triplet
 template <int G>
-__global__ __launch_bounds__(kT) void k_fm_fwd(Args a) {
+__global__ __launch_bounds__(kT) void k_fm_plain(Args a) {
   constexpr int TPB = kT / G;
   const int lane = threadIdx.x & (G - 1);
   const int t = blockIdx.x * TPB + threadIdx.x / G;
@@ -105,17 +109,6 @@ __global__ __launch_bounds__(kT) void k_fm_fwd(Args a) {
   const float si = eu + ei, sj = eu + ej;
   const float fi = 0.5f * (si * si - (eu * eu + ei * ei));
   const float fj = 0.5f * (sj * sj - (eu * eu + ej * ej));
-  if (a.bn) {
-    if (t < a.B) {
-      a.X[(int64_t)t * a.ld + lane] = fi;
-      a.X[((int64_t)a.B + t) * a.ld + lane] = fj;
-    }
-    double v[4] = {act ? (double)fi : 0.0, act ? (double)fi * fi : 0.0, act ? (double)fj : 0.0,
-                   act ? (double)fj * fj : 0.0};
-    block_sums<G, 4>(v, a.part + (int64_t)blockIdx.x * 4 * a.ld, a.ld);
-    return;
-  }
-  // no BatchNorm: the whole step here
   const float mi = act ? drop_scale(a, t, 0, lane) : 0.f, mj = act ? drop_scale(a, t, 1, lane) : 0.f;
   const float yi = gsum<G>(act ? fi * mi : 0.f), yj = gsum<G>(act ? fj * mj : 0.f);
   float c = 0.f;
@@ -129,6 +122,7 @@ __global__ __launch_bounds__(kT) void k_fm_fwd(Args a) {
       a.cbuf[t] = d;
       add_row(a.Gb, xi, 1, 0, -c);
       add_row(a.Gb, xj, 1, 0, c);
+      if (a.sweep) a.stamp[u] = a.stamp[xi] = a.stamp[xj] = a.step + 1;
     }
   }
   if (act) {
@@ -139,82 +133,138 @@ __global__ __launch_bounds__(kT) void k_fm_fwd(Args a) {
   }
 }
 
-// batch statistics of both sides + running statistics (one workgroup of ld threads x 2 sides)
-__global__ void k_fm_stats(Args a, int nblk) {
-  const int e = threadIdx.x % a.ld, side = threadIdx.x / a.ld;
-  if (side >= 2 || e >= a.k) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int q = 0; q < nblk; ++q) {
-    s1 += a.part[((int64_t)q * 4 + 2 * side) * a.ld + e];
-    s2 += a.part[((int64_t)q * 4 + 2 * side + 1) * a.ld + e];
-  }
-  const double mean = s1 / a.B;
-  const double var = fmax(s2 / a.B - mean * mean, 0.0);  // biased (training normalisation)
-  a.stats[(2 * side) * a.ld + e] = (float)mean;
-  a.stats[(2 * side + 1) * a.ld + e] = (float)(1.0 / sqrt(var + 1e-5));
-  // running statistics, i side then j side (the forward calls FM_layers twice, :56-57)
-  if (side == 0) {
-    double rm = a.run[e], rv = a.run[a.ld + e];
-    for (int sd = 0; sd < 2; ++sd) {
-      double t1 = 0.0, t2 = 0.0;
-      for (int q = 0; q < nblk; ++q) {
-        t1 += a.part[((int64_t)q * 4 + 2 * sd) * a.ld + e];
-        t2 += a.part[((int64_t)q * 4 + 2 * sd + 1) * a.ld + e];
-      }
-      const double mu = t1 / a.B, vb = fmax(t2 / a.B - mu * mu, 0.0);
-      const double vu = a.B > 1 ? vb * a.B / (a.B - 1) : vb;
-      rm = 0.9 * rm + 0.1 * mu;
-      rv = 0.9 * rv + 0.1 * vu;
+// BN on, pass 1: fm rows of both sides -> X; per-workgroup sums of fm and fm^2 (double).  nb
+// workgroups stride over the batch, so the statistics kernel sums few partials.
+template <int G>
+__global__ __launch_bounds__(kT) void k_fm_fwd(Args a, int nb) {
+  constexpr int TPB = kT / G;
+  const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (lane < a.k) {
+    for (int t = blockIdx.x * TPB + slot; t < a.B; t += nb * TPB) {
+      const int64_t u = a.u[t], xi = a.i[t], xj = a.j[t];
+      const float eu = a.E[u * a.ld + lane], ei = a.E[xi * a.ld + lane], ej = a.E[xj * a.ld + lane];
+      const float si = eu + ei, sj = eu + ej;
+      const float fi = 0.5f * (si * si - (eu * eu + ei * ei));
+      const float fj = 0.5f * (sj * sj - (eu * eu + ej * ej));
+      a.X[(int64_t)t * a.ld + lane] = fi;
+      a.X[((int64_t)a.B + t) * a.ld + lane] = fj;
+      v[0] += fi;
+      v[1] += (double)fi * fi;
+      v[2] += fj;
+      v[3] += (double)fj * fj;
     }
-    a.run[e] = (float)rm;
-    a.run[a.ld + e] = (float)rv;
   }
+  block_sums<G, 4>(v, a.part + (int64_t)blockIdx.x * 4 * a.ld, a.ld);
 }
 
-template <int G>
-__global__ __launch_bounds__(kT) void k_fm_mid(Args a) {
-  constexpr int TPB = kT / G;
-  const int lane = threadIdx.x & (G - 1);
-  const int t = blockIdx.x * TPB + threadIdx.x / G;
-  const bool act = t < a.B && lane < a.k;
-  float xh[2] = {0.f, 0.f}, m[2] = {0.f, 0.f}, yv[2] = {0.f, 0.f};
-  const float ga = act ? a.gamma[lane] : 0.f, be = act ? a.beta[lane] : 0.f;
+// fixed-order sums of the 4 per-workgroup partial rows over nblk (<= kMaxParts) workgroups.
+// Workgroup w of ceil(ld / 4) sums factors 4w..4w+3: thread = (pair p = (q, e) of 16, chunk c of
+// 64); chunk c holds partials c, c + 64, ... (8 loads issued together), then an LDS tree over the
+// chunks.  sums[q][e - 4w] for e < k on return.
+constexpr int kRT = 1024;
+constexpr int kMaxParts = 512;
+static __device__ void reduce_parts(const Args& a, int nblk, double (*sums)[4]) {
+  __shared__ double red[64][16];
+  const int p = threadIdx.x & 15, c = threadIdx.x >> 4;
+  const int q = p >> 2, e = blockIdx.x * 4 + (p & 3);
+  double x[kMaxParts / 64];
 #pragma unroll
-  for (int sd = 0; sd < 2; ++sd) {
-    if (act) {
-      const float x = a.X[((int64_t)sd * a.B + t) * a.ld + lane];
-      xh[sd] = (x - a.stats[(2 * sd) * a.ld + lane]) * a.stats[(2 * sd + 1) * a.ld + lane];
-      m[sd] = drop_scale(a, t, sd, lane);
-      yv[sd] = (ga * xh[sd] + be) * m[sd];
+  for (int m = 0; m < kMaxParts / 64; ++m) {
+    const int b = c + 64 * m;
+    x[m] = (b < nblk && e < a.ld) ? a.part[((int64_t)b * 4 + q) * a.ld + e] : 0.0;
+  }
+  double v = 0.0;
+#pragma unroll
+  for (int m = 0; m < kMaxParts / 64; ++m) v += x[m];
+  red[c][p] = v;
+  __syncthreads();
+#pragma unroll
+  for (int h = 32; h >= 1; h >>= 1) {
+    if (c < h) red[c][p] += red[c + h][p];
+    __syncthreads();
+  }
+  if (threadIdx.x < 16) sums[q][p & 3] = red[0][p];
+  __syncthreads();
+}
+
+// batch statistics of both sides + running statistics
+__global__ __launch_bounds__(kRT) void k_fm_stats(Args a, int nblk) {
+  __shared__ double sums[4][4];
+  reduce_parts(a, nblk, sums);
+  const int el = threadIdx.x, e = blockIdx.x * 4 + el;
+  if (el >= 4 || e >= a.k) return;
+  double rm = a.run[e], rv = a.run[a.ld + e];
+  for (int side = 0; side < 2; ++side) {
+    const double mean = sums[2 * side][el] / a.B;
+    const double var = fmax(sums[2 * side + 1][el] / a.B - mean * mean, 0.0);  // biased
+    a.stats[(2 * side) * a.ld + e] = (float)mean;
+    a.stats[(2 * side + 1) * a.ld + e] = (float)(1.0 / sqrt(var + 1e-5));
+    // running statistics, i side then j side (the forward calls FM_layers twice, :56-57)
+    const double vu = a.B > 1 ? var * a.B / (a.B - 1) : var;
+    rm = 0.9 * rm + 0.1 * mean;
+    rv = 0.9 * rv + 0.1 * vu;
+  }
+  a.run[e] = (float)rm;
+  a.run[a.ld + e] = (float)rv;
+}
+
+// BN on, pass 2: y, dropout, pred, d = pred_i - pred_j -> cbuf, c = sigmoid(-d); per-workgroup
+// sums of gy and gy * xhat per side (the BatchNorm backward's batch terms)
+template <int G>
+__global__ __launch_bounds__(kT) void k_fm_mid(Args a, int nb) {
+  constexpr int TPB = kT / G;
+  const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
+  const bool act = lane < a.k;
+  float ga = 0.f, be = 0.f, mu[2] = {0.f, 0.f}, inv[2] = {0.f, 0.f};
+  if (act) {
+    ga = a.gamma[lane];
+    be = a.beta[lane];
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      mu[sd] = a.stats[(2 * sd) * a.ld + lane];
+      inv[sd] = a.stats[(2 * sd + 1) * a.ld + lane];
     }
   }
-  const float yi = gsum<G>(yv[0]), yj = gsum<G>(yv[1]);
-  float c = 0.f;
-  if (t < a.B) {
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = blockIdx.x * TPB + slot; t < a.B; t += nb * TPB) {  // uniform per lane group
     const int64_t u = a.u[t], xi = a.i[t], xj = a.j[t];
+    float xh[2] = {0.f, 0.f}, m[2] = {0.f, 0.f}, yv[2] = {0.f, 0.f};
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      if (act) {
+        const float x = a.X[((int64_t)sd * a.B + t) * a.ld + lane];
+        xh[sd] = (x - mu[sd]) * inv[sd];
+        m[sd] = drop_scale(a, t, sd, lane);
+        yv[sd] = (ga * xh[sd] + be) * m[sd];
+      }
+    }
+    const float yi = gsum<G>(yv[0]), yj = gsum<G>(yv[1]);
     const float bu = a.b[u];
     const float pi = (yi + (bu + a.b[xi])) + *a.bias_;
     const float pj = (yj + (bu + a.b[xj])) + *a.bias_;
     const float d = pi - pj;
-    c = 1.0f / (1.0f + expf(d));
+    const float c = 1.0f / (1.0f + expf(d));
     if (lane == 0) a.cbuf[t] = d;
+    // dL/dy = -c (i side), +c (j side), through the dropout mask
+    const float gi = act ? -c * m[0] : 0.f, gj = act ? c * m[1] : 0.f;
+    v[0] += gi;
+    v[1] += (double)gi * xh[0];
+    v[2] += gj;
+    v[3] += (double)gj * xh[1];
   }
-  // dL/dy = -c (i side), +c (j side), through the dropout mask
-  const float gi = act ? -c * m[0] : 0.f, gj = act ? c * m[1] : 0.f;
-  double v[4] = {gi, (double)gi * xh[0], gj, (double)gj * xh[1]};
   block_sums<G, 4>(v, a.part + (int64_t)blockIdx.x * 4 * a.ld, a.ld);
 }
 
 // sums of gy and gy * xhat per side; dgamma / dbeta (the module serves both sides)
-__global__ void k_fm_stats2(Args a, int nblk) {
-  const int e = threadIdx.x;
-  if (e >= a.k) return;
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int q = 0; q < nblk; ++q)
-    for (int w = 0; w < 4; ++w) s[w] += a.part[((int64_t)q * 4 + w) * a.ld + e];
-  for (int w = 0; w < 4; ++w) a.stats2[w * a.ld + e] = (float)s[w];
-  a.gbeta[e] = (float)(s[0] + s[2]);
-  a.ggamma[e] = (float)(s[1] + s[3]);
+__global__ __launch_bounds__(kRT) void k_fm_stats2(Args a, int nblk) {
+  __shared__ double sums[4][4];
+  reduce_parts(a, nblk, sums);
+  const int el = threadIdx.x, e = blockIdx.x * 4 + el;
+  if (el >= 4 || e >= a.k) return;
+  for (int w = 0; w < 4; ++w) a.stats2[w * a.ld + e] = (float)sums[w][el];
+  a.gbeta[e] = (float)(sums[0][el] + sums[2][el]);
+  a.ggamma[e] = (float)(sums[1][el] + sums[3][el]);
 }
 
 template <int G>
@@ -247,31 +297,39 @@ __global__ __launch_bounds__(kT) void k_fm_back(Args a) {
   if (lane == 0) {
     add_row(a.Gb, xi, 1, 0, -c);
     add_row(a.Gb, xj, 1, 0, c);
+    if (a.sweep) a.stamp[u] = a.stamp[xi] = a.stamp[xj] = a.step + 1;
   }
 }
 
-// Adagrad (torch _single_tensor_adagrad: acc += g^2; p += -lr * (g / (sqrt(acc) + 1e-10))) on each
-// touched row, once
-template <int G>
-__global__ __launch_bounds__(kT) void k_fm_apply(Args a) {
-  constexpr int TPB = kT / G;
-  const int lane = threadIdx.x & (G - 1);
-  const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x / G;  // reference: 3 per triplet
-  if (blockIdx.x == 0 && a.bn && threadIdx.x < a.k) {  // gamma, beta
-    const int e = threadIdx.x;
-    const float g1 = a.ggamma[e], g2 = a.gbeta[e];
-    a.acc_gamma[e] += g1 * g1;
-    a.gamma[e] += -a.lr * (g1 / (sqrtf(a.acc_gamma[e]) + 1e-10f));
-    a.acc_beta[e] += g2 * g2;
-    a.beta[e] += -a.lr * (g2 / (sqrtf(a.acc_beta[e]) + 1e-10f));
+// loss of the step from the stored d = pred_i - pred_j: sum of log(1 + e^-d), fixed order (one
+// workgroup; each thread issues its 16 loads of a round together)
+static __device__ void loss_sum(const Args& a) {
+  constexpr int R = 16;
+  __shared__ double red[kT];
+  double s = 0.0;
+  for (int t0 = 0; t0 < a.B; t0 += kT * R) {
+    float d[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const int t = t0 + m * kT + threadIdx.x;
+      d[m] = t < a.B ? a.cbuf[t] : INFINITY;  // softplus(-inf) = 0
+    }
+#pragma unroll
+    for (int m = 0; m < R; ++m) s += (double)softplus(-d[m]);
   }
-  if (r >= 3LL * a.B) return;
-  const int64_t t = r / 3, w = r % 3;
-  const int64_t row = w == 0 ? a.u[t] : w == 1 ? a.i[t] : a.j[t];
-  int32_t old = 0;
-  if (lane == 0) old = atomicExch(a.stamp + row, a.step + 1);
-  old = __shfl(old, (threadIdx.x & 63) & ~(G - 1));
-  if (old == a.step + 1) return;  // another reference of this row applies it
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = kT / 2; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.loss[0] += red[0];
+}
+
+// Adagrad (torch _single_tensor_adagrad: acc += g^2; p += -lr * (g / (sqrt(acc) + 1e-10))) on one
+// row and its bias, G re-zeroed
+template <int G>
+static __device__ __forceinline__ void adagrad_row(const Args& a, int64_t row, int lane) {
   if (lane < a.k) {
     const int64_t o = row * a.ld + lane;
     const float g = a.GE[o];
@@ -289,18 +347,37 @@ __global__ __launch_bounds__(kT) void k_fm_apply(Args a) {
   }
 }
 
-// loss of the step from the stored d = pred_i - pred_j: sum of log(1 + e^-d), fixed order
-__global__ void k_fm_loss(Args a) {
-  __shared__ double red[kT];
-  double s = 0.0;
-  for (int t = threadIdx.x; t < a.B; t += kT) s += (double)softplus(-a.cbuf[t]);
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int h = kT / 2; h >= 1; h >>= 1) {
-    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-    __syncthreads();
+// every touched row once.  sweep: one lane group per feature row, applied if the backward stamped
+// it this step (small tables: no atomics); otherwise one lane group per row reference (3 per
+// triplet), the first to swap its stamp applies it.  Workgroup 0 also does gamma / beta and the
+// loss.
+template <int G>
+__global__ __launch_bounds__(kT) void k_fm_apply(Args a) {
+  constexpr int TPB = kT / G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x / G;
+  if (blockIdx.x == 0) loss_sum(a);  // (block-uniform: every thread of block 0 reaches it)
+  if (blockIdx.x == 0 && a.bn && threadIdx.x < a.k) {  // gamma, beta
+    const int e = threadIdx.x;
+    const float g1 = a.ggamma[e], g2 = a.gbeta[e];
+    a.acc_gamma[e] += g1 * g1;
+    a.gamma[e] += -a.lr * (g1 / (sqrtf(a.acc_gamma[e]) + 1e-10f));
+    a.acc_beta[e] += g2 * g2;
+    a.beta[e] += -a.lr * (g2 / (sqrtf(a.acc_beta[e]) + 1e-10f));
   }
-  if (threadIdx.x == 0) a.loss[0] += red[0];
+  if (a.sweep) {
+    if (r >= a.F || a.stamp[r] != a.step + 1) return;
+    adagrad_row<G>(a, r, lane);
+    return;
+  }
+  if (r >= 3LL * a.B) return;
+  const int64_t t = r / 3, w = r % 3;
+  const int64_t row = w == 0 ? a.u[t] : w == 1 ? a.i[t] : a.j[t];
+  int32_t old = 0;
+  if (lane == 0) old = atomicExch(a.stamp + row, a.step + 1);
+  old = __shfl(old, (threadIdx.x & 63) & ~(G - 1));
+  if (old == a.step + 1) return;  // another reference of this row applies it
+  adagrad_row<G>(a, row, lane);
 }
 
 // pred for n (u, x) pairs in eval mode (BatchNorm on the running statistics, no dropout)
@@ -372,22 +449,31 @@ int lanes_for(int k) {
   return g;
 }
 
-int64_t part_blocks(int k, int B) { return ((int64_t)B + kT / lanes_for(k) - 1) / (kT / lanes_for(k)); }
+// workgroups of the BatchNorm passes: the batch's lane groups, at most kMaxParts workgroups
+int64_t part_blocks(int k, int B) {
+  const int64_t tpb = kT / lanes_for(k);
+  return std::max<int64_t>(1, std::min<int64_t>(((int64_t)B + tpb - 1) / tpb, kMaxParts));
+}
 
 hipError_t step(const Args& a, hipStream_t s) {
   if (a.k <= 0 || a.k > 64 || a.B <= 0) return hipErrorInvalidValue;
-  const int nblk = (int)part_blocks(a.k, a.B);
-  const unsigned ablk = (unsigned)((3LL * a.B + kT / lanes_for(a.k) - 1) / (kT / lanes_for(a.k)));
+  const int64_t tpb = kT / lanes_for(a.k);
+  const unsigned nt = (unsigned)((a.B + tpb - 1) / tpb);      // one lane group per triplet
+  const int64_t napply = a.sweep ? a.F : 3LL * a.B;  // feature rows, or row references
+  const unsigned na = (unsigned)((napply + tpb - 1) / tpb);
+  const int nb = (int)part_blocks(a.k, a.B);
+  const unsigned nr = (unsigned)((a.ld + 3) / 4);  // reduce workgroups: 4 factors each
   FM_G(a.k, ({
-    k_fm_fwd<G_><<<nblk, kT, 0, s>>>(a);
     if (a.bn) {
-      k_fm_stats<<<1, 2 * a.ld, 0, s>>>(a, nblk);
-      k_fm_mid<G_><<<nblk, kT, 0, s>>>(a);
-      k_fm_stats2<<<1, a.ld, 0, s>>>(a, nblk);
-      k_fm_back<G_><<<nblk, kT, 0, s>>>(a);
+      k_fm_fwd<G_><<<nb, kT, 0, s>>>(a, nb);
+      k_fm_stats<<<nr, kRT, 0, s>>>(a, nb);
+      k_fm_mid<G_><<<nb, kT, 0, s>>>(a, nb);
+      k_fm_stats2<<<nr, kRT, 0, s>>>(a, nb);
+      k_fm_back<G_><<<nt, kT, 0, s>>>(a);
+    } else {
+      k_fm_plain<G_><<<nt, kT, 0, s>>>(a);
     }
-    k_fm_loss<<<1, kT, 0, s>>>(a);
-    k_fm_apply<G_><<<ablk, kT, 0, s>>>(a);
+    k_fm_apply<G_><<<na, kT, 0, s>>>(a);
   }));
   return hipGetLastError();
 }

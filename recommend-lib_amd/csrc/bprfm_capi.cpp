@@ -61,6 +61,9 @@ fm::Args args_of(const bprfm_handle* h, int B) {
   a.acc_b = h->acc_b;
   a.Gb = h->Gb;
   a.stamp = h->stamp;
+  a.F = h->cfg.num_features;
+  // small tables: sweeping the F row stamps beats claiming 3B references with atomics
+  a.sweep = a.F <= 4LL * B ? 1 : 0;
   const int ld = h->ld;
   a.gamma = h->bn;
   a.beta = h->bn + ld;

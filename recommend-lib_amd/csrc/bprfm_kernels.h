@@ -12,6 +12,8 @@ struct Args {
   float *E, *acc_E, *GE;          // [F, ld] embeddings of the F features
   float *b, *acc_b, *Gb;          // [F] feature biases
   int32_t* stamp;                 // [F] step of a row's last update (apply claims a row once)
+  int64_t F;                      // feature rows
+  int32_t sweep;                  // apply sweeps all F rows (stamped by the backward)
   float *gamma, *beta, *acc_gamma, *acc_beta, *ggamma, *gbeta;  // [ld] BatchNorm1d affine
   float* run;                     // [2, ld] BatchNorm running mean, running variance
   const float* bias_;             // [1] global bias (its gradient is identically zero)

@@ -1,7 +1,8 @@
 """recommend-lib_amd — MI355X-native BPR-MF training path (drop-in for the reference's
 BPRMFRecommender / util.data_loader.BPRData / util.metrics BPR parts), plus the NCF path of
 SURVEY.md §8f (NCFRecommender / NCFData), the Cython rating-SGD models SVD / RSVD
-(util/matrix_factorization.pyx) and BPR-FM (BPRFMRecommender / BPRFMData).
+(util/matrix_factorization.pyx) BPR-FM (BPRFMRecommender / BPRFMData) and Item2Vec (Item2VecRecommender SGNS /
+BuildCorpus).
 
 The directory name is not a Python identifier; import it with
     importlib.import_module("recommend-lib_amd")
@@ -25,8 +26,11 @@ from . import mf
 from .mf import SVD, RSVD
 from . import bprfm
 from .bprfm import BPRFM, BPRFMData
+from . import item2vec
+from .item2vec import Item2Vec, SGNS, BuildCorpus, PermutedSubsampledCorpus
 
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 
 __all__ = ["BPRMF", "BPR", "BPRData", "NCF", "NCFData", "ShardedBPRMF", "BprmfError", "metrics",
-           "ingest", "load_rate", "load_mat", "SVD", "RSVD", "BPRFM", "BPRFMData", "build", "LIB_PATH"]
+           "ingest", "load_rate", "load_mat", "SVD", "RSVD", "BPRFM", "BPRFMData", "Item2Vec", "SGNS", "BuildCorpus",
+           "PermutedSubsampledCorpus", "build", "LIB_PATH"]

@@ -1,4 +1,4 @@
-"""ctypes binding of libbprmf_amd.so (include/bprmf.h, ncf.h, mf.h, bprfm.h).
+"""ctypes binding of libbprmf_amd.so (include/bprmf.h, ncf.h, mf.h, bprfm.h, sgns.h).
 
 The HIP library is the only compute path: if it is missing or no GPU is visible, handle creation
 raises — there is no CPU fallback in the product.
@@ -140,6 +140,17 @@ SIGNATURES = {
     "bprfm_dropout_mask": [_P, ctypes.c_int32, _P],
     "bprfm_predict": [_P, _P, _P, _I64, _P],
     "bprfm_steps": [_P],
+    # include/sgns.h (sgns_config / sgns_stats: recommend-lib_amd/item2vec.py)
+    "sgns_create": [_P, ctypes.POINTER(ctypes.c_void_p)],
+    "sgns_destroy": [_P],
+    "sgns_set_noise": [_P, _P],
+    "sgns_set_weights": [_P, _P, _P],
+    "sgns_get_weights": [_P, _P, _P],
+    "sgns_set_adam": [_P, _I64, _P, _P, _P, _P],
+    "sgns_get_adam": [_P, _P, _P, _P, _P, _P],
+    "sgns_train": [_P, _P, _P, _P, _I64, ctypes.c_int32, _P],
+    "sgns_negatives": [_P, ctypes.c_int32, _P],
+    "sgns_lookup": [_P, ctypes.c_int32, _P, _I64, _P],
 }
 RESTYPES = {"bprmf_last_error": ctypes.c_char_p, "bprfm_steps": ctypes.c_int64}
 

@@ -11,8 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libbprmf_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "dist.hip", "topk.hip", "ncf.hip", "capi.cpp", "dist.cpp", "ncf_capi.cpp", "ingest.cpp", "mf.hip", "mf_capi.cpp", "bprfm.hip", "bprfm_capi.cpp")]
-HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h", "handle.h", "ncf_kernels.h", "mf_kernels.h", "bprfm_kernels.h")] + [os.path.join(ROOT, "include", n) for n in ("bprmf.h", "ncf.h", "mf.h", "bprfm.h")]
+SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "dist.hip", "topk.hip", "ncf.hip", "capi.cpp", "dist.cpp", "ncf_capi.cpp", "ingest.cpp", "mf.hip", "mf_capi.cpp", "bprfm.hip", "bprfm_capi.cpp", "sgns.hip", "sgns_capi.cpp")]
+HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h", "handle.h", "ncf_kernels.h", "mf_kernels.h", "bprfm_kernels.h", "sgns_kernels.h")] + [os.path.join(ROOT, "include", n) for n in ("bprmf.h", "ncf.h", "mf.h", "bprfm.h", "sgns.h")]
 ARCH = os.environ.get("BPRMF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -36,7 +36,7 @@ def build(force=False, verbose=False):
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
-           "-o", tmp] + SOURCES + ["-L/opt/rocm/lib", "-lrccl"]
+           "-o", tmp] + SOURCES + ["-L/opt/rocm/lib", "-lrccl", "-lrocblas"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -1,0 +1,222 @@
+// sgns.hip — gfx950 kernels of the Item2Vec training step (include/sgns.h), SURVEY.md §8f row 4:
+// SGNS.forward (Item2VecRecommender.py:82-97), its backward and Adam (:272, :282-286).
+//
+// Per example b (centre word i, C context words o_c, C * n negatives w):
+//   loss = 1/(B C) sum_b [ sum_c softplus(-o_c . i) + sum_{c,k} softplus(w_ck . i) ]
+//   d loss / d (o . i) = -(1 - sigma(o . i)) / (B C),   d loss / d (w . i) = sigma(w . i) / (B C)
+// K1 (k_sgns_fwd): one wave per example, lane l holding factors l, l + 64, ... of the centre row in
+// registers; the R = C (1 + n) ovectors rows are streamed U at a time (coalesced 256-byte row
+// segments), each dot reduced across the wave; the centre row's gradient sum_r g_r o_r stays in
+// registers and is added into GI with f32 atomics; g_r goes into S[word, b].  The ovectors
+// gradient is then one GEMM, GO = S^T-weighted sum of the centre rows: GO [V, E] = S [V, B] x IB
+// [B, E] (rocBLAS sgemm, sgns_capi.cpp), and both tables take a dense Adam sweep (ncf.hip
+// adam_rows: rows never touched keep m = v = 0 and are skipped, exactly as torch leaves them).
+// Row 0 is nn.Embedding's padding_idx: it gets no gradient.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "sgns_kernels.h"
+
+namespace bprmf {
+namespace sgns {
+
+constexpr int kT = 256;  // 4 waves, one example each
+constexpr int kU = 4;    // ovectors rows in flight per wave
+constexpr uint32_t TAG_SGNS = 0x53474E00u;
+
+static __device__ __forceinline__ int32_t draw_neg(const Args& a, int b, int k) {
+  uint32_t c0 = (uint32_t)b, c1 = (uint32_t)k, c2 = (uint32_t)a.t, c3 = TAG_SGNS;
+  philox10(c0, c1, c2, c3, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+  const float u = (float)(c0 >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+  if (!a.cdf) {  // torch.FloatTensor(...).uniform_(0, V - 1).long(): [0, V - 2]
+    const int64_t w = (int64_t)(u * (float)(a.V - 1));
+    return (int32_t)std::min<int64_t>(w, a.V - 2 > 0 ? a.V - 2 : 0);
+  }
+  // torch.multinomial(weights, ..., replacement=True): first x with cdf[x] > u
+  int64_t lo = 0, hi = a.V - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a.cdf[mid] > u) hi = mid;
+    else lo = mid + 1;
+  }
+  return (int32_t)lo;
+}
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+template <int M>
+__global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  if (b >= a.B) return;  // whole waves
+  const int64_t iw = a.iw[b];
+  const int C = a.C, CN = a.C * a.n, R = C + CN;
+  const float inv = 1.0f / ((float)a.B * (float)C);
+  float iv[M], gi[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int e = lane + 64 * m;
+    iv[m] = e < a.E ? a.I[iw * a.ld + e] : 0.f;
+    gi[m] = 0.f;
+    if (e < a.E) a.IB[(int64_t)b * a.ld + e] = iv[m];
+  }
+  float lsum = 0.f;
+  for (int r0 = 0; r0 < R; r0 += kU) {
+    int32_t w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int r = r0 + u;
+      w[u] = r >= R ? -1
+             : r < C ? a.ow[(int64_t)b * C + r]
+             : a.nw ? a.nw[(int64_t)b * CN + (r - C)]
+                    : draw_neg(a, b, r - C);
+    }
+    float ov[kU][M];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int e = lane + 64 * m;
+        ov[u][m] = (w[u] >= 0 && e < a.E) ? a.O[(int64_t)w[u] * a.ld + e] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (w[u] < 0) break;
+      float p = 0.f;
+#pragma unroll
+      for (int m = 0; m < M; ++m) p += iv[m] * ov[u][m];
+      const float s = wave_sum(p);
+      const float sig = 1.0f / (1.0f + expf(-s));
+      const bool ctx = r0 + u < C;
+      const float g = ctx ? -(1.0f - sig) * inv : sig * inv;
+      lsum += ctx ? softplus(-s) : softplus(s);
+#pragma unroll
+      for (int m = 0; m < M; ++m) gi[m] += g * ov[u][m];
+      if (lane == 0 && w[u] != 0) {
+        atomicAdd(a.S + (int64_t)w[u] * a.B + b, g);
+        a.touch_o[w[u]] = a.t;
+      }
+    }
+  }
+  if (iw != 0) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int e = lane + 64 * m;
+      if (e < a.E) atomicAdd(a.GI + iw * a.ld + e, gi[m]);
+    }
+    if (lane == 0) a.touch_i[iw] = a.t;
+  }
+  if (lane == 0) a.lbuf[b] = lsum * inv;
+}
+
+// the batch's loss, fixed order (one workgroup, 16 loads per thread in flight)
+__global__ __launch_bounds__(kT) void k_sgns_loss(Args a) {
+  constexpr int R = 16;
+  __shared__ double red[kT];
+  double s = 0.0;
+  for (int t0 = 0; t0 < a.B; t0 += kT * R) {
+    float v[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const int t = t0 + m * kT + threadIdx.x;
+      v[m] = t < a.B ? a.lbuf[t] : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < R; ++m) s += (double)v[m];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = kT / 2; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.loss[0] += red[0];
+}
+
+__global__ void k_sgns_negs(Args a, int32_t* __restrict__ out) {
+  const int64_t CN = (int64_t)a.C * a.n, total = CN * a.B;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x)
+    out[x] = draw_neg(a, (int)(x / CN), (int)(x % CN));
+}
+
+// Item2Vec.__init__ (:46-53): row 0 zeros, the rest uniform(-lim, lim); padding columns 0
+__global__ void k_sgns_init(float* __restrict__ W, int64_t V, int E, int ld, float lim,
+                            uint64_t seed, uint32_t tag) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < V * ld;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = x / ld;
+    const int e = (int)(x % ld);
+    float v = 0.f;
+    if (row > 0 && e < E) {
+      uint32_t c0 = (uint32_t)row, c1 = (uint32_t)(row >> 32), c2 = (uint32_t)e, c3 = tag;
+      philox10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
+      v = lim * (2.f * ((float)(c0 >> 8) * (1.0f / 16777216.0f)) - 1.f);
+    }
+    W[x] = v;
+  }
+}
+
+__global__ void k_sgns_lookup(const float* __restrict__ W, int ld, int E,
+                              const int32_t* __restrict__ idx, int64_t n, float* __restrict__ out) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n * E;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = x / E;
+    out[x] = W[(int64_t)idx[q] * ld + (x % E)];
+  }
+}
+
+static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+
+int lanes_elems(int E) { return (E + 63) / 64; }
+
+hipError_t init_uniform(float* W, int64_t V, int E, int ld, float lim, uint64_t seed, uint32_t tag,
+                        hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  k_sgns_init<<<grid_for(V * ld), 256, 0, s>>>(W, V, E, ld, lim, seed, tag);
+  return hipGetLastError();
+}
+
+hipError_t forward_backward(const Args& a, hipStream_t s) {
+  if (a.B <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((a.B + kT / 64 - 1) / (kT / 64));
+  switch (lanes_elems(a.E)) {
+#define SG(M_) \
+  case M_: k_sgns_fwd<M_><<<blocks, kT, 0, s>>>(a); break;
+    SG(1) SG(2) SG(3) SG(4) SG(5) SG(6) SG(7) SG(8) SG(9) SG(10) SG(11) SG(12) SG(13) SG(14)
+    SG(15) SG(16)
+#undef SG
+    default: return hipErrorInvalidValue;  // E > 1024
+  }
+  return hipGetLastError();
+}
+
+hipError_t loss_sum(const Args& a, hipStream_t s) {
+  if (a.B <= 0) return hipSuccess;
+  k_sgns_loss<<<1, kT, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t negatives(const Args& a, int32_t* out, hipStream_t s) {
+  if (a.B <= 0 || a.C * a.n <= 0) return hipSuccess;
+  k_sgns_negs<<<grid_for((int64_t)a.B * a.C * a.n), 256, 0, s>>>(a, out);
+  return hipGetLastError();
+}
+
+hipError_t lookup(const float* W, int ld, int E, const int32_t* idx, int64_t n, float* out,
+                  hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_sgns_lookup<<<grid_for(n * E), 256, 0, s>>>(W, ld, E, idx, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace sgns
+}  // namespace bprmf

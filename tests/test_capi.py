@@ -11,10 +11,10 @@ from conftest import ROOT
 
 def _declared():
     names = set()
-    for h in ("bprmf.h", "ncf.h", "mf.h", "bprfm.h"):
+    for h in ("bprmf.h", "ncf.h", "mf.h", "bprfm.h", "sgns.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
-        names |= set(re.findall(r"\b((?:bprmf|ncf|mf|bprfm)_[a-z0-9_]+)\s*\(", src))
+        names |= set(re.findall(r"\b((?:bprmf|ncf|mf|bprfm|sgns)_[a-z0-9_]+)\s*\(", src))
     return sorted(names)
 
 

@@ -36,7 +36,8 @@ typedef struct {
   int64_t vocab_size;     /* rows of ivectors / ovectors (len(idx2item)) */
   int32_t embedding_size; /* --e_dim (default 300), 1..1024 */
   int32_t n_negs;         /* --n_negs (default 20) */
-  int32_t context;        /* context words per example: 2 x --window (default 10) */
+  int32_t context;        /* context words per example: 2 x --window (default 10);
+                             context x (1 + n_negs) <= 1024 */
   int32_t max_batch;      /* largest batch a train call may use (--mb, default 4096) */
   float lr, beta1, beta2, eps; /* optim.Adam defaults: 1e-3, 0.9, 0.999, 1e-8 */
   uint64_t seed;          /* table init and negative draws */

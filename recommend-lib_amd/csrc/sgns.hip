@@ -7,9 +7,10 @@
 // K1 (k_sgns_fwd): one wave per example, lane l holding factors l, l + 64, ... of the centre row in
 // registers; the R = C (1 + n) ovectors rows are streamed U at a time (coalesced 256-byte row
 // segments), each dot reduced across the wave; the centre row's gradient sum_r g_r o_r stays in
-// registers and is added into GI with f32 atomics; g_r goes into S[word, b].  The ovectors
-// gradient is then one GEMM, GO = S^T-weighted sum of the centre rows: GO [V, E] = S [V, B] x IB
-// [B, E] (rocBLAS sgemm, sgns_capi.cpp), and both tables take a dense Adam sweep (ncf.hip
+// registers and is added into GI with f32 atomics; g_r goes into S[word, b] after the loop.  The
+// ovectors gradient is then a GEMM, GO [V, E] = S [V, B] x IB [B, E] (rocBLAS, split over B into
+// partial products that k_sgns_sum_parts adds, sgns_capi.cpp), and both tables take a dense Adam
+// sweep (ncf.hip
 // adam_rows: rows never touched keep m = v = 0 and are skipped, exactly as torch leaves them).
 // Row 0 is nn.Embedding's padding_idx: it gets no gradient.
 #include <hip/hip_runtime.h>
@@ -25,7 +26,8 @@ namespace bprmf {
 namespace sgns {
 
 constexpr int kT = 256;  // 4 waves, one example each
-constexpr int kU = 4;    // ovectors rows in flight per wave
+constexpr int kU = 8;    // ovectors rows in flight per wave (wave_sum8 reduces 8 at once)
+constexpr int kMaxR = 1024;  // references per example (C (1 + n)), staged in LDS
 constexpr uint32_t TAG_SGNS = 0x53474E00u;
 
 static __device__ __forceinline__ int32_t draw_neg(const Args& a, int b, int k) {
@@ -52,14 +54,44 @@ static __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// sum over the 64 lanes of 8 values at once (a transposed butterfly: 4 + 2 + 1 exchanges halve
+// the values per lane, then 3 plain steps): on return lanes 8q .. 8q + 7 hold the total of p[q]
+static __device__ __forceinline__ float wave_sum8(const float (&p)[8], int lane) {
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
+  float q4[4], q2[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float send = h5 ? p[j] : p[j + 4];
+    q4[j] = (h5 ? p[j + 4] : p[j]) + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float send = h4 ? q4[j] : q4[j + 2];
+    q2[j] = (h4 ? q4[j + 2] : q4[j]) + __shfl_xor(send, 16);
+  }
+  float v = (h3 ? q2[1] : q2[0]) + __shfl_xor(h3 ? q2[0] : q2[1], 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
 template <int M>
 __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  const int wv = threadIdx.x >> 6;
+  const int b = blockIdx.x * (kT / 64) + wv;
   if (b >= a.B) return;  // whole waves
   const int64_t iw = a.iw[b];
   const int C = a.C, CN = a.C * a.n, R = C + CN;
   const float inv = 1.0f / ((float)a.B * (float)C);
+  // the example's R words (contexts, then negatives: given, or drawn one per lane) and, after
+  // the loop, their coefficients, in this wave's LDS slice
+  __shared__ int32_t wsh[kT / 64][kMaxR];
+  __shared__ float gsh[kT / 64][kMaxR];
+  for (int r = lane; r < R; r += 64)
+    wsh[wv][r] = r < C ? a.ow[(int64_t)b * C + r]
+                : a.nw ? a.nw[(int64_t)b * CN + (r - C)] : draw_neg(a, b, r - C);
   float iv[M], gi[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -68,18 +100,16 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
     gi[m] = 0.f;
     if (e < a.E) a.IB[(int64_t)b * a.ld + e] = iv[m];
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float lsum = 0.f;
+  const int mine = lane >> 3;  // the reference of each group of 8 whose sum this lane holds
   for (int r0 = 0; r0 < R; r0 += kU) {
     int32_t w[kU];
+    float ov[kU][M], p[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int r = r0 + u;
-      w[u] = r >= R ? -1
-             : r < C ? a.ow[(int64_t)b * C + r]
-             : a.nw ? a.nw[(int64_t)b * CN + (r - C)]
-                    : draw_neg(a, b, r - C);
-    }
-    float ov[kU][M];
+    for (int u = 0; u < kU; ++u) w[u] = r0 + u < R ? wsh[wv][r0 + u] : -1;
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -89,21 +119,39 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
       }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      if (w[u] < 0) break;
-      float p = 0.f;
+      p[u] = 0.f;
 #pragma unroll
-      for (int m = 0; m < M; ++m) p += iv[m] * ov[u][m];
-      const float s = wave_sum(p);
-      const float sig = 1.0f / (1.0f + expf(-s));
-      const bool ctx = r0 + u < C;
-      const float g = ctx ? -(1.0f - sig) * inv : sig * inv;
-      lsum += ctx ? softplus(-s) : softplus(s);
-#pragma unroll
-      for (int m = 0; m < M; ++m) gi[m] += g * ov[u][m];
-      if (lane == 0 && w[u] != 0) {
-        atomicAdd(a.S + (int64_t)w[u] * a.B + b, g);
-        a.touch_o[w[u]] = a.t;
+      for (int m = 0; m < M; ++m) p[u] += iv[m] * ov[u][m];
+    }
+    const float sdot = wave_sum8(p, lane);  // o . i of reference r0 + mine
+    const int r = r0 + mine;
+    float g = 0.f;
+    if (r < R) {
+      const bool ctx = r < C;
+      const float sig = 1.0f / (1.0f + __expf(-sdot));
+      g = ctx ? -(1.0f - sig) * inv : sig * inv;
+      if ((lane & 7) == 0) {
+        lsum += ctx ? softplus(-sdot) : softplus(sdot);
+        gsh[wv][r] = g;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const float gu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), 8 * u));
+#pragma unroll
+      for (int m = 0; m < M; ++m) gi[m] += gu * ov[u][m];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // S and touch_o after the loop (gfx9 counts stores and atomics in vmcnt: issued inside the loop
+  // they would hold the next iteration's row loads until they complete)
+  for (int r = lane; r < R; r += 64) {
+    const int32_t wr = wsh[wv][r];
+    if (wr != 0) {
+      atomicAdd(a.S + (int64_t)wr * a.B + b, gsh[wv][r]);
+      a.touch_o[wr] = a.t;
     }
   }
   if (iw != 0) {
@@ -114,6 +162,7 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
     }
     if (lane == 0) a.touch_i[iw] = a.t;
   }
+  lsum = wave_sum(lsum);
   if (lane == 0) a.lbuf[b] = lsum * inv;
 }
 
@@ -174,6 +223,23 @@ __global__ void k_sgns_lookup(const float* __restrict__ W, int ld, int E,
   }
 }
 
+// GO = sum of the nsplit partial products (fixed order), float4 rows
+__global__ void k_sgns_sum_parts(const float* __restrict__ parts, int nsplit, int64_t n4,
+                                 float* __restrict__ out) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(parts)[x];
+    for (int q = 1; q < nsplit; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(parts)[q * n4 + x];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[x] = acc;
+  }
+}
+
 static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
 
 int lanes_elems(int E) { return (E + 63) / 64; }
@@ -196,6 +262,12 @@ hipError_t forward_backward(const Args& a, hipStream_t s) {
 #undef SG
     default: return hipErrorInvalidValue;  // E > 1024
   }
+  return hipGetLastError();
+}
+
+hipError_t sum_parts(const float* parts, int nsplit, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_sgns_sum_parts<<<grid_for(n / 4), 256, 0, s>>>(parts, nsplit, n / 4, out);
   return hipGetLastError();
 }
 

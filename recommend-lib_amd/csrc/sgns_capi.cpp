@@ -24,7 +24,7 @@ struct sgns_handle {
   sgns_config cfg;
   int ld = 0;
   float *I = nullptr, *O = nullptr, *mI = nullptr, *vI = nullptr, *mO = nullptr, *vO = nullptr;
-  float *GI = nullptr, *GO = nullptr, *S = nullptr, *IB = nullptr, *lbuf = nullptr, *cdf = nullptr;
+  float *GI = nullptr, *GO = nullptr, *GOp = nullptr, *S = nullptr, *IB = nullptr, *lbuf = nullptr, *cdf = nullptr;
   int32_t *touch_i = nullptr, *touch_o = nullptr;
   int32_t* ex = nullptr;  // uploaded examples: iwords [cap], owords [cap, C], nwords [cap, C n]
   int64_t cap = 0;
@@ -36,6 +36,10 @@ struct sgns_handle {
 };
 
 namespace {
+// the ovectors-gradient GEMM has ceil(E/128) x ceil(V/64) output tiles; with V ~ 2k that is far
+// fewer workgroups than CUs, so the reduction over the batch is split into partial products
+constexpr int kMaxSplit = 8;
+int split_for(int B) { return std::max(1, std::min(kMaxSplit, B / 512)); }
 int sset_dev(const sgns_handle* h) {
   HIPCHK(hipSetDevice(h->cfg.device));
   return 0;
@@ -110,6 +114,8 @@ int sgns_create(const sgns_config* cfg, sgns_handle** out) {
   if (cfg->vocab_size < 2 || cfg->embedding_size <= 0 || cfg->n_negs < 0 || cfg->context <= 0)
     return fail(BPRMF_E_INVALID, "need vocab_size >= 2, embedding_size > 0, context > 0, n_negs >= 0");
   if (cfg->embedding_size > 1024) return fail(BPRMF_E_UNSUPPORTED, "embedding_size must be <= 1024");
+  if ((int64_t)cfg->context * (1 + (int64_t)cfg->n_negs) > 1024)  // sgns.hip kMaxR
+    return fail(BPRMF_E_UNSUPPORTED, "context * (1 + n_negs) must be <= 1024");
   if (cfg->vocab_size >= INT32_MAX) return fail(BPRMF_E_UNSUPPORTED, "vocab_size must fit int32");
   if (cfg->max_batch <= 0) return fail(BPRMF_E_INVALID, "max_batch must be > 0");
   if (!(cfg->lr > 0.f) || !(cfg->eps > 0.f) || !(cfg->beta1 >= 0.f && cfg->beta1 < 1.f) ||
@@ -134,7 +140,7 @@ int sgns_create(const sgns_config* cfg, sgns_handle** out) {
   float** tabs[] = {&h->I, &h->O, &h->mI, &h->vI, &h->mO, &h->vO, &h->GI, &h->GO};
   for (float** p : tabs)
     if ((rc = zalloc(p, V * ld))) return bail(rc);
-  if ((rc = zalloc(&h->S, V * B)) || (rc = zalloc(&h->IB, B * ld)) || (rc = zalloc(&h->lbuf, B)) ||
+  if ((rc = zalloc(&h->GOp, (int64_t)kMaxSplit * V * ld)) || (rc = zalloc(&h->S, V * B)) || (rc = zalloc(&h->IB, B * ld)) || (rc = zalloc(&h->lbuf, B)) ||
       (rc = zalloc(&h->touch_i, V)) || (rc = zalloc(&h->touch_o, V)) || (rc = zalloc(&h->loss, 1)))
     return bail(rc);
   if (hipMemset(h->touch_i, 0xff, 4 * V) != hipSuccess || hipMemset(h->touch_o, 0xff, 4 * V) != hipSuccess)
@@ -153,7 +159,7 @@ int sgns_destroy(sgns_handle* h) {
   if (!h) return 0;
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  void* ptrs[] = {h->I,  h->O,    h->mI,   h->vI,      h->mO,      h->vO, h->GI, h->GO, h->S,
+  void* ptrs[] = {h->GOp, h->I,  h->O,    h->mI,   h->vI,      h->mO,      h->vO, h->GI, h->GO, h->S,
                   h->IB, h->lbuf, h->cdf, h->touch_i, h->touch_o, h->ex, h->loss};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -303,10 +309,26 @@ int sgns_train(sgns_handle* h, const int32_t* iwords, const int32_t* owords, con
     a.nw = nwords ? d_nw + beg * CN : nullptr;
     HIPCHK(hipMemsetAsync(h->S, 0, 4 * (size_t)V * B, s));
     HIPCHK(sgns::forward_backward(a, s));
-    // GO^T [E, V] = IB^T [E, B] x S^T [B, V] in rocBLAS's column-major terms
-    if (rocblas_sgemm(h->blas, rocblas_operation_none, rocblas_operation_none, E, (rocblas_int)V, B,
-                      &one, h->IB, h->ld, h->S, B, &zero, h->GO, h->ld) != rocblas_status_success)
-      return fail(BPRMF_E_HIP, "rocblas_sgemm failed");
+    // GO^T [E, V] = IB^T [E, B] x S^T [B, V] in rocBLAS's column-major terms, as nsp products
+    // over slices of B (slice q: columns q Bs.. of IB^T, rows of S^T) summed in a fixed order
+    const int nsp = split_for(B), Bs = B / nsp, tail = B - Bs * nsp;
+    if (nsp == 1) {
+      if (rocblas_sgemm(h->blas, rocblas_operation_none, rocblas_operation_none, E, (rocblas_int)V,
+                        B, &one, h->IB, h->ld, h->S, B, &zero, h->GO, h->ld) != rocblas_status_success)
+        return fail(BPRMF_E_HIP, "rocblas_sgemm failed");
+    } else {
+      if (rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_none, E,
+                                        (rocblas_int)V, Bs, &one, h->IB, h->ld, (rocblas_stride)Bs * h->ld,
+                                        h->S, B, (rocblas_stride)Bs, &zero, h->GOp, h->ld,
+                                        (rocblas_stride)V * h->ld, nsp) != rocblas_status_success)
+        return fail(BPRMF_E_HIP, "rocblas_sgemm_strided_batched failed");
+      if (tail &&  // the last B % nsp examples into the last partial
+          rocblas_sgemm(h->blas, rocblas_operation_none, rocblas_operation_none, E, (rocblas_int)V,
+                        tail, &one, h->IB + (int64_t)Bs * nsp * h->ld, h->ld, h->S + Bs * nsp, B,
+                        &one, h->GOp + (int64_t)(nsp - 1) * V * h->ld, h->ld) != rocblas_status_success)
+        return fail(BPRMF_E_HIP, "rocblas_sgemm failed");
+      HIPCHK(sgns::sum_parts(h->GOp, nsp, V * h->ld, h->GO, s));
+    }
     const ncf::AdamArgs ad = adam_args(h, a.t);
     HIPCHK(ncf::adam_rows(h->I, h->mI, h->vI, h->GI, h->touch_i, V, h->ld, a.t, ad, s));
     HIPCHK(ncf::adam_rows(h->O, h->mO, h->vO, h->GO, h->touch_o, V, h->ld, a.t, ad, s));

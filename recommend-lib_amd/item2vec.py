@@ -172,8 +172,8 @@ class SGNS:
     """SGNS(embedding, vocab_size, n_negs, weights) + optim.Adam(lr, betas, eps).
 
     train_step(iword, owords) = the loop body (loss, zero_grad, backward, step) and returns the
-    loss; train_epoch(dataset, mb) = one shuffled DataLoader pass.  `context` defaults to the
-    owords width of the first batch (2 x window)."""
+    loss; train_epoch(dataset, mb) = one shuffled DataLoader pass.  `context` is the owords
+    width, 2 x window."""
 
     def __init__(self, embedding, vocab_size=20000, n_negs=20, weights=None, context=10, lr=1e-3,
                  betas=(0.9, 0.999), eps=1e-8, max_batch=4096, seed=0, device=0):

@@ -100,6 +100,9 @@ def mf_lib():
                                          ctypes.c_double, ctypes.c_int, ctypes.c_double,
                                          ctypes.c_double, ctypes.c_double, _f64p, _f64p, _f64p,
                                          _f64p, ctypes.c_int]
+        L.oracle_svdpp_epochs.argtypes = [ctypes.c_int64, _i32p, _i32p, _f64p, ctypes.c_int,
+                                          ctypes.c_double, _f64p, _f64p, _f64p, _f64p, _f64p,
+                                          _f64p, _f64p, _i64p, _i32p, _f64p, ctypes.c_int]
         _mf = L
     return _mf
 
@@ -125,6 +128,29 @@ def rsvd_epochs(u, i, r, P, Q, bu, bi, gm, version, lr, reg, reg2, epochs):
                                 int(version), float(lr), float(reg), float(reg2), P, Q, bu, bi,
                                 int(epochs))
     return P, Q, bu, bi
+
+
+def user_items(u, i, U):
+    """ur of SVDpp.fit (:222-224): each user's items in train-set order, as CSR (uoff, uitems)."""
+    u = np.asarray(u, np.int64)
+    order = np.argsort(u, kind="stable")
+    uoff = np.zeros(U + 1, np.int64)
+    np.add.at(uoff, u + 1, 1)
+    return np.cumsum(uoff), np.ascontiguousarray(np.asarray(i, np.int32)[order])
+
+
+def svdpp_epochs(u, i, r, P, Q, Y, bu, bi, gm, lr, reg, epochs):
+    """SVDpp.fit epochs on copies of the tables; returns (P, Q, Y, bu, bi)."""
+    P, Q, Y = (np.array(x, np.float64, order="C") for x in (P, Q, Y))
+    bu, bi = np.array(bu, np.float64), np.array(bi, np.float64)
+    uoff, uitems = user_items(u, i, P.shape[0])
+    impl = np.zeros(P.shape[1])
+    mf_lib().oracle_svdpp_epochs(len(u), np.ascontiguousarray(u, np.int32),
+                                 np.ascontiguousarray(i, np.int32),
+                                 np.ascontiguousarray(r, np.float64), P.shape[1], float(gm),
+                                 np.asarray(lr, np.float64), np.asarray(reg, np.float64), P, Q, Y,
+                                 bu, bi, uoff, uitems, impl, int(epochs))
+    return P, Q, Y, bu, bi
 
 
 def mf_levels(u, i, U, I):

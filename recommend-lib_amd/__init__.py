@@ -23,7 +23,7 @@ from .ncf import NCF, NCFData
 from . import ingest
 from .ingest import load_rate, load_mat
 from . import mf
-from .mf import SVD, RSVD
+from .mf import SVD, RSVD, SVDpp
 from . import bprfm
 from .bprfm import BPRFM, BPRFMData
 from . import item2vec
@@ -32,5 +32,5 @@ from .item2vec import Item2Vec, SGNS, BuildCorpus, PermutedSubsampledCorpus
 BPR = BPRMF  # the reference's class name (BPRMFRecommender.py:28)
 
 __all__ = ["BPRMF", "BPR", "BPRData", "NCF", "NCFData", "ShardedBPRMF", "BprmfError", "metrics",
-           "ingest", "load_rate", "load_mat", "SVD", "RSVD", "BPRFM", "BPRFMData", "Item2Vec", "SGNS", "BuildCorpus",
+           "ingest", "load_rate", "load_mat", "SVD", "RSVD", "SVDpp", "BPRFM", "BPRFMData", "Item2Vec", "SGNS", "BuildCorpus",
            "PermutedSubsampledCorpus", "build", "LIB_PATH"]

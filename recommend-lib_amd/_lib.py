@@ -131,6 +131,8 @@ SIGNATURES = {
     "mf_get_weights": [_P, _P, _P, _P, _P],
     "mf_fit": [_P, ctypes.c_int32, _P],
     "mf_predict": [_P, _P, _P, _I64, _P],
+    "mf_set_implicit": [_P, _P],
+    "mf_get_implicit": [_P, _P],
     # include/bprfm.h (bprfm_config / bprfm_stats: recommend-lib_amd/bprfm.py)
     "bprfm_create": [_P, ctypes.POINTER(ctypes.c_void_p)],
     "bprfm_destroy": [_P],

@@ -19,6 +19,8 @@ using namespace bprmf;
 struct mf_handle {
   mf_config cfg;
   double *P = nullptr, *Q = nullptr, *bu = nullptr, *bi = nullptr;
+  double* Y = nullptr;  // SVDpp: yj [I, k]
+  int32_t *uoff = nullptr, *uitems = nullptr, *udup = nullptr, *uslot = nullptr;  // SVDpp
   int32_t *su = nullptr, *si = nullptr, *loff = nullptr;
   double* sr = nullptr;
   int64_t n = 0;
@@ -53,14 +55,76 @@ mf::Args args_of(const mf_handle* h) {
   a.Q = h->Q;
   a.bu = h->bu;
   a.bi = h->bi;
-  // SVD.fit: global_mean = 0 when not biased (:121-124); RSVD keeps it for the bias decay
+  // SVD.fit: global_mean = 0 when not biased (:121-124); RSVD keeps it for the bias decay, and
+  // SVDpp always adds it (:199, :246)
   a.gm = (h->cfg.model == MF_SVD && !h->cfg.variant) ? 0.0 : h->gm;
   a.variant = h->cfg.variant;
   for (int x = 0; x < 4; ++x) {
     a.lr[x] = h->cfg.lr[x];
     a.reg[x] = h->cfg.reg[x];
   }
+  a.Y = h->Y;
+  a.uoff = h->uoff;
+  a.uitems = h->uitems;
+  a.udup = h->udup;
+  a.uslot = h->uslot;
+  a.lr_yj = h->cfg.lr_yj;
+  a.reg_yj = h->cfg.reg_yj;
   return a;
+}
+
+// SVDpp: samples in train order (one level each) and ur[u] (:222-224) as CSR, list order = train
+// order; udup[u] = 1 when u's list holds an item twice
+int set_train_svdpp(mf_handle* h, const int32_t* users, const int32_t* items, const double* ratings,
+                    int64_t n, double global_mean) {
+  const int64_t U = h->cfg.user_num, I = h->cfg.item_num;
+  std::vector<int32_t> off(U + 1, 0), list(n), dup(U, 0);
+  for (int64_t s = 0; s < n; ++s) {
+    const int32_t u = users[s], i = items[s];
+    if (u < 0 || u >= U || i < 0 || i >= I)
+      return fail(BPRMF_E_RANGE, "train row %lld = (%d, %d) out of range", (long long)s, u, i);
+    off[u + 1]++;
+  }
+  for (int64_t u = 0; u < U; ++u) off[u + 1] += off[u];
+  std::vector<int32_t> pos(off.begin(), off.end() - 1);
+  for (int64_t s = 0; s < n; ++s) list[pos[users[s]]++] = items[s];
+  std::vector<int32_t> seen(I, -1), first(I, 0), slot(n);
+  for (int64_t u = 0; u < U; ++u)
+    for (int32_t q = off[u]; q < off[u + 1]; ++q) {
+      const int32_t it = list[q];
+      if (seen[it] == (int32_t)u) {
+        dup[u] = 1;
+      } else {
+        seen[it] = (int32_t)u;
+        first[it] = q - off[u];
+      }
+      slot[q] = first[it];
+    }
+  void* olds[] = {h->su, h->si, h->sr, h->loff, h->uoff, h->uitems, h->udup, h->uslot};
+  for (void* p : olds)
+    if (p) HIPCHK(hipFree(p));
+  h->su = h->si = h->loff = h->uoff = h->uitems = h->udup = h->uslot = nullptr;
+  h->sr = nullptr;
+  if (int r = malloc_dev(&h->su, n)) return r;
+  if (int r = malloc_dev(&h->si, n)) return r;
+  if (int r = malloc_dev(&h->sr, n)) return r;
+  if (int r = malloc_dev(&h->uoff, U + 1)) return r;
+  if (int r = malloc_dev(&h->uitems, n)) return r;
+  if (int r = malloc_dev(&h->udup, U)) return r;
+  if (int r = malloc_dev(&h->uslot, n)) return r;
+  if (n) {
+    HIPCHK(hipMemcpy(h->su, users, 4 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->si, items, 4 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->sr, ratings, 8 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->uitems, list.data(), 4 * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->uslot, slot.data(), 4 * n, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemcpy(h->uoff, off.data(), 4 * (U + 1), hipMemcpyHostToDevice));
+  if (U) HIPCHK(hipMemcpy(h->udup, dup.data(), 4 * U, hipMemcpyHostToDevice));
+  h->n = n;
+  h->levels = (int32_t)n;
+  h->gm = global_mean;
+  return 0;
 }
 }  // namespace
 
@@ -72,7 +136,8 @@ int mf_create(const mf_config* cfg, mf_handle** out) {
   if (cfg->user_num < 0 || cfg->item_num < 0 || cfg->n_factors <= 0)
     return fail(BPRMF_E_INVALID, "need user_num, item_num >= 0 and n_factors > 0");
   if (cfg->n_factors > 1024) return fail(BPRMF_E_UNSUPPORTED, "n_factors must be <= 1024");
-  if (cfg->model != MF_SVD && cfg->model != MF_RSVD) return fail(BPRMF_E_INVALID, "unknown model");
+  if (cfg->model != MF_SVD && cfg->model != MF_RSVD && cfg->model != MF_SVDPP)
+    return fail(BPRMF_E_INVALID, "unknown model");
   if (cfg->model == MF_RSVD && cfg->variant != 1 && cfg->variant != 2)
     return fail(BPRMF_E_INVALID, "RSVD version must be 1 or 2");
   if (cfg->user_num >= INT32_MAX || cfg->item_num >= INT32_MAX)
@@ -91,11 +156,13 @@ int mf_create(const mf_config* cfg, mf_handle** out) {
   const int64_t k = cfg->n_factors;
   if ((rc = malloc_dev(&h->P, cfg->user_num * k)) || (rc = malloc_dev(&h->Q, cfg->item_num * k)) ||
       (rc = malloc_dev(&h->bu, cfg->user_num)) || (rc = malloc_dev(&h->bi, cfg->item_num)) ||
-      (rc = malloc_dev(&h->d_err, 1)))
+      (rc = malloc_dev(&h->d_err, 1)) ||
+      (cfg->model == MF_SVDPP && (rc = malloc_dev(&h->Y, cfg->item_num * k))))
     return bail(rc);
   auto z = [&](void* p, size_t bytes) { return p && bytes ? hipMemset(p, 0, bytes) : hipSuccess; };
   if (z(h->P, 8 * cfg->user_num * k) || z(h->Q, 8 * cfg->item_num * k) ||
-      z(h->bu, 8 * cfg->user_num) || z(h->bi, 8 * cfg->item_num) || z(h->d_err, 4))
+      z(h->bu, 8 * cfg->user_num) || z(h->bi, 8 * cfg->item_num) || z(h->d_err, 4) ||
+      z(h->Y, 8 * cfg->item_num * k))
     return bail(fail(BPRMF_E_HIP, "hipMemset failed"));
   *out = h;
   return 0;
@@ -105,7 +172,8 @@ int mf_destroy(mf_handle* h) {
   if (!h) return 0;
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  void* ptrs[] = {h->P, h->Q, h->bu, h->bi, h->su, h->si, h->sr, h->loff, h->d_err};
+  void* ptrs[] = {h->P,  h->Q,    h->bu,   h->bi,     h->su,   h->si,  h->sr,
+                  h->loff, h->d_err, h->Y, h->uoff, h->uitems, h->udup, h->uslot};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
@@ -121,6 +189,7 @@ int mf_set_train(mf_handle* h, const int32_t* users, const int32_t* items, const
   if (n >= INT32_MAX) return fail(BPRMF_E_UNSUPPORTED, "at most 2^31 - 1 train rows");
   if (int r = mset_dev(h)) return r;
   const int64_t U = h->cfg.user_num, I = h->cfg.item_num;
+  if (h->cfg.model == MF_SVDPP) return set_train_svdpp(h, users, items, ratings, n, global_mean);
   // dependency levels, in train-set order
   std::vector<int32_t> lu(U, -1), li(I, -1), lvl(n);
   int32_t L = 0;
@@ -188,6 +257,25 @@ int mf_get_weights(mf_handle* h, double* P, double* Q, double* bu, double* bi) {
   return 0;
 }
 
+int mf_set_implicit(mf_handle* h, const double* Y) {
+  if (!h || !Y) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.model != MF_SVDPP) return fail(BPRMF_E_STATE, "only SVDpp has an implicit table");
+  if (int r = mset_dev(h)) return r;
+  const int64_t bytes = 8 * h->cfg.item_num * h->cfg.n_factors;
+  if (bytes) HIPCHK(hipMemcpy(h->Y, Y, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mf_get_implicit(mf_handle* h, double* Y) {
+  if (!h || !Y) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (h->cfg.model != MF_SVDPP) return fail(BPRMF_E_STATE, "only SVDpp has an implicit table");
+  if (int r = mset_dev(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int64_t bytes = 8 * h->cfg.item_num * h->cfg.n_factors;
+  if (bytes) HIPCHK(hipMemcpy(Y, h->Y, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int mf_fit(mf_handle* h, int32_t epochs, mf_stats* st) {
   if (!h || epochs < 0) return fail(BPRMF_E_INVALID, "bad arguments");
   if (int r = mset_dev(h)) return r;
@@ -210,6 +298,7 @@ int mf_predict(mf_handle* h, const int32_t* users, const int32_t* items, int64_t
   if (!h || n < 0 || (n > 0 && (!users || !items || !out))) return fail(BPRMF_E_INVALID, "bad arguments");
   if (!n) return 0;
   if (int r = mset_dev(h)) return r;
+  if (h->cfg.model == MF_SVDPP && !h->uoff) return fail(BPRMF_E_STATE, "SVDpp predict needs the train set");
   int32_t *du = nullptr, *di = nullptr;
   double* dout = nullptr;
   int rc = 0;

@@ -1,6 +1,7 @@
-"""SVD / RSVD — drop-ins for the reference's Cython rating-SGD models.
+"""SVD / RSVD / SVDpp — drop-ins for the reference's Cython rating-SGD models.
 
-`util/matrix_factorization.pyx` SVD (:81-167) and RSVD (:5-78): the same constructor arguments,
+`util/matrix_factorization.pyx` SVD (:81-167), RSVD (:5-78) and SVDpp (:169-287): the same
+constructor arguments,
 `fit(train_set)` with a DataFrame[user, item, rating] and `predict(u, i)` raising
 ValueError('Invalid user code' / 'Invalid item code').  fit() draws the initial tables from
 numpy's global RNG exactly as the reference does (np.random.normal, users then items) and
@@ -19,14 +20,14 @@ class MfConfig(ctypes.Structure):  # mf_config, include/mf.h
                 ("n_factors", ctypes.c_int32), ("model", ctypes.c_int32),
                 ("variant", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("lr", ctypes.c_double * 4), ("reg", ctypes.c_double * 4),
-                ("reserved", ctypes.c_int32 * 4)]
+                ("lr_yj", ctypes.c_double), ("reg_yj", ctypes.c_double)]
 
 
 class MfStats(ctypes.Structure):  # mf_stats
     _fields_ = [("samples", ctypes.c_int64), ("levels", ctypes.c_int64), ("seconds", ctypes.c_double)]
 
 
-MF_SVD, MF_RSVD = 0, 1
+MF_SVD, MF_RSVD, MF_SVDPP = 0, 1, 2
 
 
 def _rows(train_set):
@@ -47,10 +48,11 @@ def _rows(train_set):
 class _MF:
     _model = MF_SVD
 
-    def _open(self, user_num, item_num, n_factors, variant, lr, reg, device):
+    def _open(self, user_num, item_num, n_factors, variant, lr, reg, device, lr_yj=0.0, reg_yj=0.0):
         self._L = _lib.load()
         cfg = MfConfig(user_num=int(user_num), item_num=int(item_num), n_factors=int(n_factors),
-                       model=self._model, variant=int(variant), device=int(device))
+                       model=self._model, variant=int(variant), device=int(device),
+                       lr_yj=float(lr_yj), reg_yj=float(reg_yj))
         for x in range(4):
             cfg.lr[x] = float(lr[x])
             cfg.reg[x] = float(reg[x])
@@ -175,3 +177,80 @@ class RSVD(_MF):
         if self.version == 2:
             return self.ci[i] + self.dj[j] + np.dot(self.ui[i], self.vj[j])
         return np.dot(self.ui[i], self.vj[j])
+
+
+class SVDpp(_MF):
+    """util/matrix_factorization.pyx:169-287 (SVD++: implicit feedback y_j of the user's items).
+
+    fit() draws pu, qi, yj from numpy's global RNG as the reference does (:218-221); the epochs
+    run on the device sample by sample (include/mf.h), bit-identical to the Cython loop.
+    """
+    _model = MF_SVDPP
+
+    def __init__(self, user_num, item_num, n_factors=20, n_epochs=20, init_mean=0, init_std_dev=.1,
+                 lr_all=.007, reg_all=.02, lr_bu=None, lr_bi=None, lr_pu=None, lr_qi=None,
+                 lr_yj=None, reg_bu=None, reg_bi=None, reg_pu=None, reg_qi=None, reg_yj=None,
+                 random_state=None, verbose=True, device=0):
+        self.user_num, self.item_num = user_num, item_num
+        self.n_factors, self.n_epochs = n_factors, n_epochs
+        self.init_mean, self.init_std_dev = init_mean, init_std_dev
+        pick = lambda v: v if v is not None else lr_all  # noqa: E731
+        self.lr_bu, self.lr_bi, self.lr_pu, self.lr_qi, self.lr_yj = (
+            pick(lr_bu), pick(lr_bi), pick(lr_pu), pick(lr_qi), pick(lr_yj))
+        pick = lambda v: v if v is not None else reg_all  # noqa: E731
+        self.reg_bu, self.reg_bi, self.reg_pu, self.reg_qi, self.reg_yj = (
+            pick(reg_bu), pick(reg_bi), pick(reg_pu), pick(reg_qi), pick(reg_yj))
+        self.random_state, self.verbose = random_state, verbose
+        self._open(user_num, item_num, n_factors, 1,
+                   (self.lr_bu, self.lr_bi, self.lr_pu, self.lr_qi),
+                   (self.reg_bu, self.reg_bi, self.reg_pu, self.reg_qi), device,
+                   self.lr_yj, self.reg_yj)
+
+    def fit(self, train_set):
+        U, I, k = self.user_num, self.item_num, self.n_factors
+        pu = np.random.normal(self.init_mean, self.init_std_dev, size=(U, k))
+        qi = np.random.normal(self.init_mean, self.init_std_dev, size=(I, k))
+        yj = np.random.normal(self.init_mean, self.init_std_dev, size=(I, k))
+        u, i, r, _ = _rows(train_set)
+        Y = np.ascontiguousarray(yj, np.float64)
+        # ur (:222-224): each user's (item, rating) in train order
+        self.ur = {}
+        for a, b, c in zip(u.tolist(), i.tolist(), r.tolist()):
+            self.ur.setdefault(a, []).append((b, c))
+        if self.verbose:
+            for epoch in range(self.n_epochs):
+                print(f'processing epoch {epoch + 1}')
+        # the tables and the train set go up first, then yj, then the epochs
+        self._train_with_implicit(train_set, pu, qi, Y)
+        return self
+
+    def _train_with_implicit(self, train_set, pu, qi, Y):
+        u, i, r, gm = _rows(train_set)
+        _lib.check(self._L.mf_set_train(self._h, _lib.ptr(u), _lib.ptr(i), _lib.ptr(r), len(u),
+                                        ctypes.c_double(gm)))
+        P0 = np.ascontiguousarray(pu, np.float64)
+        Q0 = np.ascontiguousarray(qi, np.float64)
+        _lib.check(self._L.mf_set_weights(self._h, _lib.ptr(P0), _lib.ptr(Q0), None, None))
+        _lib.check(self._L.mf_set_implicit(self._h, _lib.ptr(Y)))
+        st = MfStats()
+        _lib.check(self._L.mf_fit(self._h, int(self.n_epochs), ctypes.byref(st)))
+        self.last_stats = dict(samples=st.samples, levels=st.levels, seconds=st.seconds)
+        U, I, k = self.user_num, self.item_num, self.n_factors
+        self.pu, self.qi, self.yj = np.empty((U, k)), np.empty((I, k)), np.empty((I, k))
+        self.bu, self.bi = np.empty(U), np.empty(I)
+        _lib.check(self._L.mf_get_weights(self._h, _lib.ptr(self.pu), _lib.ptr(self.qi),
+                                          _lib.ptr(self.bu), _lib.ptr(self.bi)))
+        _lib.check(self._L.mf_get_implicit(self._h, _lib.ptr(self.yj)))
+        self.global_mean = gm
+
+    def predict(self, u, i):
+        est = self.global_mean
+        self._check_ids(u, i)
+        est += self.bu[u] + self.bi[i]
+        Iu = len(self.ur.get(u, []))
+        if Iu == 0:
+            u_impl_feedback = 0
+        else:
+            u_impl_feedback = (sum(self.yj[j] for (j, _) in self.ur[u]) / np.sqrt(Iu))
+        est += np.dot(self.qi[i], self.pu[u] + u_impl_feedback)
+        return est

@@ -51,8 +51,9 @@ def test_config_layout_matches_header(rl):
     # int64 x2, int32 x5, float x5, uint64 (offset 56), int32, int32[4] -> 84, padded to 88
     assert ctypes.sizeof(rl._lib.NcfConfig) == 88
     assert rl._lib.NcfConfig.seed.offset == 56
-    # int64 x2, int32 x4, double[4] x2 (offset 32, 64), int32[4] -> 112
+    # int64 x2, int32 x4, double[4] x2 (offset 32, 64), double x2 (lr_yj, reg_yj) -> 112
     from importlib import import_module
     mf = import_module("recommend-lib_amd.mf")
     assert ctypes.sizeof(mf.MfConfig) == 112 and mf.MfConfig.lr.offset == 32
+    assert mf.MfConfig.lr_yj.offset == 96 and mf.MfConfig.reg_yj.offset == 104
     assert ctypes.sizeof(mf.MfStats) == 24

@@ -26,7 +26,7 @@ namespace bprmf {
 namespace sgns {
 
 constexpr int kT = 256;  // 4 waves, one example each
-constexpr int kU = 8;    // ovectors rows in flight per wave (wave_sum8 reduces 8 at once)
+constexpr int kU = 8;    // ovectors rows in flight per wave (a multiple of 8: wave_sum8 groups)
 constexpr int kMaxR = 1024;  // references per example (C (1 + n)), staged in LDS
 constexpr uint32_t TAG_SGNS = 0x53474E00u;
 
@@ -108,38 +108,47 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
   for (int r0 = 0; r0 < R; r0 += kU) {
     int32_t w[kU];
     float ov[kU][M], p[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) w[u] = r0 + u < R ? wsh[wv][r0 + u] : -1;
+    // the words are wave-uniform: scalar row addresses, unguarded loads (lanes past E read the
+    // row's tail or the next row, or the table's padding row: they meet iv = 0 and are never
+    // stored); past R, row 0 with a zero coefficient
 #pragma unroll
     for (int u = 0; u < kU; ++u)
+      w[u] = __builtin_amdgcn_readfirstlane(r0 + u < R ? wsh[wv][r0 + u] : 0);
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int e = lane + 64 * m;
-        ov[u][m] = (w[u] >= 0 && e < a.E) ? a.O[(int64_t)w[u] * a.ld + e] : 0.f;
-      }
+    for (int u = 0; u < kU; ++u) {
+      const float* row = a.O + (int64_t)w[u] * a.ld;
+#pragma unroll
+      for (int m = 0; m < M; ++m) ov[u][m] = row[lane + 64 * m];
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       p[u] = 0.f;
 #pragma unroll
       for (int m = 0; m < M; ++m) p[u] += iv[m] * ov[u][m];
     }
-    const float sdot = wave_sum8(p, lane);  // o . i of reference r0 + mine
-    const int r = r0 + mine;
-    float g = 0.f;
-    if (r < R) {
-      const bool ctx = r < C;
-      const float sig = 1.0f / (1.0f + __expf(-sdot));
-      g = ctx ? -(1.0f - sig) * inv : sig * inv;
-      if ((lane & 7) == 0) {
-        lsum += ctx ? softplus(-sdot) : softplus(sdot);
-        gsh[wv][r] = g;
+#pragma unroll
+    for (int gg = 0; gg < kU / 8; ++gg) {
+      float p8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p8[j] = p[8 * gg + j];
+      const float sdot = wave_sum8(p8, lane);  // o . i of reference r0 + 8 gg + mine
+      const int r = r0 + 8 * gg + mine;
+      float g = 0.f;
+      if (r < R) {
+        const bool ctx = r < C;
+        const float sig = 1.0f / (1.0f + __expf(-sdot));
+        g = ctx ? -(1.0f - sig) * inv : sig * inv;
+        if ((lane & 7) == 0) {
+          lsum += ctx ? softplus(-sdot) : softplus(sdot);
+          gsh[wv][r] = g;
+        }
       }
-    }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const float gu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), 8 * u));
+      for (int j = 0; j < 8; ++j) {
+        const float gu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), 8 * j));
 #pragma unroll
-      for (int m = 0; m < M; ++m) gi[m] += gu * ov[u][m];
+        for (int m = 0; m < M; ++m) gi[m] += gu * ov[8 * gg + j][m];
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -137,9 +137,11 @@ int sgns_create(const sgns_config* cfg, sgns_handle** out) {
       rocblas_set_stream(h->blas, h->stream) != rocblas_status_success)
     return bail(fail(BPRMF_E_HIP, "rocblas handle creation failed"));
   const int64_t V = cfg->vocab_size, ld = h->ld, B = cfg->max_batch;
-  float** tabs[] = {&h->I, &h->O, &h->mI, &h->vI, &h->mO, &h->vO, &h->GI, &h->GO};
+  float** tabs[] = {&h->I, &h->mI, &h->vI, &h->mO, &h->vO, &h->GI, &h->GO};
   for (float** p : tabs)
     if ((rc = zalloc(p, V * ld))) return bail(rc);
+  // ovectors: one padding row of 1024 floats past the end (sgns.hip reads whole 64-lane strides)
+  if ((rc = zalloc(&h->O, V * ld + 1024))) return bail(rc);
   if ((rc = zalloc(&h->GOp, (int64_t)kMaxSplit * V * ld)) || (rc = zalloc(&h->S, V * B)) || (rc = zalloc(&h->IB, B * ld)) || (rc = zalloc(&h->lbuf, B)) ||
       (rc = zalloc(&h->touch_i, V)) || (rc = zalloc(&h->touch_o, V)) || (rc = zalloc(&h->loss, 1)))
     return bail(rc);

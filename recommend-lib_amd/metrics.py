@@ -49,10 +49,28 @@ def _bpr_topk(model, test_loader, top_k):
     return np.mean(HR), np.mean(NDCG)
 
 
+def _ncf_topk(model, test_loader, top_k):
+    """util/metrics.py:68-86: each batch is one user's [ground truth, negatives] with labels;
+    model(user, item) scores them (NCF.forward, on the device)."""
+    import torch
+    HR, NDCG = [], []
+    for user, item, _ in test_loader:  # _ is the label
+        predictions = torch.as_tensor(model(user, item)).reshape(-1).cpu()
+        _, indices = torch.topk(predictions, top_k)
+        recommends = torch.take(torch.as_tensor(item).cpu(), indices).numpy().tolist()
+        gt_item = int(torch.as_tensor(item).reshape(-1)[0])
+        HR.append(_hit(gt_item, recommends))
+        NDCG.append(_ndcg(gt_item, recommends))
+    return np.mean(HR), np.mean(NDCG)
+
+
 def metric_eval(model, test_loader, top_k, algo="bpr"):
-    if algo != "bpr":
-        raise ValueError("only algo='bpr' is part of this path")
-    return _bpr_topk(model, test_loader, top_k)
+    """util/metrics.py:88-97 (algo 'bpr' or 'ncf')."""
+    if algo == "bpr":
+        return _bpr_topk(model, test_loader, top_k)
+    if algo == "ncf":
+        return _ncf_topk(model, test_loader, top_k)
+    raise ValueError(f"unknown algo {algo!r}")
 
 
 def precision_at_k(r, k):

@@ -162,3 +162,22 @@ def test_hr_ndcg_fixture_is_consistent():
     assert 0 < s["hr"]["mean"] < 1 and s["hr"]["std"] < 0.2 * s["hr"]["mean"]
     f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
     assert f["test_data"].shape[1] == 2 and len(f["gt_users"]) == len(f["gt_ptr"]) - 1
+
+
+def test_metric_eval_ncf_ranks_each_batch(rl):
+    """metric_eval(algo='ncf') (util/metrics.py:68-97) with a scoring stub: the ground truth sits
+    first in each batch; HR / NDCG follow its rank among the top-k."""
+    import torch
+
+    class Stub:  # scores = -item, so smaller ids rank first
+        def __call__(self, user, item):
+            return -torch.as_tensor(item, dtype=torch.float32)
+
+    batches = [(torch.zeros(5, dtype=torch.long), torch.tensor([3, 9, 1, 7, 5]), torch.zeros(5)),
+               (torch.ones(5, dtype=torch.long), torch.tensor([0, 9, 1, 7, 5]), torch.zeros(5))]
+    hr, ndcg = rl.metrics.metric_eval(Stub(), batches, 2, algo="ncf")
+    # batch 1: top-2 = [1, 3] -> hit at rank 1; batch 2: top-2 = [0, 1] -> hit at rank 0
+    assert hr == 1.0
+    assert ndcg == pytest.approx((1 / np.log2(3) + 1.0) / 2)
+    with pytest.raises(ValueError):
+        rl.metrics.metric_eval(Stub(), batches, 2, algo="nfm")

@@ -11,7 +11,7 @@
 // Layout: G lanes per triplet (G = next_pow2(k) <= 64), one factor per lane; TPB = 256 / G
 // triplets per workgroup.  Kernels of one step (BN on):
 //   k_fm_fwd    fm rows of both sides -> X; per-workgroup sums of fm and fm^2 (double; at most
-//               512 workgroups striding over the batch)
+//               256 workgroups striding over the batch)
 //   k_fm_stats  batch mean / 1/sqrt(var + eps) per side (fixed-order sum of the partials, one
 //               workgroup per 4 factors), and the running statistics (momentum 0.1, unbiased variance; i side,
 //               then j side)
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kT) void k_fm_fwd(Args a, int nb) {
 // 64); chunk c holds partials c, c + 64, ... (8 loads issued together), then an LDS tree over the
 // chunks.  sums[q][e - 4w] for e < k on return.
 constexpr int kRT = 1024;
-constexpr int kMaxParts = 512;
+constexpr int kMaxParts = 256;
 static __device__ void reduce_parts(const Args& a, int nblk, double (*sums)[4]) {
   __shared__ double red[64][16];
   const int p = threadIdx.x & 15, c = threadIdx.x >> 4;

@@ -227,6 +227,7 @@ __global__ __launch_bounds__(kT) void k_fm_mid(Args a, int nb) {
     }
   }
   double v[4] = {0.0, 0.0, 0.0, 0.0};
+  double lsum = 0.0;  // this lane group's loss terms (lane 0)
   for (int t = blockIdx.x * TPB + slot; t < a.B; t += nb * TPB) {  // uniform per lane group
     const int64_t u = a.u[t], xi = a.i[t], xj = a.j[t];
     float xh[2] = {0.f, 0.f}, m[2] = {0.f, 0.f}, yv[2] = {0.f, 0.f};
@@ -245,7 +246,10 @@ __global__ __launch_bounds__(kT) void k_fm_mid(Args a, int nb) {
     const float pj = (yj + (bu + a.b[xj])) + *a.bias_;
     const float d = pi - pj;
     const float c = 1.0f / (1.0f + expf(d));
-    if (lane == 0) a.cbuf[t] = d;
+    if (lane == 0) {
+      a.cbuf[t] = d;
+      lsum += (double)softplus(-d);
+    }
     // dL/dy = -c (i side), +c (j side), through the dropout mask
     const float gi = act ? -c * m[0] : 0.f, gj = act ? c * m[1] : 0.f;
     v[0] += gi;
@@ -254,11 +258,33 @@ __global__ __launch_bounds__(kT) void k_fm_mid(Args a, int nb) {
     v[3] += (double)gj * xh[1];
   }
   block_sums<G, 4>(v, a.part + (int64_t)blockIdx.x * 4 * a.ld, a.ld);
+  // the workgroup's loss, its lane groups in slot order -> lpart (k_fm_stats2 adds those)
+  __shared__ double lred[TPB];
+  if (lane == 0) lred[slot] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int q = 0; q < TPB; ++q) s += lred[q];
+    a.lpart[blockIdx.x] = s;
+  }
+}
+
+// the step's loss from k_fm_mid's per-workgroup sums, fixed order (workgroup 0 of k_fm_stats2)
+static __device__ void loss_parts(const Args& a, int nblk) {
+  __shared__ double lr2[kRT];
+  lr2[threadIdx.x] = (int)threadIdx.x < nblk ? a.lpart[threadIdx.x] : 0.0;
+  __syncthreads();
+  for (int h = kRT / 2; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) lr2[threadIdx.x] += lr2[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.loss[0] += lr2[0];
 }
 
 // sums of gy and gy * xhat per side; dgamma / dbeta (the module serves both sides)
 __global__ __launch_bounds__(kRT) void k_fm_stats2(Args a, int nblk) {
   __shared__ double sums[4][4];
+  if (blockIdx.x == 0) loss_parts(a, nblk);  // (block-uniform)
   reduce_parts(a, nblk, sums);
   const int el = threadIdx.x, e = blockIdx.x * 4 + el;
   if (el >= 4 || e >= a.k) return;
@@ -266,6 +292,7 @@ __global__ __launch_bounds__(kRT) void k_fm_stats2(Args a, int nblk) {
   a.gbeta[e] = (float)(sums[0][el] + sums[2][el]);
   a.ggamma[e] = (float)(sums[1][el] + sums[3][el]);
 }
+
 
 template <int G>
 __global__ __launch_bounds__(kT) void k_fm_back(Args a) {
@@ -356,7 +383,7 @@ __global__ __launch_bounds__(kT) void k_fm_apply(Args a) {
   constexpr int TPB = kT / G;
   const int lane = threadIdx.x & (G - 1);
   const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x / G;
-  if (blockIdx.x == 0) loss_sum(a);  // (block-uniform: every thread of block 0 reaches it)
+  if (blockIdx.x == 0 && !a.bn) loss_sum(a);  // (BN on: k_fm_mid / k_fm_stats2 sum it)
   if (blockIdx.x == 0 && a.bn && threadIdx.x < a.k) {  // gamma, beta
     const int e = threadIdx.x;
     const float g1 = a.ggamma[e], g2 = a.gbeta[e];

@@ -25,7 +25,7 @@ struct bprfm_handle {
   float* bn = nullptr;  // [8, ld]: gamma, beta, acc_gamma, acc_beta, ggamma, gbeta, run mean, run var
   float* bias_ = nullptr;
   float *X = nullptr, *stats = nullptr, *stats2 = nullptr, *cbuf = nullptr, *mask = nullptr;
-  double *part = nullptr, *loss = nullptr;
+  double *part = nullptr, *loss = nullptr, *lpart = nullptr;
   int32_t* trip = nullptr;  // [3, cap] uploaded triplets
   int64_t cap = 0;
   int64_t steps = 0;
@@ -87,6 +87,7 @@ fm::Args args_of(const bprfm_handle* h, int B) {
   a.stats2 = h->stats2;
   a.cbuf = h->cbuf;
   a.loss = h->loss;
+  a.lpart = h->lpart;
   return a;
 }
 // a 2D copy between dense [rows, k] host rows and the padded [rows, ld] device rows
@@ -137,7 +138,7 @@ int bprfm_create(const bprfm_config* cfg, bprfm_handle** out) {
       (rc = zalloc(&h->bias_, 1)) || (rc = zalloc(&h->X, 2 * B * ld)) ||
       (rc = zalloc(&h->stats, 4 * ld)) || (rc = zalloc(&h->stats2, 4 * ld)) ||
       (rc = zalloc(&h->cbuf, B)) || (rc = zalloc(&h->part, nblk * 4 * ld)) ||
-      (rc = zalloc(&h->loss, 1)))
+      (rc = zalloc(&h->loss, 1)) || (rc = zalloc(&h->lpart, nblk)))
     return bail(rc);
   // Adagrad state (initial_accumulator_value 1e-8), BatchNorm weight 1 / running var 1
   if ((rc = fill(h->acc_E, 1e-8f, F * ld)) || (rc = fill(h->acc_b, 1e-8f, F)) ||
@@ -157,7 +158,7 @@ int bprfm_destroy(bprfm_handle* h) {
   hipSetDevice(h->cfg.device);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* ptrs[] = {h->E,  h->acc_E, h->GE,     h->b,    h->acc_b, h->Gb,   h->stamp, h->bn,
-                  h->bias_, h->X, h->stats, h->stats2, h->cbuf, h->mask, h->part, h->loss, h->trip};
+                  h->bias_, h->X, h->stats, h->stats2, h->cbuf, h->mask, h->part, h->loss, h->lpart, h->trip};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

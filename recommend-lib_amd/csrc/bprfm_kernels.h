@@ -29,6 +29,7 @@ struct Args {
   float* stats2;                  // [(sum gy_i, sum gy_i xhat_i, sum gy_j, sum gy_j xhat_j), ld]
   float* cbuf;                    // [B] pred_i - pred_j
   double* loss;                   // [1] accumulated loss
+  double* lpart;                  // [blocks] per-workgroup loss sums of k_fm_mid
 };
 
 int lanes_for(int k);                 // lanes (and row stride) per triplet: next_pow2(k) <= 64

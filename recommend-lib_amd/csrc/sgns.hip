@@ -9,9 +9,9 @@
 // segments), each dot reduced across the wave; the centre row's gradient sum_r g_r o_r stays in
 // registers and is added into GI with f32 atomics; g_r goes into S[word, b] after the loop.  The
 // ovectors gradient is then a GEMM, GO [V, E] = S [V, B] x IB [B, E] (rocBLAS, split over B into
-// partial products that k_sgns_sum_parts adds, sgns_capi.cpp), and both tables take a dense Adam
-// sweep (ncf.hip
-// adam_rows: rows never touched keep m = v = 0 and are skipped, exactly as torch leaves them).
+// partial products, sgns_capi.cpp), and k_sgns_post gives both tables a dense Adam sweep (rows
+// never touched keep m = v = 0 and are skipped, exactly as torch leaves them), summing the
+// partials on the way, clears S and adds the loss.
 // Row 0 is nn.Embedding's padding_idx: it gets no gradient.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "ncf_kernels.h"
 #include "sgns_kernels.h"
 
 namespace bprmf {
@@ -175,30 +176,6 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
   if (lane == 0) a.lbuf[b] = lsum * inv;
 }
 
-// the batch's loss, fixed order (one workgroup, 16 loads per thread in flight)
-__global__ __launch_bounds__(kT) void k_sgns_loss(Args a) {
-  constexpr int R = 16;
-  __shared__ double red[kT];
-  double s = 0.0;
-  for (int t0 = 0; t0 < a.B; t0 += kT * R) {
-    float v[R];
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      const int t = t0 + m * kT + threadIdx.x;
-      v[m] = t < a.B ? a.lbuf[t] : 0.f;
-    }
-#pragma unroll
-    for (int m = 0; m < R; ++m) s += (double)v[m];
-  }
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int h = kT / 2; h >= 1; h >>= 1) {
-    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.loss[0] += red[0];
-}
-
 __global__ void k_sgns_negs(Args a, int32_t* __restrict__ out) {
   const int64_t CN = (int64_t)a.C * a.n, total = CN * a.B;
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
@@ -232,21 +209,87 @@ __global__ void k_sgns_lookup(const float* __restrict__ W, int ld, int E,
   }
 }
 
-// GO = sum of the nsplit partial products (fixed order), float4 rows
-__global__ void k_sgns_sum_parts(const float* __restrict__ parts, int nsplit, int64_t n4,
-                                 float* __restrict__ out) {
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4;
-       x += (int64_t)gridDim.x * blockDim.x) {
-    float4 acc = reinterpret_cast<const float4*>(parts)[x];
-    for (int q = 1; q < nsplit; ++q) {
-      const float4 v = reinterpret_cast<const float4*>(parts)[q * n4 + x];
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
+// torch Adam (single-tensor form), as ncf.hip's adam_rows: m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= step_size * m / (sqrt(v) / bc2_sqrt + eps)
+static __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g,
+                                             const ncf::AdamArgs& ad) {
+  m = m + ad.one_minus_b1 * (g - m);
+  v = fmaf(ad.b2, v, ad.one_minus_b2 * g * g);
+  p = p - ad.step_size * (m / (sqrtf(v) / ad.bc2_sqrt + ad.eps));
+}
+
+// everything after the GEMM in one launch, all of it elementwise: Adam on ivectors (gradient GI,
+// re-zeroed) and on ovectors (gradient = the nsp GEMM partials summed in order, or GO itself),
+// rows never touched skipped (m = v = 0: torch leaves them unchanged); S zeroed for the next
+// step; the last workgroup adds the batch's loss.
+__global__ __launch_bounds__(256) void k_sgns_post(Args a, const float* __restrict__ parts, int nsp,
+                                                   ncf::AdamArgs ad, float* __restrict__ mI,
+                                                   float* __restrict__ vI, float* __restrict__ mO,
+                                                   float* __restrict__ vO) {
+  if (blockIdx.x == gridDim.x - 1) {  // the loss, fixed order (block-uniform branch)
+    constexpr int R = 16;
+    __shared__ double red[256];
+    double sum = 0.0;
+    for (int t0 = 0; t0 < a.B; t0 += 256 * R) {
+      float v[R];
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        const int t = t0 + m * 256 + threadIdx.x;
+        v[m] = t < a.B ? a.lbuf[t] : 0.f;
+      }
+#pragma unroll
+      for (int m = 0; m < R; ++m) sum += (double)v[m];
     }
-    reinterpret_cast<float4*>(out)[x] = acc;
+    red[threadIdx.x] = sum;
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.loss[0] += red[0];
   }
+  // 4 elements (one float4, within one row: ld % 4 == 0) per thread and iteration
+  const int64_t n = a.V * a.ld, n4 = n / 4, stride = (int64_t)gridDim.x * blockDim.x;
+  const int ld4 = a.ld / 4;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < 2 * n4; x += stride) {
+    const bool o = x >= n4;
+    const int64_t y = o ? x - n4 : x;
+    const int32_t row = (int32_t)((uint32_t)y / (uint32_t)ld4);
+    const int32_t st = o ? a.touch_o[row] : a.touch_i[row];
+    if (st < 0) continue;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (st == a.t) {
+      if (o) {
+        g = reinterpret_cast<const float4*>(parts)[y];
+        for (int q = 1; q < nsp; ++q) {
+          const float4 v = reinterpret_cast<const float4*>(parts)[q * n4 + y];
+          g.x += v.x;
+          g.y += v.y;
+          g.z += v.z;
+          g.w += v.w;
+        }
+      } else {
+        g = reinterpret_cast<const float4*>(a.GI)[y];
+        reinterpret_cast<float4*>(a.GI)[y] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    float4* P = reinterpret_cast<float4*>(o ? a.O : a.I) + y;
+    float4* Mm = reinterpret_cast<float4*>(o ? mO : mI) + y;
+    float4* Vv = reinterpret_cast<float4*>(o ? vO : vI) + y;
+    float4 p = *P, m = *Mm, v = *Vv;
+    adam1(p.x, m.x, v.x, g.x, ad);
+    adam1(p.y, m.y, v.y, g.y, ad);
+    adam1(p.z, m.z, v.z, g.z, ad);
+    adam1(p.w, m.w, v.w, g.w, ad);
+    *P = p;
+    *Mm = m;
+    *Vv = v;
+  }
+  const int64_t s4 = a.V * a.B / 4;  // S for the next step (V * B is a multiple of 4: B % 4 below)
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < s4; x += stride)
+    reinterpret_cast<float4*>(a.S)[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t x = 4 * s4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < a.V * a.B; x += stride)
+    a.S[x] = 0.f;
 }
 
 static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
@@ -274,15 +317,12 @@ hipError_t forward_backward(const Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t sum_parts(const float* parts, int nsplit, int64_t n, float* out, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  k_sgns_sum_parts<<<grid_for(n / 4), 256, 0, s>>>(parts, nsplit, n / 4, out);
-  return hipGetLastError();
-}
-
-hipError_t loss_sum(const Args& a, hipStream_t s) {
+hipError_t post(const Args& a, const float* parts, int nsp, const ncf::AdamArgs& ad, float* mI,
+                float* vI, float* mO, float* vO, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
-  k_sgns_loss<<<1, kT, 0, s>>>(a);
+  const int64_t n = 2 * a.V * a.ld / 4;
+  const unsigned blocks = (unsigned)std::max<int64_t>(2, std::min<int64_t>((n + 255) / 256, 4096));
+  k_sgns_post<<<blocks, 256, 0, s>>>(a, parts, nsp, ad, mI, vI, mO, vO);
   return hipGetLastError();
 }
 

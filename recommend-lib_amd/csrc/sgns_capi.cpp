@@ -3,9 +3,9 @@
 //
 // One handle = one GPU: ivectors / ovectors [V, ld] (ld = E rounded up to 4 floats), their Adam
 // moments, the ivectors gradient, the per-row touch steps, and the step scratch sized for
-// max_batch: S [V, B] (the coefficient matrix of the ovectors gradient, zeroed per step),
-// IB [B, ld], GO [V, ld], per-example losses.  Per step: memset S, K1, GO = S x IB (sgemm), Adam
-// over both tables, the loss sum.
+// max_batch: S [V, B] (the coefficient matrix of the ovectors gradient, zero between steps),
+// IB [B, ld], GO [V, ld] or its split partials, per-example losses.  Per step: K1, the GEMM
+// (split over B), then one elementwise launch: Adam over both tables, S cleared, the loss sum.
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 
@@ -309,8 +309,7 @@ int sgns_train(sgns_handle* h, const int32_t* iwords, const int32_t* owords, con
     a.iw = d_iw + beg;
     a.ow = d_ow + beg * C;
     a.nw = nwords ? d_nw + beg * CN : nullptr;
-    HIPCHK(hipMemsetAsync(h->S, 0, 4 * (size_t)V * B, s));
-    HIPCHK(sgns::forward_backward(a, s));
+    HIPCHK(sgns::forward_backward(a, s));  // S is zero: at create, then after every step
     // GO^T [E, V] = IB^T [E, B] x S^T [B, V] in rocBLAS's column-major terms, as nsp products
     // over slices of B (slice q: columns q Bs.. of IB^T, rows of S^T) summed in a fixed order
     const int nsp = split_for(B), Bs = B / nsp, tail = B - Bs * nsp;
@@ -329,12 +328,10 @@ int sgns_train(sgns_handle* h, const int32_t* iwords, const int32_t* owords, con
                         tail, &one, h->IB + (int64_t)Bs * nsp * h->ld, h->ld, h->S + Bs * nsp, B,
                         &one, h->GOp + (int64_t)(nsp - 1) * V * h->ld, h->ld) != rocblas_status_success)
         return fail(BPRMF_E_HIP, "rocblas_sgemm failed");
-      HIPCHK(sgns::sum_parts(h->GOp, nsp, V * h->ld, h->GO, s));
     }
+    // Adam on both tables, S cleared, the loss: one launch
     const ncf::AdamArgs ad = adam_args(h, a.t);
-    HIPCHK(ncf::adam_rows(h->I, h->mI, h->vI, h->GI, h->touch_i, V, h->ld, a.t, ad, s));
-    HIPCHK(ncf::adam_rows(h->O, h->mO, h->vO, h->GO, h->touch_o, V, h->ld, a.t, ad, s));
-    HIPCHK(sgns::loss_sum(a, s));
+    HIPCHK(sgns::post(a, nsp == 1 ? h->GO : h->GOp, nsp, ad, h->mI, h->vI, h->mO, h->vO, s));
     ++h->t;
   }
   HIPCHK(hipEventRecord(h->ev1, s));

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ncf_kernels.h"
+
 namespace bprmf {
 namespace sgns {
 
@@ -26,9 +28,10 @@ int lanes_elems(int E);  // factors per lane of the one-wave-per-example layout 
 hipError_t init_uniform(float* W, int64_t V, int E, int ld, float lim, uint64_t seed, uint32_t tag,
                         hipStream_t s);
 hipError_t forward_backward(const Args& a, hipStream_t s);  // K1: dots, coefficients, GI, S, IB
-hipError_t loss_sum(const Args& a, hipStream_t s);  // the batch's loss into loss[0]
-// out[x] = sum_q parts[q n + x] (n a multiple of 4), q in fixed order
-hipError_t sum_parts(const float* parts, int nsplit, int64_t n, float* out, hipStream_t s);
+// after the GEMM: Adam on both tables (ovectors' gradient = the nsp partials summed in order),
+// S zeroed for the next step, the batch's loss into loss[0]
+hipError_t post(const Args& a, const float* parts, int nsp, const ncf::AdamArgs& ad, float* mI,
+                float* vI, float* mO, float* vO, hipStream_t s);
 hipError_t negatives(const Args& a, int32_t* out, hipStream_t s);  // [B, C * n] draws of step t
 hipError_t lookup(const float* W, int ld, int E, const int32_t* idx, int64_t n, float* out,
                   hipStream_t s);

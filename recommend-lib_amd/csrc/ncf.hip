@@ -324,9 +324,10 @@ __global__ __launch_bounds__(256) void k_ncf_adam_rows(float* __restrict__ W, fl
                                                        int64_t rows, int dim, int32_t t, AdamArgs a) {
   const int q = dim / 4;
   const int64_t total = rows * q;
+  const bool narrow = total < (1LL << 31);  // 32-bit row division (a 64-bit one costs ~40 VALU)
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
        x += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = x / q;
+    const int64_t r = narrow ? (int64_t)((uint32_t)x / (uint32_t)q) : x / q;
     const int32_t st = touch[r];
     if (st < 0) continue;  // never touched: m = v = 0, torch's step leaves it unchanged
     const int64_t e = r * dim + 4 * (x - r * q);

@@ -193,3 +193,23 @@ def test_fit_epoch_over_bprfm_data(rl):
     np.random.seed(3)
     loss = m.fit_epoch(d, batch_size=8)
     assert np.isfinite(loss) and m.steps == 3 and m.last_stats["triplets"] == 18
+
+
+@pytest.mark.parametrize("k,bn", [(1, True), (5, False), (33, True), (64, False)])
+def test_factor_widths_against_oracle(rl, k, bn):
+    """Lane groups of every width (G = next_pow2(k): 1, 8, 64, 64): two steps with dropout replayed."""
+    g = np.random.default_rng(k)
+    U, I, B = 50, 70, 96
+    E = (0.05 * g.standard_normal((U + I, k))).astype(np.float32)
+    m = rl.BPRFM(U + I, k, bn, [0.3], lr=0.05, max_batch=B, seed=k)
+    m.load_state_dict({"embeddings.weight": E})
+    st = O.State(E, np.zeros(U + I), np.zeros(1), np.ones(k) if bn else None,
+                 np.zeros(k) if bn else None)
+    for _ in range(2):
+        u, i, j = g.integers(0, U, B), U + g.integers(0, I, B), U + g.integers(0, I, B)
+        masks = m.dropout_mask(B).astype(np.float64)
+        want = O.step(st, 0, u, i, j, 0.05, masks=masks)
+        got = m.train_triplets(u, i, j)
+        assert got == pytest.approx(want, rel=LOSS_RTOL)
+    check_params(m.state_dict(), st.E, st.b, st.bias_,
+                 *((st.gamma, st.beta, st.run_mean, st.run_var) if bn else ()))

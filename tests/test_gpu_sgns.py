@@ -150,3 +150,24 @@ def test_epoch_over_corpus_and_bad_inputs(rl):
     with pytest.raises(ValueError):
         s.train_examples([1], np.zeros((1, 4)), batch_size=129)
     assert s.train_examples(np.zeros(0), np.zeros((0, 4))) == 0.0
+
+
+@pytest.mark.parametrize("E,C,n", [(1, 2, 1), (64, 4, 0), (130, 6, 3), (1024, 2, 2)])
+def test_embedding_widths_against_oracle(rl, E, C, n):
+    """Every lanes-per-wave width (ceil(E/64) = 1, 1, 3, 16), no negatives, odd widths."""
+    import torch
+    g = np.random.default_rng(E)
+    V, B = 90, 40
+    torch.manual_seed(E)
+    m = rl.Item2Vec(V, E)
+    s = rl.SGNS(m, V, n_negs=n, context=C, max_batch=B)
+    st = O.State(*m._init)
+    for _ in range(2):
+        iw, ow = g.integers(0, V, B), g.integers(0, V, (B, C))
+        nw = s.negatives(B) if n else np.zeros((B, 0), np.int64)
+        want = O.step(st, iw, ow, nw)
+        got = s.train_examples(iw, ow)
+        assert got == pytest.approx(want, rel=LOSS_RTOL)
+    sd = s.state_dict()
+    np.testing.assert_allclose(sd["embedding.ivectors.weight"], st.I, rtol=0, atol=PARAM_ATOL)
+    np.testing.assert_allclose(sd["embedding.ovectors.weight"], st.O, rtol=0, atol=PARAM_ATOL)

@@ -140,7 +140,8 @@ __global__ __launch_bounds__(kT) void k_sgns_fwd(Args a) {
         const float sig = 1.0f / (1.0f + __expf(-sdot));
         g = ctx ? -(1.0f - sig) * inv : sig * inv;
         if ((lane & 7) == 0) {
-          lsum += ctx ? softplus(-sdot) : softplus(sdot);
+          const float z = ctx ? -sdot : sdot;  // softplus(z) on the fast exp / log
+          lsum += fmaxf(z, 0.f) + __logf(1.0f + __expf(-fabsf(z)));
           gsh[wv][r] = g;
         }
       }

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(kT) void k_fm_mid(Args a, int nb) {
     const float c = 1.0f / (1.0f + expf(d));
     if (lane == 0) {
       a.cbuf[t] = d;
-      lsum += (double)softplus(-d);
+      lsum += (double)(fmaxf(-d, 0.f) + __logf(1.0f + __expf(-fabsf(d))));  // softplus(-d), fast exp / log
     }
     // dL/dy = -c (i side), +c (j side), through the dropout mask
     const float gi = act ? -c * m[0] : 0.f, gj = act ? c * m[1] : 0.f;

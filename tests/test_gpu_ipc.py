@@ -86,7 +86,7 @@ def _loopback(rl, world, spec, mode, key):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world):
     U, I, D, GB, steps = 301, 157, 128, 512, 6
     g = np.random.default_rng(11)

@@ -33,7 +33,7 @@ def _run_threads(rl, world, fn):
     return out
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_sharded_replay_equals_single_gpu_global_batch(rl, world):
     g = np.random.default_rng(world)
     P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
@@ -165,7 +165,7 @@ def _batches(g, steps, GB, hot=True):
     return out
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_runner_replay_equals_single_gpu_global_batch(rl, world):
     g = np.random.default_rng(100 + world)
     P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)

@@ -30,18 +30,41 @@ def is_stale():
     return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
 
 
+def _compile(args):
+    cmd, src = args
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    return src, r.returncode, r.stdout + r.stderr
+
+
 def build(force=False, verbose=False):
+    """Compile every source to an object in parallel (objects outside the tree), then link."""
     if not force and not is_stale():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
+    obj_dir = os.environ.get("BPRMF_OBJ_DIR", os.path.join("/tmp", "bprmf_amd_obj"))
+    os.makedirs(obj_dir, exist_ok=True)
+    hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
+    jobs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
+            jobs.append(([hipcc()] + flags + ["-c", src, "-o", obj], src))
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8))
+    with ThreadPoolExecutor(workers) as ex:
+        for src, rc, out in ex.map(_compile, jobs):
+            if verbose:
+                print(f"compiled {src}", file=sys.stderr)
+            if rc != 0:
+                raise RuntimeError(f"hipcc failed on {src} ({rc}):\n{out}")
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
-           "-o", tmp] + SOURCES + ["-L/opt/rocm/lib", "-lrccl", "-lrocblas"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp] + objs + \
+          ["-L/opt/rocm/lib", "-lrccl", "-lrocblas"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
     return LIB
 

@@ -38,6 +38,7 @@ int fail(int code, const char* fmt, ...) {
 }  // namespace bprmf
 
 static void drop_graphs(bprmf_handle* h);
+static int ensure_step_graphs(bprmf_handle* h);
 
 // Profiling events skip the system-scope fence a default event record performs (an L2 write-back
 // that would otherwise land inside the measured interval: +2 us per kernel measured on gfx950).
@@ -147,8 +148,15 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
-  TRY(dalloc(&h->d_loss, kLossSlots));
-  TRY(dalloc(&h->d_err, 1));
+  const size_t status_bytes = 16 + sizeof(double) * kLossSlots;
+  TRY(dalloc(&h->d_status, (int64_t)status_bytes));
+  if (hipHostMalloc((void**)&h->h_status, status_bytes, hipHostMallocDefault) != hipSuccess) {
+    h->h_status = nullptr;
+    bprmf_destroy(h);
+    return fail(BPRMF_E_HIP, "hipHostMalloc failed");
+  }
+  h->d_err = reinterpret_cast<int32_t*>(h->d_status);
+  h->d_loss = reinterpret_cast<double*>(h->d_status + 16);
   h->P.rows = h->U;
   h->Q.rows = h->I;
   auto memz = [&](void* p, size_t bytes) -> int {
@@ -158,8 +166,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   };
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
-  TRY(memz(h->d_err, sizeof(int32_t)));
-  TRY(memz(h->d_loss, sizeof(double) * kLossSlots));
+  TRY(memz(h->d_status, status_bytes));
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size
   const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
   e = init_normal(g, h->P.W, h->U, cfg->init_std, s0, s1, 0u, (int)W, (int)R, h->stream);
@@ -179,13 +186,14 @@ int bprmf_destroy(bprmf_handle* h) {
   hipSetDevice(h->cfg.device);
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
-                  h->d_indptr, h->d_indices, h->d_trip, h->d_loss, h->d_err,
+                  h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
   dist_free(h->dist);
   for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
+  if (h->h_status) hipHostFree(h->h_status);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own_stream) hipStreamDestroy(h->own_stream);
@@ -287,6 +295,16 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   int hb = 1;
   while (hb < 32 && (1ull << (2 * hb)) < N) ++hb;
   h->feistel_h = hb;
+  // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
+  // the first calls (a larger chunk later would reallocate and recapture)
+  if (h->cfg.world == 1 && seg_mode(h)) {
+    const int64_t B = h->cfg.batch_size;
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(chunk_triplets(h) / B, ((int64_t)N + B - 1) / B));
+    if (int r = ensure_seg(h, nb)) return r;
+    if (int r = ensure_trip(h, nb * B)) return r;
+    if (h->use_graphs)
+      if (int r = ensure_step_graphs(h)) return r;
+  }
   return 0;
 }
 
@@ -318,31 +336,46 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
 
 // sum of the per-wave loss slots (copied back once per call)
 int bprmf::read_loss(bprmf_handle* h, double* loss) {
-  std::vector<double> slots(kLossSlots);
-  HIPCHK(hipMemcpyAsync(slots.data(), h->d_loss, sizeof(double) * kLossSlots, hipMemcpyDeviceToHost,
+  const size_t n = h->loss_slots_used ? kLossSlots : 1;
+  HIPCHK(hipMemcpyAsync(h->h_status + 16, h->d_loss, sizeof(double) * n, hipMemcpyDeviceToHost,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  const double* slots = reinterpret_cast<const double*>(h->h_status + 16);
   double s = 0;
-  for (double v : slots) s += v;
+  for (size_t k = 0; k < n; ++k) s += slots[k];
   *loss = s;
   return 0;
 }
 
 int bprmf::begin_call(bprmf_handle* h) {
   if (int r = set_dev(h)) return r;
-  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlots, h->stream));
+  // the segmented step adds its loss to slot 0 only; the atomic path uses every per-wave slot
+  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * (h->loss_slots_used ? kLossSlots : 1),
+                        h->stream));
+  h->loss_slots_used = false;
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   return 0;
 }
 
+// one copy back of {err, loss} (one host synchronisation per call)
 int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   HIPCHK(hipEventRecord(h->ev1, h->stream));
+  const size_t n = h->loss_slots_used ? kLossSlots : 1;
+  HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * n, hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int32_t e = *reinterpret_cast<const int32_t*>(h->h_status);
+  if (e) {
+    HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
+    if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
+    if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
+    return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
+  }
+  const double* slots = reinterpret_cast<const double*>(h->h_status + 16);
   double loss = 0;
-  if (int r = read_loss(h, &loss)) return r;
-  HIPCHK(hipEventSynchronize(h->ev1));
+  for (size_t k = 0; k < n; ++k) loss += slots[k];
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-  if (int r = check_err_flag(h)) return r;
   if (st) {
     st->triplets = triplets;
     st->steps = steps;
@@ -360,7 +393,7 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
     if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
     if (int r = dalloc(&h->d_ugrad, B * h->geom.ld)) return r;
     if (int r = dalloc(&h->d_xloss, B)) return r;
-    if (int r = dalloc(&h->d_tbase, 1)) return r;
+    if (int r = dalloc(&h->d_tbase, 4)) return r;
   }
   if (n_batches <= h->batch_cap) return 0;
   drop_graphs(h);  // captured graphs point into the old batch buffer
@@ -393,17 +426,17 @@ extern "C" {
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done);
 
-// The step launches of a chunk (user_step k, item_step k; k < nb) in blocks of kGraphSteps steps:
-// block j is captured once into a hipGraph and replayed for every chunk that reaches it (every
-// argument is fixed: batch k's records sit at a fixed offset of the batch buffer, t is read from
-// d_tbase), so replays cost one host call per block and no chunk length ever triggers a capture
-// again; the last nb % kGraphSteps steps are launched directly.
+// The step launches of a chunk.  Graph path: position-independent graphs of kGraphSizes steps,
+// each captured once per batch buffer (kernels take batch 0's view plus the batch stride and read
+// the batch and the step from the cursor d_tbase, which each replay's last node advances), so a
+// chunk of any length at any offset replays at most a few of them and never captures again.
 static void drop_graphs(bprmf_handle* h) {
   for (auto& ge : h->graphs)
     if (ge.exec) hipGraphExecDestroy(ge.exec);
   h->graphs.clear();
 }
 
+// eager launches of steps [k0, k1) of the chunk (bv of each batch, cursor {t, 0})
 static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
   const int B = h->cfg.batch_size;
   const BatchBuf bb{h->d_batch, B};
@@ -417,31 +450,72 @@ static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
   return 0;
 }
 
-static int launch_step_graph(bprmf_handle* h, int64_t nb) {
-  for (int64_t j = 0; (j + 1) * kGraphSteps <= nb; ++j) {
-    StepGraph* ge = nullptr;
-    for (auto& g : h->graphs)
-      if (g.nb == j) ge = &g;
-    if (!ge) {
-      StepGraph ng;
-      ng.nb = j;
-      HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-      const int rc = step_launches(h, j * kGraphSteps, (j + 1) * kGraphSteps);
-      hipGraph_t graph = nullptr;
-      const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
-      if (rc || e2 != hipSuccess) {
-        if (graph) hipGraphDestroy(graph);
-        return rc ? rc : fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e2));
-      }
-      const hipError_t e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
-      hipGraphDestroy(graph);
-      if (e != hipSuccess) return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
-      h->graphs.push_back(ng);
-      ge = &h->graphs.back();
-    }
-    HIPCHK(hipGraphLaunch(ge->exec, h->stream));
+static int capture_step_graph(bprmf_handle* h, int64_t n, StepGraph* out) {
+  const int B = h->cfg.batch_size;
+  const BatchBuf bb{h->d_batch, B};
+  const BatchView v0 = bb.view(0);
+  const int64_t stride = BatchBuf::stride_for(B);
+  HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = 0;
+  for (int64_t r = 0; r < n && !rc; ++r) {
+    hipError_t e = user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, h->d_xloss,
+                             h->d_contrib, h->d_ugrad, nullptr, h->stream, PeerWait{}, stride);
+    if (e == hipSuccess)
+      e = item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, h->d_contrib,
+                    h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss, stride);
+    if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph launch: %s", hipGetErrorString(e));
   }
-  return step_launches(h, nb / kGraphSteps * kGraphSteps, nb);
+  if (!rc) {
+    const hipError_t e = advance_cursor(h->d_tbase, (int32_t)n, h->stream);
+    if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph cursor: %s", hipGetErrorString(e));
+  }
+  hipGraph_t graph = nullptr;
+  const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+  if (rc || e2 != hipSuccess) {
+    if (graph) hipGraphDestroy(graph);
+    return rc ? rc : fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e2));
+  }
+  out->n = n;
+  const hipError_t e = hipGraphInstantiate(&out->exec, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  if (e != hipSuccess) {
+    out->exec = nullptr;
+    return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
+  }
+  return 0;
+}
+
+// capture every graph size once (batch buffer and contrib buffers must exist: ensure_seg)
+static int ensure_step_graphs(bprmf_handle* h) {
+  if ((int)h->graphs.size() == kGraphKinds) return 0;
+  drop_graphs(h);
+  for (int g = 0; g < kGraphKinds; ++g) {
+    StepGraph sg;
+    if (int r = capture_step_graph(h, kGraphSizes[g], &sg)) {
+      drop_graphs(h);
+      return r;
+    }
+    h->graphs.push_back(sg);
+  }
+  return 0;
+}
+
+// the cursor holds {h->t, 0}: nb steps as replays of the largest graphs that fit
+static int launch_step_graph(bprmf_handle* h, int64_t nb) {
+  if (int r = ensure_step_graphs(h)) return r;
+  for (int g = 0; g < kGraphKinds; ++g)
+    for (; nb >= h->graphs[g].n; nb -= h->graphs[g].n) HIPCHK(hipGraphLaunch(h->graphs[g].exec, h->stream));
+  return 0;
+}
+
+// sampled chunks of at most this many batches draw their triplets with the grid-wide sampler
+// first and build from those (the builder then has no sampler latency: one workgroup per batch
+// cannot hide it when a chunk is short); longer chunks sample inside the builder, whose
+// workgroups then fill the chip anyway.  BPRMF_SPLIT_BUILD=0/1 forces either.
+static bool split_build(int64_t nb) {
+  const char* e = getenv("BPRMF_SPLIT_BUILD");
+  if (e && *e) return e[0] != '0';
+  return nb <= 512;
 }
 
 // One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler
@@ -469,11 +543,21 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   }
   if (int r = ensure_seg(h, nb)) return r;
   BatchBuf bb{h->d_batch, (int)B};
-  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
+  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream));
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
-    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
-                         h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream));
+    if (!ru && split_build(nb)) {
+      if (int r = ensure_trip(h, n)) return r;
+      int32_t* tu = h->d_trip;
+      HIPCHK(sample(sampler_args(h), epoch, first_slot, n, tu, tu + h->trip_cap,
+                    tu + 2 * h->trip_cap, h->d_err, h->stream));
+      HIPCHK(build_batches(sampler_args(h), epoch, 0, n, (int)B, tu, tu + h->trip_cap,
+                           tu + 2 * h->trip_cap, h->U, h->cfg.item_num, 1, false, 0, nb, bb,
+                           h->d_err, h->stream));
+    } else {
+      HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
+                           h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream));
+    }
   }
   if (h->use_graphs) {
     // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
@@ -516,6 +600,7 @@ static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, cons
                      int64_t n, int64_t* steps_done) {
   const int64_t B = h->cfg.batch_size;
   if (int r = ensure_grad(h)) return r;
+  h->loss_slots_used = true;
   for (int64_t off = 0; off < n; off += B) {
     const int64_t nb = std::min(B, n - off);
     if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");

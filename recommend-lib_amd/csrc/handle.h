@@ -20,9 +20,13 @@ int fail(int code, const char* fmt, ...);
     if (e_ != hipSuccess) return bprmf::fail(BPRMF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
 
-constexpr int64_t kGraphSteps = 64;  // steps per captured step graph (launch_step_graph)
-struct StepGraph {  // a captured block of step launches (launch_step_graph)
-  int64_t nb = 0;   // the block's index j: steps [j * kGraphSteps, (j + 1) * kGraphSteps) of a chunk
+// position-independent step graphs (launch_step_graph): a graph of n steps runs the batches and
+// optimizer steps the device cursor d_tbase = {t, k} names, then advances it by n; any chunk is
+// a sum of these sizes, so no chunk length or offset ever triggers a capture after the first
+constexpr int64_t kGraphSizes[] = {64, 16, 4, 1};
+constexpr int kGraphKinds = 4;
+struct StepGraph {
+  int64_t n = 0;  // steps per replay
   hipGraphExec_t exec = nullptr;
 };
 constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step
@@ -54,12 +58,16 @@ struct bprmf_handle {
   float* d_contrib = nullptr;  // [B, ld] c*P_u per triplet (K1 -> K2)
   float* d_ugrad = nullptr;    // [B, ld] user gradient per triplet of multi-triplet users
   float* d_xloss = nullptr;    // [B] x per triplet (K1 -> K2's loss workgroup)
-  int32_t* d_tbase = nullptr;  // step count before the chunk (kernels read t from here)
+  int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;
   // misc device scalars
-  double* d_loss = nullptr;
-  int32_t* d_err = nullptr;
+  // device status block: {int32 err, pad, double loss[kLossSlots]} (one copy back per call)
+  unsigned char* d_status = nullptr;
+  unsigned char* h_status = nullptr;  // pinned host mirror
+  double* d_loss = nullptr;           // = d_status + 16
+  int32_t* d_err = nullptr;           // = d_status
+  bool loss_slots_used = false;       // the f32-atomic path wrote per-wave loss slots this call
   int32_t t = 0;  // optimizer steps taken
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;

@@ -52,6 +52,10 @@ constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgrou
 constexpr int kMaxWorld = 64;
 struct BatchView {
   int32_t *trec, *mrec, *irec, *lrec, *refs, *useg, *ioff, *ukey, *meta, *own;
+  __host__ __device__ BatchView shifted(int64_t off) const {
+    return BatchView{trec + off, mrec + off, irec + off, lrec + off, refs + off,
+                     useg + off, ioff + off, ukey + off, meta + off, own + off};
+  }
 };
 struct BatchBuf {
   int32_t* base;
@@ -93,6 +97,10 @@ struct SamplerArgs {
 };
 
 // --- launches (all asynchronous on `s`) ---
+// step cursor c = {t, k}: the step kernels of a position-independent graph run batch c[1] + r at
+// optimizer step c[0] + r + 1 (r = the launch's index in the graph); advance adds n to both
+hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s);
+hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s);
 hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
                        uint32_t table_tag, int world, int rank, hipStream_t s);
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,
@@ -121,9 +129,12 @@ struct PeerWait {
 // K1, one lane group per triplet: c*P_u -> contrib[p]; single-triplet users updated in place,
 // the others' per-triplet gradients -> ugrad[p]; x = <P_u,Q_i> - <P_u,Q_j> -> xloss[p] (if set).  item_rows != null: sharded K1 (item rows by
 // slot from the exchange buffer)
+// bstride != 0: bv is batch 0's view and the kernel runs batch tbase[1] + step (cursor graphs);
+// bstride == 0: bv is the batch's own view.  Either way t = tbase[0] + step + 1.
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
-                     const float* item_rows, hipStream_t s, const PeerWait& pw = PeerWait{});
+                     const float* item_rows, hipStream_t s, const PeerWait& pw = PeerWait{},
+                     int64_t bstride = 0);
 // K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
 // grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items).
 // loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
@@ -131,7 +142,7 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss = nullptr,
-                     double* loss = nullptr);
+                     double* loss = nullptr, int64_t bstride = 0);
 int item_long_blocks(int B);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,

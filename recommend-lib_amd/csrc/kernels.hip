@@ -344,6 +344,26 @@ hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_
   return hipGetLastError();
 }
 
+// the step cursor {t, batch} that position-independent step graphs read (capi.cpp)
+__global__ void k_set_cursor(int32_t* __restrict__ c, int32_t t, int32_t k) {
+  c[0] = t;
+  c[1] = k;
+}
+__global__ void k_advance_cursor(int32_t* __restrict__ c, int32_t n) {
+  c[0] += n;
+  c[1] += n;
+}
+
+hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s) {
+  k_set_cursor<<<1, 1, 0, s>>>(cursor, t, k);
+  return hipGetLastError();
+}
+
+hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s) {
+  k_advance_cursor<<<1, 1, 0, s>>>(cursor, n);
+  return hipGetLastError();
+}
+
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,
                   int32_t* oi, int32_t* oj, int32_t* err, hipStream_t s) {
   if (count <= 0) return hipSuccess;

@@ -10,6 +10,7 @@
 //      segments, their references in a fixed order, hot-item records, per-owner counts;
 //   4. 32-byte segment records so each step kernel needs ONE dependent load before its gathers.
 // Layout: kernels.h (BatchBuf).  Step kernels: step.hip.
+#include <stdlib.h>
 #include <string.h>
 
 #include <rocprim/block/block_radix_sort.hpp>
@@ -28,7 +29,100 @@ static __device__ __forceinline__ void store_rec(int32_t* rec, int a, int b, int
   reinterpret_cast<int4*>(rec)[1] = make_int4(e, f, g, h);
 }
 
-template <int IPT>
+// ------------------------------------------------------------------------------------------------
+// Bucket sort of a workgroup's (key, value) pairs in blocked arrangement (thread t holds input
+// positions t*E .. t*E+E-1), replacing rocPRIM's radix passes for B <= 4096.  The result equals a
+// stable sort by key (ties by input position) — the arrangement the radix sort gives, bit for bit
+// — in four LDS phases instead of ceil(bits/4) radix passes:
+//   1. count per bucket, bucket = key >> (bits - 12): MONOTONE in the key (4096 buckets);
+//   2. exclusive scan of the counts -> bucket starts;
+//   3. scatter (key << 32 | position) into the bucket's range (order inside a bucket arbitrary);
+//   4. each element's rank inside its bucket = #{smaller (key, position)} -> its sorted slot.
+// Phase 4 costs sum(c^2) over buckets: a batch's keys spread over ~4096 buckets (1-2 per bucket)
+// except a hot item's references (<= ~80 at ml-20m shape), which share one bucket; the lanes of a
+// wave scan the same bucket, so those reads are LDS broadcasts.  Invalid keys (kNone) take the
+// positions after every valid key, in any order (their values are never read).
+// ------------------------------------------------------------------------------------------------
+constexpr int kBucketBits = 12;
+constexpr int kBuckets = 1 << kBucketBits;
+
+template <int T>
+struct BucketScratch {
+  uint64_t* bk;     // [n] (key << 32 | input position), bucket order
+  int32_t* srt;     // [n] input position at each sorted position
+  int32_t* start;   // [kBuckets + 1] bucket starts (start[kBuckets] = valid count)
+  int32_t* ninv;    // invalid-key counter
+  typename rocprim::block_scan<int, T>::storage_type* scan;
+};
+
+template <int T, int E, class KeyOf, class ValOf>
+static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t (&val)[E], int bits,
+                                                   const BucketScratch<T>& sc, KeyOf key_of,
+                                                   ValOf val_of) {
+  using Scan = rocprim::block_scan<int, T>;
+  static_assert(kBuckets % T == 0, "buckets per thread");
+  constexpr int PB = kBuckets / T;
+  const int tid = threadIdx.x;
+  const int shift = bits > kBucketBits ? bits - kBucketBits : 0;
+  for (int b = tid; b <= kBuckets; b += T) sc.start[b] = 0;
+  if (tid == 0) *sc.ninv = 0;
+  __syncthreads();
+  int li[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k)
+    li[k] = key[k] != kNone ? atomicAdd(&sc.start[key[k] >> shift], 1) : -1;
+  __syncthreads();
+  int c[PB], sum = 0;
+#pragma unroll
+  for (int m = 0; m < PB; ++m) {
+    c[m] = sc.start[tid * PB + m];
+    sum += c[m];
+  }
+  int pre = 0, total = 0;
+  Scan().exclusive_scan(sum, pre, 0, total, *sc.scan, rocprim::plus<int>());
+#pragma unroll
+  for (int m = 0; m < PB; ++m) {
+    sc.start[tid * PB + m] = pre;
+    pre += c[m];
+  }
+  if (tid == 0) sc.start[kBuckets] = total;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E; ++k) {
+    const int q = tid * E + k;
+    if (li[k] >= 0)
+      sc.bk[sc.start[key[k] >> shift] + li[k]] = ((uint64_t)key[k] << 32) | (uint32_t)q;
+    else
+      sc.srt[total + atomicAdd(sc.ninv, 1)] = q;
+  }
+  __syncthreads();
+  for (int x = tid; x < total; x += T) {
+    const uint64_t me = sc.bk[x];
+    const int b = (int)((uint32_t)(me >> 32) >> shift);
+    const int bs = sc.start[b], be = sc.start[b + 1];
+    int rank = 0;
+    for (int y = bs; y < be; ++y) rank += sc.bk[y] < me;
+    sc.srt[bs + rank] = (int32_t)(uint32_t)me;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E; ++k) {
+    const int pos = tid * E + k;
+    const int q = sc.srt[pos];
+    if (pos < total) {
+      key[k] = key_of(q);
+      val[k] = val_of(q);
+    } else {
+      key[k] = kNone;
+      val[k] = 0;
+    }
+  }
+  __syncthreads();  // the caller reuses the scratch (its sorted keys alias bk)
+}
+
+// BUCKET: bucket sorts (B <= kBuildThreads * 4); else rocPRIM block radix sorts.  Both give the
+// same arrangement, so the batches (and every step result) are identical either way.
+template <int IPT, bool BUCKET>
 __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
@@ -39,19 +133,30 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
   using SortI = rocprim::block_radix_sort<uint32_t, T, IPT2, uint32_t>;
   using Scan = rocprim::block_scan<int, T>;
-  union Smem {  // the sorted keys alias the sort storage (barrier after every sort)
+  union RadixSmem {  // the sorted keys alias the sort storage (barrier after every sort)
     typename SortU::storage_type su;
     typename SortI::storage_type si;
     uint32_t key[T * IPT2];
   };
-  __shared__ Smem sm;
+  // bucket layout: bk u64[T*IPT2] (sorted keys alias it; user keys by slot sit in its upper half
+  // during the user sort), srt i32[T*IPT2], start i32[kBuckets + 1]
+  constexpr size_t kBucketBytes = 12 * (size_t)T * IPT2 + 4 * (kBuckets + 4);
+  constexpr size_t kSortBytes = BUCKET ? kBucketBytes : sizeof(RadixSmem);
+  __shared__ __attribute__((aligned(16))) unsigned char s_sort[kSortBytes];
   __shared__ typename Scan::storage_type sscan;
   __shared__ int32_t s_i[T * IPT];  // per sorted position: item row (world 1) or item slot
   __shared__ int32_t s_j[T * IPT];
   __shared__ int s_own[kMaxWorld];
   __shared__ int s_opre[kMaxWorld];  // first item segment of each owner (padded slots)
-  uint32_t* s_key = sm.key;
-
+  __shared__ int32_t s_ninv;
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_sort);
+  uint32_t* s_u = reinterpret_cast<uint32_t*>(s_sort) + 2 * T * IPT;  // bucket mode, user sort
+  BucketScratch<T> bs;
+  bs.bk = reinterpret_cast<uint64_t*>(s_sort);
+  bs.srt = reinterpret_cast<int32_t*>(s_sort + 8 * (size_t)T * IPT2);
+  bs.start = reinterpret_cast<int32_t*>(s_sort + 12 * (size_t)T * IPT2);
+  bs.ninv = &s_ninv;
+  bs.scan = &sscan;
   const int tid = threadIdx.x;
   const int64_t batch = blockIdx.x;
   const int64_t b0 = batch * (int64_t)B;
@@ -93,6 +198,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
           (uint64_t)j < (uint64_t)i_rows) {
         key[k] = (uint32_t)u;
+        if (BUCKET) s_u[p] = (uint32_t)u;
         s_i[p] = i;
         s_j[p] = j;
       } else {
@@ -100,8 +206,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       }
     }
   }
-  SortU().sort(key, val, sm.su, 0, user_bits);
-  __syncthreads();
+  if constexpr (BUCKET) {
+    bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
+                        [](int q) { return (uint32_t)q; });
+  } else {
+    SortU().sort(key, val, reinterpret_cast<RadixSmem*>(s_sort)->su, 0, user_bits);
+    __syncthreads();
+  }
   // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
   int32_t my_i[IPT], my_j[IPT];
   int valid = 0;
@@ -153,8 +264,19 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       iv[k] = ((uint32_t)p << 1) | (r < nvalid ? 0u : 1u);
     }
   }
-  SortI().sort(ik, iv, sm.si, 0, item_bits);
-  __syncthreads();  // also: every read of s_i/s_j above is done
+  if constexpr (BUCKET) {
+    const int nv = nvalid;
+    bucket_sort<T, IPT2>(
+        ik, iv, item_bits, bs,
+        [&](int r) {
+          const uint32_t item = (uint32_t)(r < nv ? s_i[r] : s_j[r - nv]);
+          return (item % (uint32_t)world) * (uint32_t)iloc + item / (uint32_t)world;
+        },
+        [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); });
+  } else {
+    SortI().sort(ik, iv, reinterpret_cast<RadixSmem*>(s_sort)->si, 0, item_bits);
+    __syncthreads();  // also: every read of s_i/s_j above is done
+  }
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) s_key[tid * IPT2 + k] = ik[k];
   __syncthreads();
@@ -311,12 +433,17 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // one value above every valid key: an empty position (kNone) must sort after all of them, and
   // the sorts see only these low bits of it
   const int ub = bits_for(u_rows + 1), ib = bits_for(iloc * world + 1);
-  if (B <= kBuildThreads * 4)
-    k_build_batches<4><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
+  const bool radix = getenv("BPRMF_RADIX_BUILD") != nullptr;  // A/B of the two sorts (tests)
+  if (B <= kBuildThreads * 4 && !radix)
+    k_build_batches<4, true><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
+        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
+        slots ? slot_stride : 0, ub, ib, bb, err);
+  else if (B <= kBuildThreads * 4)
+    k_build_batches<4, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
         slots ? slot_stride : 0, ub, ib, bb, err);
   else
-    k_build_batches<8><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
+    k_build_batches<8, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
         slots ? slot_stride : 0, ub, ib, bb, err);
   return hipGetLastError();

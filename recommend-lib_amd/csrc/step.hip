@@ -55,9 +55,10 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
                                                       float* __restrict__ contrib,
                                                       float* __restrict__ ugrad,
                                                       const float* __restrict__ item_rows,
-                                                      PeerWait pw) {
+                                                      PeerWait pw, int64_t bstride) {
   const int sub = threadIdx.x & (G4 - 1);
   const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
+  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
   // independent loads: the record (allocated for every p < B), the triplet count, the step base
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[p];
@@ -196,8 +197,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   const float* __restrict__ ugrad, int long_blocks,
                                                   int item_blocks, float* __restrict__ grads,
                                                   const float* __restrict__ xloss,
-                                                  double* __restrict__ loss) {
+                                                  double* __restrict__ loss, int64_t bstride) {
   constexpr int NG = KB / G4;
+  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
   const int32_t t = *tbase + step + 1;
@@ -351,15 +353,18 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
 
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
-                     const float* item_rows, hipStream_t s, const PeerWait& pw) {
+                     const float* item_rows, hipStream_t s, const PeerWait& pw,
+                     int64_t bstride) {
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
     if (item_rows)
       k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                           contrib, ugrad, item_rows, pw);
+                                                           contrib, ugrad, item_rows, pw,
+                                                           bstride);
     else
       k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                            contrib, ugrad, nullptr, pw);
+                                                            contrib, ugrad, nullptr, pw,
+                                                            bstride);
   }));
   return hipGetLastError();
 }
@@ -368,7 +373,8 @@ int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg
 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
-                     float* grads, hipStream_t s, const float* xloss, double* loss) {
+                     float* grads, hipStream_t s, const float* xloss, double* loss,
+                     int64_t bstride) {
   const int long_blocks = item_long_blocks(B);
   if (!xloss) loss = nullptr;
   BPRMF_DISPATCH4(g, ({
@@ -380,11 +386,12 @@ hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
     if (grads)
       k_item_step<G4_, S_, true, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
                                                            ugrad, long_blocks, item_blocks, grads,
-                                                           xloss, loss);
+                                                           xloss, loss, bstride);
     else
       k_item_step<G4_, S_, false, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
                                                             contrib, ugrad, long_blocks,
-                                                            item_blocks, nullptr, xloss, loss);
+                                                            item_blocks, nullptr, xloss, loss,
+                                                            bstride);
   }));
   return hipGetLastError();
 }

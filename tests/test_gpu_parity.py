@@ -221,6 +221,79 @@ def test_device_sampled_training_equals_replay_of_oracle_triplets(rl, golden):
     assert np.array_equal(Pa, Pb) and np.array_equal(Qa, Qb)
 
 
+@pytest.mark.parametrize("B", [4096, 1000, 96])
+def test_batch_builders_agree_bitwise(rl, golden, monkeypatch, B):
+    """The bucket-sort batch builder (B <= 4096), the rocPRIM radix builder, and the grid-wide
+    sampler ahead of the builder vs the sampler inside it all give the same batches, so training
+    is bitwise identical (partial last batches included: the ml-100k epoch is not a multiple of B)."""
+    pos, U, I = _ml100k_pos(golden)
+    outs = []
+    for env in ({}, {"BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_BUILD": "0"},
+                {"BPRMF_SPLIT_BUILD": "1", "BPRMF_RADIX_BUILD": "1"}):
+        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_BUILD"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = _model(rl, U, I, 32, B, seed=7)
+        m.set_train(pos)
+        n = m.epoch_size()[1]
+        m.train_steps(0, 0, min(n, 37))
+        m.train_steps(0, n - 2, 2)  # ends on the partial batch
+        st = m.train_steps(1, 3, 5)
+        outs.append((m.get_weights(), st["loss"]))
+    for (P, Q), loss in outs[1:]:
+        assert np.array_equal(P, outs[0][0][0]) and np.array_equal(Q, outs[0][0][1])
+        assert loss == outs[0][1]
+
+
+def test_replay_bucket_builder_empty_slots_and_duplicates(rl, monkeypatch):
+    """Replayed batches with repeated users/items, i == j and an all-duplicate batch: the bucket
+    builder equals the radix builder bitwise and both equal the dense oracle."""
+    g = np.random.default_rng(12)
+    U, I, d, B = 300, 40, 16, 512
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    n = 3 * B + 77
+    u, i, j = g.integers(0, 5, n), g.integers(0, I, n), g.integers(0, I, n)
+    u[:B] = 3  # one user for a whole batch
+    i[:B] = 7
+    j[B:B + 50] = i[B:B + 50]
+    outs = []
+    for radix in (False, True):
+        monkeypatch.delenv("BPRMF_RADIX_BUILD", raising=False)
+        if radix:
+            monkeypatch.setenv("BPRMF_RADIX_BUILD", "1")
+        m = _model(rl, U, I, d, B, lr=0.05, wd=0.01)
+        m.set_weights(P0, Q0)
+        m.train_triplets(u, i, j)
+        outs.append(m.get_weights())
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    P, Q = P0.copy(), Q0.copy()
+    for s in range(0, n, B):
+        O.bpr_step_dense(P, Q, u[s:s + B], i[s:s + B], j[s:s + B], 0.05, 0.01)
+    np.testing.assert_allclose(outs[0][0], P, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(outs[0][1], Q, rtol=1e-5, atol=1e-6)
+
+
+def test_step_graphs_equal_eager_launches(rl, golden, monkeypatch):
+    """Position-independent step graphs (sizes 64/16/4/1 replayed from the device cursor) give
+    the same result as eager launches for chunks of any length at any offset."""
+    pos, U, I = _ml100k_pos(golden)
+    outs = []
+    for eager in (False, True):
+        monkeypatch.delenv("BPRMF_NO_GRAPH", raising=False)
+        if eager:
+            monkeypatch.setenv("BPRMF_NO_GRAPH", "1")
+        m = _model(rl, U, I, 16, 256, seed=3)
+        m.set_train(pos)
+        first = 0
+        for c in (1, 3, 17, 64, 85, 130, 5):
+            m.train_steps(0, first, c)
+            first += c
+        outs.append(m.get_weights())
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
 def test_training_is_bitwise_reproducible(rl, golden):
     pos, U, I = _ml100k_pos(golden)
     out = []

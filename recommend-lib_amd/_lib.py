@@ -8,6 +8,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbprmf_amd.so")
+# diagnostic variants only (tools/ubench_build.py loads a stamped build); never set by the product
+if os.environ.get("BPRMF_DIAG_LIB"):
+    LIB_PATH = os.environ["BPRMF_DIAG_LIB"]
 
 E_INVALID, E_RANGE, E_HIP, E_STATE, E_NO_NEGATIVE, E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 

@@ -36,16 +36,20 @@ def _compile(args):
     return src, r.returncode, r.stdout + r.stderr
 
 
-def build(force=False, verbose=False):
-    """Compile every source to an object in parallel (objects outside the tree), then link."""
-    if not force and not is_stale():
+def build(force=False, verbose=False, defines=(), out=None):
+    """Compile every source to an object in parallel (objects outside the tree), then link.
+    defines/out: a diagnostic variant (e.g. tools/ubench_build.py) with its own objects."""
+    out = out or LIB
+    if not force and out == LIB and not is_stale():
         return LIB
     from concurrent.futures import ThreadPoolExecutor
     obj_dir = os.environ.get("BPRMF_OBJ_DIR", os.path.join("/tmp", "bprmf_amd_obj"))
+    if defines:
+        obj_dir += "_" + "_".join(d.lower() for d in defines)
     os.makedirs(obj_dir, exist_ok=True)
     hdr_t = max(os.path.getmtime(h) for h in HEADERS)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
+             "-Wno-unused-function", "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines]
     jobs, objs = [], []
     for src in SOURCES:
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
@@ -54,19 +58,19 @@ def build(force=False, verbose=False):
             jobs.append(([hipcc()] + flags + ["-c", src, "-o", obj], src))
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8))
     with ThreadPoolExecutor(workers) as ex:
-        for src, rc, out in ex.map(_compile, jobs):
+        for src, rc, log in ex.map(_compile, jobs):
             if verbose:
                 print(f"compiled {src}", file=sys.stderr)
             if rc != 0:
-                raise RuntimeError(f"hipcc failed on {src} ({rc}):\n{out}")
-    tmp = LIB + ".tmp"
+                raise RuntimeError(f"hipcc failed on {src} ({rc}):\n{log}")
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp] + objs + \
           ["-L/opt/rocm/lib", "-lrccl", "-lrocblas"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -139,10 +140,6 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   }
   h->stream = h->own_stream;
   h->use_graphs = getenv("BPRMF_NO_GRAPH") == nullptr;
-  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
-    bprmf_destroy(h);
-    return fail(BPRMF_E_HIP, "hipEventCreate failed");
-  }
   const int64_t ld = g.ld;
   TRY(dalloc(&h->P.W, h->U * ld));
   TRY(dalloc(&h->P.stamp, h->U));
@@ -150,10 +147,12 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->Q.stamp, h->I));
   const size_t status_bytes = 16 + sizeof(double) * kLossSlots;
   TRY(dalloc(&h->d_status, (int64_t)status_bytes));
-  if (hipHostMalloc((void**)&h->h_status, status_bytes, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void**)&h->h_status, status_bytes, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->h_status_dev, h->h_status, 0) != hipSuccess) {
+    if (h->h_status) (void)!hipHostFree(h->h_status);
     h->h_status = nullptr;
     bprmf_destroy(h);
-    return fail(BPRMF_E_HIP, "hipHostMalloc failed");
+    return fail(BPRMF_E_HIP, "hipHostMalloc (mapped status) failed");
   }
   h->d_err = reinterpret_cast<int32_t*>(h->d_status);
   h->d_loss = reinterpret_cast<double*>(h->d_status + 16);
@@ -194,8 +193,6 @@ int bprmf_destroy(bprmf_handle* h) {
   dist_free(h->dist);
   for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
   if (h->h_status) hipHostFree(h->h_status);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own_stream) hipStreamDestroy(h->own_stream);
   delete h;
   return 0;
@@ -334,53 +331,67 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   return a;
 }
 
-// sum of the per-wave loss slots (copied back once per call)
+static double host_seconds() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// sum of every per-wave loss slot (the Python-orchestrated sharded step)
 int bprmf::read_loss(bprmf_handle* h, double* loss) {
-  const size_t n = h->loss_slots_used ? kLossSlots : 1;
-  HIPCHK(hipMemcpyAsync(h->h_status + 16, h->d_loss, sizeof(double) * n, hipMemcpyDeviceToHost,
-                        h->stream));
+  HIPCHK(hipMemcpyAsync(h->h_status + 16, h->d_loss, sizeof(double) * kLossSlots,
+                        hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   const double* slots = reinterpret_cast<const double*>(h->h_status + 16);
   double s = 0;
-  for (size_t k = 0; k < n; ++k) s += slots[k];
+  for (int k = 0; k < kLossSlots; ++k) s += slots[k];
   *loss = s;
   return 0;
 }
 
+int bprmf::loss_zero_slots(bprmf_handle* h) {
+  if (!h->loss_pending) return 0;
+  h->loss_pending = false;
+  const int n = h->slots_dirty ? kLossSlots : 1;
+  h->slots_dirty = false;
+  return n;
+}
+
+// no GPU work here: the call's first launch zeroes the loss (set_cursor / loss_zero_slots)
 int bprmf::begin_call(bprmf_handle* h) {
   if (int r = set_dev(h)) return r;
-  // the segmented step adds its loss to slot 0 only; the atomic path uses every per-wave slot
-  HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * (h->loss_slots_used ? kLossSlots : 1),
-                        h->stream));
-  h->loss_slots_used = false;
-  HIPCHK(hipEventRecord(h->ev0, h->stream));
+  h->loss_pending = true;
+  h->call_slots = false;
+  h->call_t0 = host_seconds();
   return 0;
 }
 
-// one copy back of {err, loss} (one host synchronisation per call)
+// one status read per call: {err, loss} written into mapped host memory by one tiny kernel (the
+// f32-atomic path's per-wave slots: one copy), then one stream synchronisation
 int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
-  HIPCHK(hipEventRecord(h->ev1, h->stream));
-  const size_t n = h->loss_slots_used ? kLossSlots : 1;
-  HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * n, hipMemcpyDeviceToHost,
-                        h->stream));
+  const bool ran = !h->loss_pending;
+  h->loss_pending = false;
+  if (h->call_slots) {
+    HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * kLossSlots,
+                          hipMemcpyDeviceToHost, h->stream));
+  } else {
+    HIPCHK(status_out(h->d_status, h->h_status_dev, 3, h->stream));
+  }
   HIPCHK(hipStreamSynchronize(h->stream));
-  const int32_t e = *reinterpret_cast<const int32_t*>(h->h_status);
+  const int32_t e = *reinterpret_cast<const volatile int32_t*>(h->h_status);
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
     return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
   }
-  const double* slots = reinterpret_cast<const double*>(h->h_status + 16);
+  const volatile double* slots = reinterpret_cast<const volatile double*>(h->h_status + 16);
   double loss = 0;
-  for (size_t k = 0; k < n; ++k) loss += slots[k];
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  if (ran)
+    for (int k = 0; k < (h->call_slots ? kLossSlots : 1); ++k) loss += slots[k];
   if (st) {
     st->triplets = triplets;
     st->steps = steps;
     st->loss = loss;
-    st->seconds = ms * 1e-3;
+    st->seconds = host_seconds() - h->call_t0;
   }
   return 0;
 }
@@ -543,8 +554,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   }
   if (int r = ensure_seg(h, nb)) return r;
   BatchBuf bb{h->d_batch, (int)B};
-  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream));
-  {
+  {  // the batches first: the GPU starts on them while the host enqueues the rest
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     if (!ru && split_build(nb)) {
       if (int r = ensure_trip(h, n)) return r;
@@ -559,6 +569,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
                            h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream));
     }
   }
+  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
   if (h->use_graphs) {
     // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
     // the step kernels and their gaps; per-kernel splits come from rocprofv3)
@@ -600,7 +611,9 @@ static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, cons
                      int64_t n, int64_t* steps_done) {
   const int64_t B = h->cfg.batch_size;
   if (int r = ensure_grad(h)) return r;
-  h->loss_slots_used = true;
+  if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
+  h->slots_dirty = true;
+  h->call_slots = true;
   for (int64_t off = 0; off < n; off += B) {
     const int64_t nb = std::min(B, n - off);
     if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");

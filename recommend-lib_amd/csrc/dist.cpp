@@ -512,7 +512,7 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   const BatchBuf bb{h->d_batch, B};
   const int par = (int)(d->chunks & 1);
   const int32_t seq = (int32_t)(d->chunks + 1);
-  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_tbase, h->t, 1, h->stream));
+  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
   int64_t first_slot = 0, n_slots = n * B;
   if (!ru) {
     int64_t N;

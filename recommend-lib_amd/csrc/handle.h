@@ -64,14 +64,17 @@ struct bprmf_handle {
   // misc device scalars
   // device status block: {int32 err, pad, double loss[kLossSlots]} (one copy back per call)
   unsigned char* d_status = nullptr;
-  unsigned char* h_status = nullptr;  // pinned host mirror
-  double* d_loss = nullptr;           // = d_status + 16
-  int32_t* d_err = nullptr;           // = d_status
-  bool loss_slots_used = false;       // the f32-atomic path wrote per-wave loss slots this call
+  unsigned char* h_status = nullptr;      // pinned, mapped host mirror
+  unsigned char* h_status_dev = nullptr;  // its device address (k_status_out writes there)
+  double* d_loss = nullptr;               // = d_status + 16
+  int32_t* d_err = nullptr;               // = d_status
+  bool loss_pending = false;    // a call began: the loss slots are zeroed before the first step
+  bool slots_dirty = true;      // slots past 0 may hold values (the f32-atomic path uses them)
+  bool call_slots = false;      // this call's loss is spread over every slot (atomic path)
+  double call_t0 = 0;           // host clock at begin_call (stats.seconds)
   int32_t t = 0;  // optimizer steps taken
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // live per-kernel timing (bprmf_profile): event pairs around each launch of each kind
   bool prof_on = false;
   std::vector<hipEvent_t> prof_pool;
@@ -119,6 +122,8 @@ bool seg_mode(const bprmf_handle* h);
 int check_err_flag(bprmf_handle* h);
 SamplerArgs sampler_args(bprmf_handle* h);
 int read_loss(bprmf_handle* h, double* loss);
+// loss slots the first launch of a call must zero (0 once done for this call)
+int loss_zero_slots(bprmf_handle* h);
 int begin_call(bprmf_handle* h);
 int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps);
 

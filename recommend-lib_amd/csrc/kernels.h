@@ -99,7 +99,11 @@ struct SamplerArgs {
 // --- launches (all asynchronous on `s`) ---
 // step cursor c = {t, k}: the step kernels of a position-independent graph run batch c[1] + r at
 // optimizer step c[0] + r + 1 (r = the launch's index in the graph); advance adds n to both
-hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s);
+// (loss != null: also zero loss[0 .. nloss))
+hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, double* loss = nullptr,
+                      int nloss = 0);
+// copy `words` 8-byte words of device memory into mapped host memory (one tiny kernel)
+hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s);
 hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s);
 hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
                        uint32_t table_tag, int world, int rank, hipStream_t s);

@@ -344,18 +344,35 @@ hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_
   return hipGetLastError();
 }
 
-// the step cursor {t, batch} that position-independent step graphs read (capi.cpp)
-__global__ void k_set_cursor(int32_t* __restrict__ c, int32_t t, int32_t k) {
-  c[0] = t;
-  c[1] = k;
+// the step cursor {t, batch} that position-independent step graphs read (capi.cpp); the same
+// launch clears the call's loss slots (one launch at the head of a call instead of two)
+__global__ void k_set_cursor(int32_t* __restrict__ c, int32_t t, int32_t k, double* __restrict__ loss,
+                             int nloss) {
+  if (threadIdx.x == 0) {
+    c[0] = t;
+    c[1] = k;
+  }
+  for (int i = threadIdx.x; i < nloss; i += blockDim.x) loss[i] = 0.0;
 }
 __global__ void k_advance_cursor(int32_t* __restrict__ c, int32_t n) {
   c[0] += n;
   c[1] += n;
 }
+// the call's status words straight into mapped host memory (system-scope stores), so the host
+// reads them after one stream synchronisation without a copy command
+__global__ void k_status_out(const uint64_t* __restrict__ src, uint64_t* dst, int n) {
+  const int i = threadIdx.x;
+  if (i < n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
-hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s) {
-  k_set_cursor<<<1, 1, 0, s>>>(cursor, t, k);
+hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, double* loss, int nloss) {
+  k_set_cursor<<<1, 256, 0, s>>>(cursor, t, k, loss, loss ? nloss : 0);
+  return hipGetLastError();
+}
+
+hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s) {
+  k_status_out<<<1, 64, 0, s>>>(static_cast<const uint64_t*>(d_status),
+                                static_cast<uint64_t*>(h_status_dev), words);
   return hipGetLastError();
 }
 

@@ -21,6 +21,20 @@
 namespace bprmf {
 
 constexpr int kBuildThreads = 1024;
+
+// diagnostic build only (-DBPRMF_BUILD_STAMPS, tools/ubench_build.py): s_memrealtime at the
+// builder's phase boundaries, first workgroup, first thread
+#ifdef BPRMF_BUILD_STAMPS
+__device__ uint64_t g_build_stamps[16];
+#define BSTAMP(k)                                                                          \
+  do {                                                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_build_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 static __device__ __forceinline__ void store_rec(int32_t* rec, int a, int b, int c, int d, int e,
@@ -100,8 +114,12 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
     const uint64_t me = sc.bk[x];
     const int b = (int)((uint32_t)(me >> 32) >> shift);
     const int bs = sc.start[b], be = sc.start[b + 1];
-    int rank = 0;
-    for (int y = bs; y < be; ++y) rank += sc.bk[y] < me;
+    int rank = 0, y = bs;
+    for (; y + 4 <= be; y += 4) {  // four reads in flight (a hot item's bucket holds ~80)
+      const uint64_t a0 = sc.bk[y], a1 = sc.bk[y + 1], a2 = sc.bk[y + 2], a3 = sc.bk[y + 3];
+      rank += (int)(a0 < me) + (int)(a1 < me) + (int)(a2 < me) + (int)(a3 < me);
+    }
+    for (; y < be; ++y) rank += sc.bk[y] < me;
     sc.srt[bs + rank] = (int32_t)(uint32_t)me;
   }
   __syncthreads();
@@ -151,6 +169,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   __shared__ int32_t s_ninv;
   uint32_t* s_key = reinterpret_cast<uint32_t*>(s_sort);
   uint32_t* s_u = reinterpret_cast<uint32_t*>(s_sort) + 2 * T * IPT;  // bucket mode, user sort
+  // bucket mode, after the item sort: LDS copies of refs and of the item segment starts, so the
+  // record phases read LDS instead of their own global stores back (s_key keeps bk's first half)
+  int32_t* s_refs = reinterpret_cast<int32_t*>(s_sort) + T * IPT2;
+  int32_t* s_ioff = reinterpret_cast<int32_t*>(s_sort + 8 * (size_t)T * IPT2);  // srt, start
   BucketScratch<T> bs;
   bs.bk = reinterpret_cast<uint64_t*>(s_sort);
   bs.srt = reinterpret_cast<int32_t*>(s_sort + 8 * (size_t)T * IPT2);
@@ -164,6 +186,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
   const BatchView v = bb.view(batch);
   if (tid < kMaxWorld) s_own[tid] = 0;
+  BSTAMP(0);
 
   // 1. the batch's triplets in slot order, keyed by local user row
   uint32_t key[IPT], val[IPT];
@@ -206,6 +229,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       }
     }
   }
+  BSTAMP(1);
   if constexpr (BUCKET) {
     bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
                         [](int q) { return (uint32_t)q; });
@@ -213,6 +237,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SortU().sort(key, val, reinterpret_cast<RadixSmem*>(s_sort)->su, 0, user_bits);
     __syncthreads();
   }
+  BSTAMP(2);
   // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
   int32_t my_i[IPT], my_j[IPT];
   int valid = 0;
@@ -238,17 +263,23 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   __syncthreads();
   Scan().exclusive_scan(valid, vpre, 0, nvalid, sscan, rocprim::plus<int>());
   bool uhead[IPT];
+  int uend[IPT];  // a head's segment end (users repeat a few times per batch at most)
   {
     int s = seg0;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
       uhead[k] = key[k] != kNone && (p == 0 || s_key[p - 1] != key[k]);
-      if (uhead[k]) v.useg[s++] = p;
+      uend[k] = p + 1;
+      if (uhead[k]) {
+        v.useg[s++] = p;
+        while (uend[k] < nvalid && s_key[uend[k]] == key[k]) ++uend[k];
+      }
     }
   }
   if (tid == 0) v.useg[n_useg] = nvalid;
   __syncthreads();  // useg visible block-wide; s_i/s_j sorted; s_key free for the item keys
+  BSTAMP(3);
 
   // 2. item references: r < nvalid -> i of sorted triplet r (sign -), else j of r - nvalid (sign +)
   uint32_t ik[IPT2], iv[IPT2];
@@ -277,6 +308,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SortI().sort(ik, iv, reinterpret_cast<RadixSmem*>(s_sort)->si, 0, item_bits);
     __syncthreads();  // also: every read of s_i/s_j above is done
   }
+  BSTAMP(4);
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) s_key[tid * IPT2 + k] = ik[k];
   __syncthreads();
@@ -287,6 +319,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     if (ik[k] != kNone) {
       iheads += (r == 0 || s_key[r - 1] != ik[k]);
       v.refs[r] = (int32_t)iv[k];
+      if (BUCKET) s_refs[r] = (int32_t)iv[k];
     }
   }
   int iseg0 = 0, n_iseg = 0;
@@ -300,6 +333,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       if (r == 0 || s_key[r - 1] != ik[k]) {
         ++s;
         v.ioff[s] = r;
+        if (BUCKET) s_ioff[s] = r;
         if (slots) {
           v.ukey[s] = (int32_t)(ik[k] % (uint32_t)iloc);
           atomicAdd(&s_own[ik[k] / (uint32_t)iloc], 1);
@@ -309,7 +343,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     }
   }
   if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
+  if (BUCKET && tid == 0) s_ioff[n_iseg] = 2 * nvalid;
+  auto ioff_at = [&](int seg) { return BUCKET ? s_ioff[seg] : v.ioff[seg]; };
+  auto ref_at = [&](int r) { return BUCKET ? s_refs[r] : v.refs[r]; };
   __syncthreads();  // ioff, refs, slots, s_own visible block-wide
+  BSTAMP(5);
   if (slot_stride) {
     if (tid == 0) {
       int acc = 0;
@@ -339,19 +377,20 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
-        const int end = v.ioff[s + 1];
+        const int end = ioff_at(s + 1);
         const int len = end - r;
         const int lng = len > kLongSeg;
         nlong_mine += lng;
-        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k], r, end, v.refs[r],
-                  len > 1 ? v.refs[r + 1] : 0, len > 2 ? v.refs[r + 2] : 0,
-                  len > 3 ? v.refs[r + 3] : 0, lng);
+        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k], r, end, ref_at(r),
+                  len > 1 ? ref_at(r + 1) : 0, len > 2 ? ref_at(r + 2) : 0,
+                  len > 3 ? ref_at(r + 3) : 0, lng);
         ++s;
       }
     }
   }
   __syncthreads();
   int lpre = 0, n_long = 0;
+  BSTAMP(6);
   Scan().exclusive_scan(nlong_mine, lpre, 0, n_long, sscan, rocprim::plus<int>());
   if (nlong_mine) {
     int s = iseg0;
@@ -359,7 +398,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
-        const int end = v.ioff[s + 1];
+        const int end = ioff_at(s + 1);
         if (end - r > kLongSeg) {
           if (lpre < kMaxLongItems)
             store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
@@ -375,35 +414,23 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   // 3. triplet records, now that s_i/s_j hold the final item rows (world 1) or slots, and the
   //    records of user segments with more than one triplet (K2 finishes those users)
   int nmulti_mine = 0;
-  {
-    int s = seg0;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int p = tid * IPT + k;
-      if (uhead[k]) {
-        nmulti_mine += v.useg[s + 1] - p > 1;
-        ++s;
-      }
-    }
-  }
+  for (int k = 0; k < IPT; ++k) nmulti_mine += uhead[k] && uend[k] - (tid * IPT + k) > 1;
   __syncthreads();  // sscan reuse
   int mpre = 0, n_multi = 0;
+  BSTAMP(7);
   Scan().exclusive_scan(nmulti_mine, mpre, 0, n_multi, sscan, rocprim::plus<int>());
-  {
-    int s = seg0 - 1;  // segment of this thread's first position when that is not a head
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int p = tid * IPT + k;
-      if (key[k] == kNone) continue;
-      if (uhead[k]) ++s;
-      const int beg = v.useg[s], end = v.useg[s + 1];
-      const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
-      const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
-      reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], end - beg == 1);
-      if (uhead[k] && end - beg > 1) {
-        store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], beg, end, 0, 0, 0, 0, 0);
-        ++mpre;
-      }
+  for (int k = 0; k < IPT; ++k) {
+    const int p = tid * IPT + k;
+    if (key[k] == kNone) continue;
+    const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
+    const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
+    const int len = uhead[k] ? uend[k] - p : 2;  // a non-head shares its user's segment
+    reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], len == 1);
+    if (len > 1 && uhead[k]) {
+      store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], p, uend[k], 0, 0, 0, 0, 0);
+      ++mpre;
     }
   }
   if (tid < world && slots) v.own[tid] = s_own[tid];
@@ -414,7 +441,14 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     v.meta[3] = min(n_long, kMaxLongItems);
     v.meta[4] = n_multi;
   }
+  BSTAMP(8);
 }
+
+#ifdef BPRMF_BUILD_STAMPS
+extern "C" int bprmf_debug_build_stamps(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), sizeof(uint64_t) * 16) == hipSuccess ? 0 : -3;
+}
+#endif
 
 static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
   int b = 1;

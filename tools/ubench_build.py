@@ -1,0 +1,55 @@
+"""Phase timing of the batch builder (k_build_batches) from a diagnostic build with s_memrealtime
+stamps (-DBPRMF_BUILD_STAMPS): the first workgroup's time per phase, ml-20m shape, B = 4096.
+
+  python tools/ubench_build.py build          # here: compile tools/libbprmf_stamps.so
+  python tools/ubench_build.py                # GPU box: run and print the phase table
+"""
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "tools", "libbprmf_stamps.so")
+PHASES = ["loads", "user sort", "user segments", "item keys+sort", "item heads/refs",
+          "item records", "long items", "triplet records"]
+
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    b = importlib.import_module("recommend-lib_amd.build")
+    print(b.build(force=True, defines=("BPRMF_BUILD_STAMPS",), out=LIB))
+    sys.exit(0)
+
+os.environ["BPRMF_DIAG_LIB"] = LIB
+import ctypes  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+rl = importlib.import_module("recommend-lib_amd")
+syn = importlib.import_module("recommend-lib_amd.synthetic")
+L = rl._lib.load()
+L.bprmf_debug_build_stamps.argtypes = [ctypes.c_void_p]
+pos = syn.make_positives(138493, 26744, 10_000_000, 20261015)
+res = {}
+for radix in ("0", "1"):
+    for split in ("1", "0"):
+        os.environ["BPRMF_SPLIT_BUILD"] = split
+        if radix == "1":
+            os.environ["BPRMF_RADIX_BUILD"] = "1"
+        else:
+            os.environ.pop("BPRMF_RADIX_BUILD", None)
+        m = rl.BPRMF(138493, 26744, 128, batch_size=4096, seed=1, device=0)
+        m.set_train(pos)
+        rows = []
+        for rep in range(5):
+            m.train_steps(0, 20 * rep, 20)
+            st = np.zeros(16, np.uint64)
+            assert L.bprmf_debug_build_stamps(st.ctypes.data) == 0
+            d = np.diff(st[:9].astype(np.int64)) * 0.01  # 100 MHz -> us
+            rows.append(d)
+        med = np.median(np.array(rows[1:]), axis=0)
+        key = f"radix={radix} split={split}"
+        res[key] = {p: round(float(v), 2) for p, v in zip(PHASES, med)}
+        res[key]["total"] = round(float(med.sum()), 2)
+        m.close()
+print(json.dumps(res, indent=1))

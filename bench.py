@@ -106,6 +106,9 @@ def main():
     ap.add_argument("--python-orchestration", action="store_true",
                     help="sharded: per-step Python orchestration over torch.distributed instead of "
                          "the library's runner")
+    ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group backend (gloo: rehearse several ranks on one GPU, IPC "
+                         "transport; RCCL refuses two ranks on one device)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,12 +119,19 @@ def main():
     import torch
     rl = importlib.import_module("recommend-lib_amd")
     syn = importlib.import_module("recommend-lib_amd.synthetic")
+    local = local % max(1, torch.cuda.device_count())  # ranks beyond the GPUs: rehearsal only
     torch.cuda.set_device(local)
     dist = None
     sharded = world > 1 or a.sharded
     if sharded:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if "RANK" not in os.environ:  # --sharded without a launcher: a one-rank group
+            os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=os.environ.get("MASTER_PORT", "29529"))
+        if a.pg_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     U, I, d, B = a.users, a.items, a.factor, a.batch_size
     pos = syn.make_positives(U, I, a.positives, a.seed)
@@ -168,7 +178,8 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         if dist:
-            t = torch.tensor([el], dtype=torch.float64, device="cuda")
+            t = torch.tensor([el], dtype=torch.float64,
+                             device="cuda" if a.pg_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el

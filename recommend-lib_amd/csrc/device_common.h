@@ -108,25 +108,36 @@ static __device__ __forceinline__ void wave_add_loss(double* slots, float v) {
   if ((threadIdx.x & 63) == 0) atomicAdd(&slots[blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)], (double)v);
 }
 
+// One IPC flag wait: spin until *flag >= seq.  A wait that outlives ~10 s (a peer died) raises
+// err bit 4 and gives up instead of hanging the queue; once bit 4 is up (this wait's or an earlier
+// one's), later waits return at once, so a dead peer costs one timeout per call, not one per wait.
+// The flags and the data they guard are uncached, so relaxed polls suffice.
+static __device__ __forceinline__ bool ipc_spin(const int32_t* flag, int32_t seq, int32_t* err) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4) return false;
+  int64_t spins = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    __builtin_amdgcn_s_sleep(2);
+    ++spins;
+    if ((spins & 4095) == 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4))
+      return false;
+    if (spins > 150000000) {
+      atomicOr(err, 4);
+      return false;
+    }
+  }
+  return true;
+}
+
 // Sharded steps over the IPC transport: the first thread of every workgroup waits until each
 // peer's flag (this rank's flag array for one exchange kind, written remotely by the peers' push
-// kernels) reaches the step's sequence number, then the workgroup proceeds.  The flags and the
-// data they guard are uncached, so relaxed polls suffice.  A wait beyond ~10 s (a peer died)
-// raises err bit 4 instead of hanging the queue.
+// kernels) reaches the step's sequence number, then the workgroup proceeds.
 static __device__ __forceinline__ void wait_peer_flags(const int32_t* flags, int world, int self,
                                                        int32_t seq, int32_t* err) {
   if (!flags) return;
   if (threadIdx.x == 0) {
     for (int p = 0; p < world; ++p) {
       if (p == self) continue;
-      int64_t spins = 0;
-      while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > 150000000) {
-          atomicOr(err, 4);
-          break;
-        }
-      }
+      if (!ipc_spin(flags + p, seq, err)) break;
     }
   }
   __syncthreads();

@@ -287,7 +287,7 @@ struct DistGraph {  // a captured chunk of sharded steps (fixed n, cap and buffe
   int64_t n = 0;
   int cap = 0;
   const void* bufs[4] = {};
-  hipGraphExec_t exec = nullptr;
+  hipGraphExec_t exec = nullptr;  // null: seen once, not captured yet
 };
 
 // Buffers of the runner.  Sizes are fixed at attach (peers of the IPC transport hold mappings of
@@ -469,19 +469,30 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
   return 0;
 }
 
+// A chunk shape (n, cap, buffers) is captured the second time it is seen and replayed from then
+// on; the first time its steps are launched eagerly (each step is several kernels of several us,
+// so the host keeps ahead): a short run of odd-length chunks (a benchmark's warm-up and timed
+// calls) then never pays a capture inside a call, and a long run replays graphs.
+// Returns 1 when the caller should enqueue the steps eagerly instead.
 static int launch_dist_graph(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
-                             const int32_t* aplan) {
+                             const int32_t* aplan, bool* eager) {
   DistState* d = h->dist;
   const void* bufs[4] = {h->d_batch, ids_recv, aplan, h->d_contrib};
   DistGraph* ge = nullptr;
   for (auto& g : d->graphs)
     if (g.n == n && g.cap == cap && std::equal(bufs, bufs + 4, g.bufs)) ge = &g;
-  if (!ge) {
-    if (d->graphs.size() >= 8) drop_dist_graphs(d);
+  *eager = false;
+  if (!ge) {  // first sighting: remember the shape, run eagerly
+    if (d->graphs.size() >= 16) drop_dist_graphs(d);
     DistGraph ng;
     ng.n = n;
     ng.cap = cap;
     std::copy(bufs, bufs + 4, ng.bufs);
+    d->graphs.push_back(ng);
+    *eager = true;
+    return 0;
+  }
+  if (!ge->exec) {
     HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     const int rc = enqueue_steps(h, n, cap, ids_recv, aplan, false);
     hipGraph_t graph = nullptr;
@@ -490,11 +501,12 @@ static int launch_dist_graph(bprmf_handle* h, int64_t n, int cap, const int32_t*
       if (graph) (void)!hipGraphDestroy(graph);
       return rc ? rc : fail(BPRMF_E_HIP, "sharded step graph capture: %s", hipGetErrorString(e2));
     }
-    const hipError_t e = hipGraphInstantiate(&ng.exec, graph, nullptr, nullptr, 0);
+    const hipError_t e = hipGraphInstantiate(&ge->exec, graph, nullptr, nullptr, 0);
     (void)!hipGraphDestroy(graph);
-    if (e != hipSuccess) return fail(BPRMF_E_HIP, "sharded step graph instantiate: %s", hipGetErrorString(e));
-    d->graphs.push_back(ng);
-    ge = &d->graphs.back();
+    if (e != hipSuccess) {
+      ge->exec = nullptr;
+      return fail(BPRMF_E_HIP, "sharded step graph instantiate: %s", hipGetErrorString(e));
+    }
   }
   HIPCHK(hipGraphLaunch(ge->exec, h->stream));
   return 0;
@@ -529,10 +541,15 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   HIPCHK(hipMemsetAsync(d->d_cap, 0, 4, h->stream));
   HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
   if (int r = d->tr->max_i32(h, d->d_cap, d->vals + par * W, seq)) return r;
-  int32_t cap = 0;
-  HIPCHK(hipMemcpyAsync(&cap, d->d_cap, 4, hipMemcpyDeviceToHost, h->stream));
+  // cap and the error word back in one synchronisation (pinned staging in the status block)
+  int32_t* hv = reinterpret_cast<int32_t*>(h->h_status + 8);
+  HIPCHK(hipMemcpyAsync(hv, d->d_cap, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(hv + 1, h->d_err, 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  if (int r = check_err_flag(h)) return r;
+  int32_t cap = hv[0];
+  if (hv[1]) {
+    if (int r = check_err_flag(h)) return r;
+  }
   if (cap < 0 || cap > d->S) return fail(BPRMF_E_STATE, "exchange capacity %d outside [0, %d]", cap, d->S);
   const bool graph = h->use_graphs && d->tr->capturable() && cap > 0;
   if (graph) cap = std::min(d->S, (cap + 63) / 64 * 64);  // few distinct plans: graphs get reused
@@ -559,11 +576,11 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));
-  if (graph) {
-    if (int r = launch_dist_graph(h, n, cap, ids_recv, aplan)) return r;
-  } else {
+  bool eager = !graph;
+  if (graph)
+    if (int r = launch_dist_graph(h, n, cap, ids_recv, aplan, &eager)) return r;
+  if (eager)
     if (int r = enqueue_steps(h, n, cap, ids_recv, aplan, !ea)) return r;
-  }
   if (ea) {
     hipEvent_t eb = prof_event(h);
     if (eb) {

@@ -347,24 +347,15 @@ __global__ void k_ipc_push(PushArgs a, int world, int64_t bytes, const int32_t* 
   }
 }
 
-// wait until every peer's flag for this exchange reached its sequence number.  A wait that
-// outlives ~10 s (a peer died) raises err bit 4 and gives up instead of hanging the queue.
+// wait until every peer's flag for this exchange reached its sequence number (ipc_spin: a dead
+// peer raises err bit 4 once, and every later wait of the call returns at once).
 __global__ void k_ipc_wait(const int32_t* flags, int world, int self, const int32_t* __restrict__ tbase,
                            int k, int32_t seq, int32_t* __restrict__ err) {
   const int32_t s = tbase ? *tbase + k + 1 : seq;
   const int p = threadIdx.x;
-  if (p < world && p != self) {
-    int64_t spins = 0;
-    // relaxed: the flag and the data it guards live in uncached memory, so no cache needs
-    // invalidating (an acquire at system scope would invalidate this XCD's L2 every poll)
-    while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > 150000000) {
-        atomicOr(err, 4);
-        break;
-      }
-    }
-  }
+  // relaxed polls: the flag and the data it guards live in uncached memory, so no cache needs
+  // invalidating (an acquire at system scope would invalidate this XCD's L2 every poll)
+  if (p < world && p != self) ipc_spin(flags + p, s, err);
   __syncthreads();
 }
 
@@ -378,16 +369,7 @@ __global__ void k_ipc_recv(PushArgs a, int world, int self, int64_t bytes, int b
   const int p = blockIdx.x / blocks_per_peer;
   if (p >= world || p == self || !a.src[p]) return;
   const int32_t s = tbase ? *tbase + k + 1 : seq;
-  if (threadIdx.x == 0) {
-    int64_t spins = 0;
-    while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > 150000000) {
-        atomicOr(err, 4);
-        break;
-      }
-    }
-  }
+  if (threadIdx.x == 0) ipc_spin(flags + p, s, err);
   __syncthreads();
   const int64_t n16 = bytes / 16, per = n16 + (bytes % 16) / 4;
   const int64_t stride = (int64_t)blocks_per_peer * blockDim.x;

@@ -55,13 +55,14 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
                                                       float* __restrict__ contrib,
                                                       float* __restrict__ ugrad,
                                                       const float* __restrict__ item_rows,
-                                                      PeerWait pw, int64_t bstride) {
+                                                      PeerWait pw, int64_t bstride, int B) {
   const int sub = threadIdx.x & (G4 - 1);
   const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
-  // independent loads: the record (allocated for every p < B), the triplet count, the step base
-  const int4 r = reinterpret_cast<const int4*>(bv.trec)[p];
+  // independent loads: the record, the triplet count, the step base.  The grid covers B rounded
+  // up to whole blocks: the index is clamped into the batch's B records (never read past them)
+  const int4 r = reinterpret_cast<const int4*>(bv.trec)[min(p, B - 1)];
   const int n = bv.meta[0];
   const int32_t t = *tbase + step + 1;
   if (p < n) {
@@ -197,7 +198,8 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   const float* __restrict__ ugrad, int long_blocks,
                                                   int item_blocks, float* __restrict__ grads,
                                                   const float* __restrict__ xloss,
-                                                  double* __restrict__ loss, int64_t bstride) {
+                                                  double* __restrict__ loss, int64_t bstride,
+                                                  int B) {
   constexpr int NG = KB / G4;
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   const int sub = threadIdx.x & (G4 - 1);
@@ -222,7 +224,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
   const int bid = (int)blockIdx.x - (loss ? 1 : 0);
   if (bid >= long_blocks + item_blocks) {  // users with several triplets
     const int m = (bid - long_blocks - item_blocks) * NG + grp;
-    const int4 r0 = reinterpret_cast<const int4*>(bv.mrec + (int64_t)m * kRec)[0];
+    // indices clamped into the batch's record arrays (B/2 user records, 2B item records): the
+    // groups past the count read a valid record and return
+    const int4 r0 = reinterpret_cast<const int4*>(bv.mrec + (int64_t)min(m, max(B / 2 - 1, 0)) * kRec)[0];
     const int n_multi = bv.meta[4];
     if (m >= n_multi) return;
     const int32_t u = r0.x;
@@ -293,8 +297,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     return;
   }
   const int s = (bid - long_blocks) * NG + grp;
-  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
-  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
+  const int sc = min(s, 2 * B - 1);
+  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
+  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
   const int n_iseg = bv.meta[2];
   if (s >= n_iseg || r1.w) return;  // past the batch's items, or a workgroup-served hot item
   const int32_t item = r0.x;
@@ -360,11 +365,11 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
     if (item_rows)
       k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
                                                            contrib, ugrad, item_rows, pw,
-                                                           bstride);
+                                                           bstride, B);
     else
       k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
                                                             contrib, ugrad, nullptr, pw,
-                                                            bstride);
+                                                            bstride, B);
   }));
   return hipGetLastError();
 }
@@ -386,12 +391,12 @@ hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
     if (grads)
       k_item_step<G4_, S_, true, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
                                                            ugrad, long_blocks, item_blocks, grads,
-                                                           xloss, loss, bstride);
+                                                           xloss, loss, bstride, B);
     else
       k_item_step<G4_, S_, false, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
                                                             contrib, ugrad, long_blocks,
                                                             item_blocks, nullptr, xloss, loss,
-                                                            bstride);
+                                                            bstride, B);
   }));
   return hipGetLastError();
 }

@@ -308,12 +308,22 @@ class BPRMF:
             raise ValueError("user, item_i, item_j must have the same number of elements")
         oi = torch.empty(u.numel(), dtype=torch.float32, device=dev)
         oj = torch.empty_like(oi)
-        self.set_stream(torch.cuda.current_stream(dev))
+        # the library runs on a dedicated non-default stream ordered after the caller's (torch's
+        # default stream is handle 0, which bprmf_set_stream reads as "own stream", unordered)
+        caller = torch.cuda.current_stream(dev)
+        if getattr(self, "_fwd_stream", None) is None:
+            self._fwd_stream = torch.cuda.Stream(dev)
+        s = self._fwd_stream
+        s.wait_stream(caller)
+        self.set_stream(s)
         try:
             _lib.check(self._L.bprmf_forward_dev(self._h, u.data_ptr(), i.data_ptr(), j.data_ptr(),
                                                  u.numel(), oi.data_ptr(), oj.data_ptr()))
         finally:
             self.set_stream(None)
+        caller.wait_stream(s)
+        for t in (u, i, j, oi, oj):
+            t.record_stream(s)
         oi, oj = oi.reshape(shape), oj.reshape(shape)
         if back_to_cpu:
             oi, oj = oi.cpu(), oj.cpu()

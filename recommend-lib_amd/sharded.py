@@ -157,9 +157,17 @@ class HipShard:
         import torch
         self.device = torch.device("cuda", device)
 
-    def bind_stream(self):
+    def stream(self):
+        """The dedicated (non-default) torch stream every per-step phase runs on.  The library
+        and torch's collectives are ordered on it; binding torch's default stream instead would
+        hand the library handle 0, which bprmf_set_stream reads as "the handle's own stream"."""
         import torch
-        self.m.set_stream(torch.cuda.current_stream(self.device))
+        if getattr(self, "_stream", None) is None:
+            self._stream = torch.cuda.Stream(self.device)
+        return self._stream
+
+    def bind_stream(self):
+        self.m.set_stream(self.stream())
 
     def set_train(self, pos):
         self.m.set_train(pos)
@@ -206,12 +214,19 @@ class HipShard:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         _lib.check(self.L.bprmf_dist_init_rccl(self.h, ctypes.addressof(buf)))
 
-    def runner_ipc(self, all_gather_bytes):
+    def ipc_export(self):
+        """This rank's IPC handles (raises on failure)."""
         blob = (ctypes.c_uint8 * _lib.IPC_BLOB_BYTES)()
         _lib.check(self.L.bprmf_dist_ipc_export(self.h, ctypes.addressof(blob)))
-        blobs = b"".join(all_gather_bytes(bytes(blob)))
+        return bytes(blob)
+
+    def ipc_init(self, blobs):
         allb = (ctypes.c_uint8 * len(blobs)).from_buffer_copy(blobs)
         _lib.check(self.L.bprmf_dist_init_ipc(self.h, ctypes.addressof(allb)))
+
+    def runner_ipc(self, all_gather_bytes):
+        blob = self.ipc_export()
+        self.ipc_init(b"".join(all_gather_bytes(blob)))
 
     def runner_loopback(self, key):
         _lib.check(self.L.bprmf_dist_init_loopback(self.h, int(key)))
@@ -327,11 +342,23 @@ class ShardedBPRMF:
         elif transport == "ipc":
             self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
         elif transport == "auto":  # ipc where every rank can map its peers, else rccl
-            ok = 1
+            # Every rank joins every collective whatever failed locally: a status byte travels
+            # with the handles, so a rank whose export failed cannot leave its peers waiting in
+            # the all-gather, and the fallback is agreed on by all ranks together.
+            ok, blob = 1, bytes(_lib.IPC_BLOB_BYTES)
             try:
-                self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
+                blob = self.b.ipc_export()
             except Exception as e:  # noqa: BLE001 (reported, then the fallback is agreed on)
                 self.transport_error = str(e)
+                ok = 0
+            got = self.comm.all_gather_bytes(bytes([ok]) + blob, self.device)
+            if all(g[0] == 1 for g in got):
+                try:
+                    self.b.ipc_init(b"".join(g[1:] for g in got))
+                except Exception as e:  # noqa: BLE001
+                    self.transport_error = str(e)
+                    ok = 0
+            else:
                 ok = 0
             if -self.comm.allreduce_max(-ok, self.device) == 1:
                 transport = "ipc"
@@ -365,13 +392,28 @@ class ShardedBPRMF:
         return self._run(k, want_loss)
 
     def _run(self, k, want_loss):
+        import contextlib
+        import torch
+        if hasattr(self.b, "stream"):
+            # one non-default stream for the library's kernels, torch's allocations and the
+            # collectives, then the caller's stream waits for it
+            s = self.b.stream()
+            self.b.bind_stream()
+            caller = torch.cuda.current_stream(self.device)
+            s.wait_stream(caller)
+            with torch.cuda.stream(s):
+                out = self._run_on_stream(k, want_loss)
+            caller.wait_stream(s)
+            return out
+        with contextlib.nullcontext():
+            return self._run_on_stream(k, want_loss)
+
+    def _run_on_stream(self, k, want_loss):
         import torch
         _, _, _, send, recv = self._plan
         sc, rc = send[k], recv[k]
         ns, nr = int(sc.sum()), int(rc.sum())
         dev, ld = self.device, self.ld
-        if hasattr(self.b, "bind_stream"):
-            self.b.bind_stream()
         ids = torch.empty(max(ns, 1), dtype=torch.int32, device=dev)
         self.b.request_ids(k, ids, ns)
         rids = torch.empty(max(nr, 1), dtype=torch.int32, device=dev)

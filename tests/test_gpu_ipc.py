@@ -25,30 +25,51 @@ def _free_port():
     return p
 
 
-def _run_workers(tmp_path, spec, mode, world=2):
+def _run_workers(tmp_path, spec, mode, world=2, timeout=300):
+    """Start `world` worker processes, each logging to its own file; poll them together and stop
+    the rest as soon as one fails, so a crash on one rank reports that rank's log instead of a
+    peer's timeout (and no pipe can fill while another worker is being waited on)."""
+    import time
     spec_path = str(tmp_path / f"spec_{mode}.npz")
     np.savez(spec_path, **spec)
     port = _free_port()
-    procs, outs = [], []
+    procs, outs, logs = [], [], []
     for r in range(world):
         out = str(tmp_path / f"out_{mode}_{r}.npz")
         outs.append(out)
+        log = str(tmp_path / f"log_{mode}_{r}.txt")
+        logs.append(log)
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
                    WORLD_SIZE=str(world), LOCAL_RANK="0", IPC_SPEC=spec_path)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ipc_worker.py"),
-                                       out, mode], env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.STDOUT, text=True))
-    logs = []
+        with open(log, "w") as lf:
+            procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ipc_worker.py"),
+                                           out, mode], env=env, stdout=lf, stderr=subprocess.STDOUT))
+
+    def tail(r):
+        with open(logs[r]) as f:
+            return f.read()[-3000:]
+
+    deadline = time.monotonic() + timeout
+    failed = None
     try:
-        for p in procs:
-            o, _ = p.communicate(timeout=300)
-            logs.append(o)
+        while time.monotonic() < deadline:
+            codes = [p.poll() for p in procs]
+            bad = [r for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.2)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for p, o in zip(procs, logs):
-        assert p.returncode == 0, o[-3000:]
+                p.wait()
+    if failed is not None:
+        raise AssertionError(f"worker {failed} exited {procs[failed].returncode}:\n{tail(failed)}")
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"worker {r} did not finish in {timeout} s:\n{tail(r)}"
     return [dict(np.load(o)) for o in outs]
 
 

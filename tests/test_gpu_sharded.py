@@ -266,8 +266,9 @@ def test_runner_rccl_transport_one_rank(rl):
                         os.environ.pop(k)
                     else:
                         os.environ[k] = v
-            m.train_replay(batches)
-            m.train_replay(batches)  # second call: the cached graph is replayed
+            m.train_replay(batches)  # first sighting of the chunk shape: eager launches
+            m.train_replay(batches)  # second: captured into a hipGraph
+            m.train_replay(batches)  # third: the cached graph is replayed
             res.append(m.get_weights())
     finally:
         if own:
@@ -275,3 +276,44 @@ def test_runner_rccl_transport_one_rank(rl):
     for r in res[1:]:
         for x, y in zip(res[0], r):
             assert np.array_equal(x, y)
+
+
+def test_python_orchestrated_steps_over_nccl_world1(rl):
+    """The per-step Python path (plan_replay + step_replay over TorchComm on nccl = RCCL) at world
+    1 against the dense oracle: the library's kernels and torch's collectives and allocations run
+    on one dedicated non-default stream, from torch's default stream and from a side stream."""
+    import os
+    import torch
+    import torch.distributed as dist
+    g = np.random.default_rng(17)
+    P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, D))).astype(np.float32)
+    batches = _batches(g, 6, 512)
+    sh = rl.sharded
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29534")
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        outs = []
+        for side in (False, True):
+            m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=512, device=0)
+            m.set_weights(P0, Q0)
+            m.plan_replay(batches)
+            ctx = torch.cuda.stream(torch.cuda.Stream(0)) if side else torch.cuda.stream(
+                torch.cuda.current_stream(0))
+            with ctx:
+                for k in range(len(batches)):
+                    m.step_replay(k)
+            torch.cuda.synchronize()
+            outs.append(m.get_weights())
+    finally:
+        if own:
+            dist.destroy_process_group()
+    Pr, Qr = P0.copy(), Q0.copy()
+    for u, i, j in batches:
+        O.bpr_step_dense(Pr, Qr, u, i, j, 0.05, 0.01)
+    for P, Q in outs:
+        np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)

@@ -294,12 +294,13 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   h->feistel_h = hb;
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
   // the first calls (a larger chunk later would reallocate and recapture)
-  if (h->cfg.world == 1 && seg_mode(h)) {
+  if (seg_mode(h)) {
     const int64_t B = h->cfg.batch_size;
-    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(chunk_triplets(h) / B, ((int64_t)N + B - 1) / B));
+    const int64_t steps = h->cfg.world == 1 ? chunk_triplets(h) / B : dist_chunk_steps(h);
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(steps, ((int64_t)N + B - 1) / B));
     if (int r = ensure_seg(h, nb)) return r;
     if (int r = ensure_trip(h, nb * B)) return r;
-    if (h->use_graphs)
+    if (h->cfg.world == 1 && h->use_graphs)
       if (int r = ensure_step_graphs(h)) return r;
   }
   return 0;
@@ -394,6 +395,16 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
     st->seconds = host_seconds() - h->call_t0;
   }
   return 0;
+}
+
+// sampled chunks of at most this many batches draw their triplets with the grid-wide sampler
+// first and build from those (the builder then has no sampler latency: one workgroup per batch
+// cannot hide it when a chunk is short); longer chunks sample inside the builder, whose
+// workgroups then fill the chip anyway.  BPRMF_SPLIT_BUILD=0/1 forces either.
+bool bprmf::split_build(int64_t nb) {
+  const char* e = getenv("BPRMF_SPLIT_BUILD");
+  if (e && *e) return e[0] != '0';
+  return nb <= 512;
 }
 
 bool bprmf::seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSegBatch; }
@@ -519,15 +530,6 @@ static int launch_step_graph(bprmf_handle* h, int64_t nb) {
   return 0;
 }
 
-// sampled chunks of at most this many batches draw their triplets with the grid-wide sampler
-// first and build from those (the builder then has no sampler latency: one workgroup per batch
-// cannot hide it when a chunk is short); longer chunks sample inside the builder, whose
-// workgroups then fill the chip anyway.  BPRMF_SPLIT_BUILD=0/1 forces either.
-static bool split_build(int64_t nb) {
-  const char* e = getenv("BPRMF_SPLIT_BUILD");
-  if (e && *e) return e[0] != '0';
-  return nb <= 512;
-}
 
 // One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler
 // (ru == nullptr) or replayed device ids ru/ri/rj[0..n).  Segmented path for B <= kMaxSegBatch:

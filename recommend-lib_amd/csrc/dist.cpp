@@ -332,9 +332,11 @@ void dist_free(DistState* d) {
   delete d;
 }
 
-static int64_t dist_chunk_steps(const bprmf_handle* h) {
+int64_t dist_chunk_steps(const bprmf_handle* h) {
   return std::max<int64_t>(1, (int64_t(1) << 20) / h->cfg.batch_size);
 }
+
+static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap);
 
 static int dist_attach(bprmf_handle* h, Transport* tr) {
   if (!seg_mode(h)) {
@@ -369,6 +371,10 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   if (int r = dalloc(&d->ids_send, ids)) return r;
   if (int r = dalloc(&d->rows_send, rows)) return r;
   if (int r = dalloc(&d->grads_send, rows)) return r;
+  // both parities' apply plans at their largest (a full chunk at the largest capacity), so no
+  // chunk ever reallocates one inside a call (a free synchronises the device)
+  for (int par = 0; par < 2; ++par)
+    if (int r = ensure_aplan(h, par, d->nmax, d->S)) return r;
   // rows past a peer's request count are sent but never read; keep them finite
   HIPCHK(hipMemsetAsync(d->rows_send, 0, sizeof(float) * rows, h->stream));
   HIPCHK(hipMemsetAsync(d->grads_send, 0, sizeof(float) * rows, h->stream));
@@ -534,8 +540,18 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   }
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
-    HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
-                         h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream));
+    if (!ru && n_slots > 0 && split_build(n)) {  // short chunk: grid-wide sampler first
+      if (int r = ensure_trip(h, n_slots)) return r;
+      int32_t* tu = h->d_trip;
+      HIPCHK(sample(sampler_args(h), epoch, first_slot, n_slots, tu, tu + h->trip_cap,
+                    tu + 2 * h->trip_cap, h->d_err, h->stream));
+      HIPCHK(build_batches(sampler_args(h), epoch, 0, n_slots, B, tu, tu + h->trip_cap,
+                           tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true, d->S, n, bb,
+                           h->d_err, h->stream));
+    } else {
+      HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
+                           h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream));
+    }
   }
   // exchange capacity of the chunk: the largest request count of any (rank, step, owner)
   HIPCHK(hipMemsetAsync(d->d_cap, 0, 4, h->stream));

@@ -119,6 +119,9 @@ int ensure_trip(bprmf_handle* h, int64_t n);
 int ensure_seg(bprmf_handle* h, int64_t n_batches);
 int ensure_grad(bprmf_handle* h);
 bool seg_mode(const bprmf_handle* h);
+// a sampled chunk of nb batches draws its triplets with the grid-wide sampler before the builder
+bool split_build(int64_t nb);
+int64_t dist_chunk_steps(const bprmf_handle* h);  // steps per chunk of the sharded runner
 int check_err_flag(bprmf_handle* h);
 SamplerArgs sampler_args(bprmf_handle* h);
 int read_loss(bprmf_handle* h, double* loss);

@@ -351,7 +351,7 @@ int bprmf::read_loss(bprmf_handle* h, double* loss) {
 int bprmf::loss_zero_slots(bprmf_handle* h) {
   if (!h->loss_pending) return 0;
   h->loss_pending = false;
-  const int n = h->slots_dirty ? kLossSlots : 1;
+  const int n = h->slots_dirty ? kLossSlots : kSegLossSlots;
   h->slots_dirty = false;
   return n;
 }
@@ -374,7 +374,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
     HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * kLossSlots,
                           hipMemcpyDeviceToHost, h->stream));
   } else {
-    HIPCHK(status_out(h->d_status, h->h_status_dev, 3, h->stream));
+    HIPCHK(status_out(h->d_status, h->h_status_dev, 2 + kSegLossSlots, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   const int32_t e = *reinterpret_cast<const volatile int32_t*>(h->h_status);
@@ -387,7 +387,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   const volatile double* slots = reinterpret_cast<const volatile double*>(h->h_status + 16);
   double loss = 0;
   if (ran)
-    for (int k = 0; k < (h->call_slots ? kLossSlots : 1); ++k) loss += slots[k];
+    for (int k = 0; k < (h->call_slots ? kLossSlots : kSegLossSlots); ++k) loss += slots[k];
   if (st) {
     st->triplets = triplets;
     st->steps = steps;
@@ -565,10 +565,10 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
       HIPCHK(build_batches(sampler_args(h), epoch, 0, n, (int)B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, 1, false, 0, nb, bb,
-                           h->d_err, h->stream));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
-                           h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream));
+                           h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     }
   }
   HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
@@ -946,7 +946,7 @@ int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, (int)B, nullptr, nullptr,
                          nullptr, h->U, h->cfg.item_num, h->cfg.world, true, 0, n_steps, bb, h->d_err,
-                         h->stream));
+                         h->stream, k1_triplets_per_block(h->geom)));
   }
   return dist_counts(h, n_steps, owner_counts);
 }
@@ -974,7 +974,7 @@ int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, 
   HIPCHK(hipMemcpyAsync(tj, j, 4 * n, hipMemcpyHostToDevice, h->stream));
   const BatchBuf bb{h->d_batch, (int)B};
   HIPCHK(build_batches(sampler_args(h), 0, 0, n, (int)B, tu, ti, tj, h->U, h->cfg.item_num,
-                       h->cfg.world, true, 0, n_steps, bb, h->d_err, h->stream));
+                       h->cfg.world, true, 0, n_steps, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
   return dist_counts(h, n_steps, owner_counts);
 }
 

@@ -547,10 +547,10 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
       HIPCHK(build_batches(sampler_args(h), epoch, 0, n_slots, B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true, d->S, n, bb,
-                           h->d_err, h->stream));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
-                           h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream));
+                           h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     }
   }
   // exchange capacity of the chunk: the largest request count of any (rank, step, owner)

@@ -13,6 +13,7 @@ namespace bprmf {
 // per-wave loss partial slots of the step kernels: grid <= kMaxGridBlocks blocks of 4 waves
 constexpr int kMaxGridBlocks = 256 * 8;
 constexpr int kLossSlots = kMaxGridBlocks * 4;
+constexpr int kSegLossSlots = 32;  // loss slots of the segmented step (item_step's loss workgroups)
 
 struct Geom {
   int D, G, EPL, ld;
@@ -30,11 +31,15 @@ struct Table {
 
 // One batch of a step, as laid out by k_build_batches (int32, positions within the batch).  Every
 // step kernel reaches its rows after ONE dependent load of a 16- or 32-byte record:
-//   trec  [B][4]    per triplet, sorted by (local) user row: {i, j, u, single}; single = the user
-//                   has no other triplet in the batch (K1 then updates the user row itself)
-//   mrec  [B/2][8]  user segments with more than one triplet: {u, beg, end, 0...} (meta[4] of them;
-//                   K2 sums their per-triplet user gradients in position order)
-//   irec  [2B][8]   item segment s: {item, beg, end, ref0..ref3, long}        (meta[2] of them)
+//   trec  [B][4]    per triplet, sorted by (local) user row: {i, j, u, w}; w = 1: the user has no
+//                   other triplet in the batch (K1 updates the user row itself); w >= 2: head of the
+//                   user's segment of w triplets, all in one K1 workgroup (K1 sums it in LDS and
+//                   updates the row); w = -1: another member of such a segment; w = 0: a segment
+//                   spanning K1 workgroups (K2 finishes it)
+//   mrec  [B/2][8]  the w = 0 user segments: {u, beg, end, 0...} (meta[4] of them; K2 sums their
+//                   per-triplet user gradients in position order)
+//   irec  [2B][8]   item segment s: {item, beg | len << 15 | long << 30, refs 0..11 two per int
+//                   (16-bit halves, low first)}                                 (meta[2] of them)
 //                   (sharded mode: item = the segment's slot)
 //   lrec  [B/8][8]  copies of the records of item segments with > kLongSeg references (meta[3];
 //                   at most 2B/(kLongSeg+1) < B/8 of them)
@@ -48,6 +53,7 @@ struct Table {
 // In sharded mode trec holds item SLOTS (rows of the exchange buffers) instead of item rows.
 constexpr int kRec = 8;
 constexpr int kLongSeg = 16;
+constexpr int kInlineRefs = 12;  // refs held in an item segment's record (B <= 8192: 14-bit refs)
 constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
 constexpr int kMaxWorld = 64;
 struct BatchView {
@@ -123,7 +129,9 @@ hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
-                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s);
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb);
+// triplets per K1 workgroup for a geometry (the builder marks user segments that lie in one)
+int k1_triplets_per_block(const Geom& g);
 // sharded K1 over the IPC transport: wait for the peers' row flags first (flags == null: none)
 struct PeerWait {
   const int32_t* flags = nullptr;
@@ -142,7 +150,8 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 // K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
 // grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items).
 // loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
-// left in xloss[B], to loss[0] (fixed-order f64 tree)
+// x K1 left in xloss, to loss[0 .. ceil(B / 256)) (one slot per loss workgroup, fixed order;
+// at most kSegLossSlots slots)
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss = nullptr,

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
     int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int slot_stride,
-    int user_bits, int item_bits, BatchBuf bb, int32_t* __restrict__ err) {
+    int user_bits, int item_bits, int tpb, BatchBuf bb, int32_t* __restrict__ err) {
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -264,6 +264,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   Scan().exclusive_scan(valid, vpre, 0, nvalid, sscan, rocprim::plus<int>());
   bool uhead[IPT];
   int uend[IPT];  // a head's segment end (users repeat a few times per batch at most)
+  // trec.w: 1 = the user's only triplet; >= 2 = head of a segment of that length that lies in one
+  // K1 workgroup (tpb consecutive positions: K1 sums it in LDS and updates the user); -1 = another
+  // member of such a segment; 0 = a segment across workgroups (K2 sums its ugrad rows, mrec)
+  int uw[IPT];
   {
     int s = seg0;
 #pragma unroll
@@ -271,9 +275,21 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       const int p = tid * IPT + k;
       uhead[k] = key[k] != kNone && (p == 0 || s_key[p - 1] != key[k]);
       uend[k] = p + 1;
+      uw[k] = 0;
       if (uhead[k]) {
         v.useg[s++] = p;
         while (uend[k] < nvalid && s_key[uend[k]] == key[k]) ++uend[k];
+      }
+      if (key[k] != kNone) {  // this position's segment, searched at most tpb positions each way
+        int b = p, e = p + 1;
+        while (b > 0 && p - b < tpb && s_key[b - 1] == key[k]) --b;
+        while (e < nvalid && e - p < tpb && s_key[e] == key[k]) ++e;
+        const bool whole = !(b > 0 && s_key[b - 1] == key[k]) && !(e < nvalid && s_key[e] == key[k]);
+        const int len = e - b;
+        if (len == 1)
+          uw[k] = 1;
+        else if (whole && b / tpb == (e - 1) / tpb)
+          uw[k] = p == b ? len : -1;
       }
     }
   }
@@ -381,9 +397,15 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         const int len = end - r;
         const int lng = len > kLongSeg;
         nlong_mine += lng;
-        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k], r, end, ref_at(r),
-                  len > 1 ? ref_at(r + 1) : 0, len > 2 ? ref_at(r + 2) : 0,
-                  len > 3 ? ref_at(r + 3) : 0, lng);
+        int pk[kInlineRefs / 2];
+#pragma unroll
+        for (int m = 0; m < kInlineRefs / 2; ++m) {
+          const int a = 2 * m < len ? ref_at(r + 2 * m) : 0;
+          const int b = 2 * m + 1 < len ? ref_at(r + 2 * m + 1) : 0;
+          pk[m] = a | (b << 16);
+        }
+        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k],
+                  r | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
         ++s;
       }
     }
@@ -403,7 +425,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
           if (lpre < kMaxLongItems)
             store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
           else
-            v.irec[(int64_t)s * kRec + 7] = 0;  // over the cap: served by the short path
+            v.irec[(int64_t)s * kRec + 1] = r | ((end - r) << 15);  // over the cap: short path
           ++lpre;
         }
         ++s;
@@ -415,7 +437,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   //    records of user segments with more than one triplet (K2 finishes those users)
   int nmulti_mine = 0;
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) nmulti_mine += uhead[k] && uend[k] - (tid * IPT + k) > 1;
+  for (int k = 0; k < IPT; ++k) nmulti_mine += uhead[k] && uw[k] == 0;
   __syncthreads();  // sscan reuse
   int mpre = 0, n_multi = 0;
   BSTAMP(7);
@@ -426,9 +448,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     if (key[k] == kNone) continue;
     const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
     const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
-    const int len = uhead[k] ? uend[k] - p : 2;  // a non-head shares its user's segment
-    reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], len == 1);
-    if (len > 1 && uhead[k]) {
+    reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], uw[k]);
+    if (uhead[k] && uw[k] == 0) {  // a segment K2 finishes
       store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], p, uend[k], 0, 0, 0, 0, 0);
       ++mpre;
     }
@@ -459,7 +480,7 @@ static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
-                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s) {
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb) {
   if (n_batches <= 0) return hipSuccess;
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
   const int64_t iloc = (i_rows + world - 1) / world;
@@ -471,15 +492,15 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   if (B <= kBuildThreads * 4 && !radix)
     k_build_batches<4, true><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
   else if (B <= kBuildThreads * 4)
     k_build_batches<4, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
   else
     k_build_batches<8, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
   return hipGetLastError();
 }
 

@@ -16,14 +16,60 @@
 // Row layout: G4 lanes per row, each lane one float4 per stripe (16 B/lane, whole 64..1024 B rows
 // per wave instruction); 64/G4 rows per wave.  Nothing here is an atomic: every output row has
 // exactly one writer, so the result does not depend on scheduling.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "device_common.h"
 
 namespace bprmf {
 
+// diagnostic build only (-DBPRMF_STEP_STAMPS, tools/ubench_step_stamps.py): per workgroup,
+// s_memrealtime at entry, after its record load, after its row loads / sums, and after its stores
+// drained (thread 0; the waits serialise that thread, so the stamps bound each phase from above).
+#ifdef BPRMF_STEP_STAMPS
+__device__ uint64_t g_step_stamps[2][8192][6];
+#define SSTAMP(kern, k)                                                           \
+  do {                                                                            \
+    if (threadIdx.x == 0) {                                                       \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
+      g_step_stamps[kern][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();      \
+    }                                                                             \
+  } while (0)
+#define SROLE(kern, r)                                                            \
+  do {                                                                            \
+    if (threadIdx.x == 0) g_step_stamps[kern][blockIdx.x][5] = (r);               \
+  } while (0)
+extern "C" int bprmf_debug_step_stamps(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)) == hipSuccess ? 0 : -3;
+}
+#else
+#define SSTAMP(kern, k) \
+  do {                  \
+  } while (0)
+#define SROLE(kern, r) \
+  do {                 \
+  } while (0)
+#endif
+
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// A row the NEXT kernel reads (or the next step's kernels), stored write-through (sc1): the line
+// leaves the XCD's L2 as it is written instead of staying dirty there, so the kernel boundary has
+// no L2 write-back of it to wait for (MI355X_MICROARCH.md: boundary + B / 6 TB/s of dirty bytes).
+// Plain vector store form, one per lane (no scalar-cache store).
+template <bool WT>
+static __device__ __forceinline__ void st4o(float* p, float4 v) {
+  if constexpr (WT) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = {v.x, v.y, v.z, v.w};
+    // s_nop: the wait states the compiler inserts after its own >8-byte vector stores before a
+    // VALU may overwrite their data registers (it cannot see inside the asm to do so)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
 static __device__ __forceinline__ float4 scale4(float4 a, float s) {
   return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }
@@ -48,7 +94,7 @@ static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, floa
 
 // K1, one lane group per triplet p (sorted by user).  SH (sharded): i/j are slots of item_rows,
 // the rows the owners sent for this step, already brought to step t-1 by the owner (no stamps).
-template <int G4, int S, bool SH>
+template <int G4, int S, bool SH, bool WT>
 __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
                                                       int ld, const int32_t* __restrict__ tbase,
                                                       int step, float* __restrict__ xloss,
@@ -56,6 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
                                                       float* __restrict__ ugrad,
                                                       const float* __restrict__ item_rows,
                                                       PeerWait pw, int64_t bstride, int B) {
+  SSTAMP(0, 0);
   const int sub = threadIdx.x & (G4 - 1);
   const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
@@ -65,16 +112,25 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[min(p, B - 1)];
   const int n = bv.meta[0];
   const int32_t t = *tbase + step + 1;
+  SSTAMP(0, 1);
+  // kept past the workgroup barrier for an in-workgroup segment head (w >= 2)
+  float4 pu[S];
+  float* prow = nullptr;
+  int w = 0;
+  int32_t u = 0;
+  __shared__ float4 s_g[S * kBlock];  // per-triplet user gradients of in-workgroup segments
   if (p < n) {
-    const int32_t i = r.x, j = r.y, u = r.z;
-    float* pw = P.W + (int64_t)u * ld + 4 * sub;
+    const int32_t i = r.x, j = r.y;
+    u = r.z;
+    w = r.w;
+    prow = P.W + (int64_t)u * ld + 4 * sub;
     const float* qbase = SH ? item_rows : Q.W;
     const float* qi = qbase + (int64_t)i * ld + 4 * sub;
     const float* qj = qbase + (int64_t)j * ld + 4 * sub;
-    float4 pu[S], vi[S], vj[S];
+    float4 vi[S], vj[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      pu[k] = ld4(pw + 4 * G4 * k);
+      pu[k] = ld4(prow + 4 * G4 * k);
       vi[k] = ld4(qi + 4 * G4 * k);
       vj[k] = ld4(qj + 4 * G4 * k);
     }
@@ -94,22 +150,44 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
     di = group_sum<G4>(di);
     dj = group_sum<G4>(dj);
     const float x = di - dj;
+    SSTAMP(0, 2);
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
     if (sub == 0 && xloss) xloss[p] = x;  // K2 sums the loss terms
     float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4(cb + 4 * G4 * k, scale4(pu[k], c));
-    if (r.w) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
+    for (int k = 0; k < S; ++k) st4o<WT>(cb + 4 * G4 * k, scale4(pu[k], c));
+    if (w == 1) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
 #pragma unroll
       for (int k = 0; k < S; ++k)
-        st4(pw + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
+        st4o<WT>(prow + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
       if (sub == 0) P.stamp[u] = t;
-    } else {  // K2 sums the segment's gradients in position order
+    } else if (w == 0) {  // a segment across workgroups: K2 sums its gradients in position order
       float* ub = ugrad + (int64_t)p * ld + 4 * sub;
 #pragma unroll
-      for (int k = 0; k < S; ++k) st4(ub + 4 * G4 * k, scale4(sub4(vi[k], vj[k]), -c));
+      for (int k = 0; k < S; ++k) st4o<WT>(ub + 4 * G4 * k, scale4(sub4(vi[k], vj[k]), -c));
+    } else {  // a segment inside this workgroup: its head finishes it below
+#pragma unroll
+      for (int k = 0; k < S; ++k) s_g[k * kBlock + threadIdx.x] = scale4(sub4(vi[k], vj[k]), -c);
     }
   }
+  // The head of an in-workgroup segment adds its members' gradients in position order (K2's
+  // order and arithmetic for the same segment) and applies SGD + decay: most users with several
+  // triplets in a batch never wait for K2.
+  __syncthreads();
+  if (w >= 2) {
+    const int q0 = threadIdx.x - sub;  // = (this triplet's slot in the workgroup) * G4
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int m = 0; m < w; ++m) {
+        const float4 x = s_g[k * kBlock + q0 + m * G4 + sub];
+        g = make_float4(g.x + x.x, g.y + x.y, g.z + x.z, g.w + x.w);
+      }
+      st4o<WT>(prow + 4 * G4 * k, sgd4(pu[k], g, hp.lr, hp.wd));
+    }
+    if (sub == 0) P.stamp[u] = t;
+  }
+  SSTAMP(0, 3);
 }
 
 // an item row and its stamp, loaded as soon as the segment's record is known so the loads run
@@ -145,7 +223,7 @@ static __device__ __forceinline__ void acc_ref(float4 (&g)[S], const float4 (&ro
 
 // finish one item segment: apply W = V - lr (g + wd V) to the preloaded row (single GPU) or hand
 // the gradient to the exchange (sharded)
-template <int G4, int S, bool SH>
+template <int G4, int S, bool SH, bool WT>
 static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int slot,
                                                    const float4 (&g)[S], const ItemRow<G4, S, SH>& row,
                                                    const Hyper& hp, int ld, int32_t t, int sub,
@@ -153,12 +231,12 @@ static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int sl
   if (SH) {
     float* o = grads + (int64_t)slot * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4(o + 4 * G4 * k, g[k]);
+    for (int k = 0; k < S; ++k) st4o<WT>(o + 4 * G4 * k, g[k]);
   } else {
     float* w = Q.W + (int64_t)item * ld + 4 * sub;
     const float f = decay_pow(hp.log2a, t - 1 - row.stamp);
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4(w + 4 * G4 * k, sgd4(scale4(row.x[k], f), g[k], hp.lr, hp.wd));
+    for (int k = 0; k < S; ++k) st4o<WT>(w + 4 * G4 * k, sgd4(scale4(row.x[k], f), g[k], hp.lr, hp.wd));
     if (sub == 0) Q.stamp[item] = t;
   }
 }
@@ -191,7 +269,7 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
 
 // KB threads per block: 1024 (512 for rows over 1 KB) so a hot item's workgroup has 16-32 lane
 // groups fetching its references in parallel
-template <int G4, int S, bool SH, int KB>
+template <int G4, int S, bool SH, int KB, bool WT>
 __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp, int ld,
                                                   const int32_t* __restrict__ tbase, int step,
                                                   const float* __restrict__ contrib,
@@ -201,33 +279,40 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   double* __restrict__ loss, int64_t bstride,
                                                   int B) {
   constexpr int NG = KB / G4;
+  SSTAMP(1, 0);
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
   const int32_t t = *tbase + step + 1;
-  if (loss && blockIdx.x == 0) {  // the step's loss (first block: dispatched first, off the tail)
+  // the step's loss: the first loss_blocks(B, KB) workgroups (dispatched first, off the tail) each
+  // sum log(1 + e^-x) over KB triplets, one per thread, in a fixed tree, and add it to their own
+  // slot loss[b] (one writer per slot per launch; the host adds the slots once per call)
+  const int lb = loss ? (B + KB - 1) / KB : 0;
+  if ((int)blockIdx.x < lb) {
     __shared__ double red[KB / 64];
     const int n = bv.meta[0];
-    double acc = 0.0;
-    for (int p = threadIdx.x; p < n; p += KB) acc += (double)softplus(-xloss[p]);
+    const int p = blockIdx.x * KB + threadIdx.x;
+    double acc = p < n ? (double)softplus(-xloss[p]) : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);  // fixed butterfly
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) {  // the only writer of this slot in the launch
+    if (threadIdx.x == 0) {
       double tot = 0.0;
       for (int w = 0; w < KB / 64; ++w) tot += red[w];
-      loss[0] += tot;
+      loss[blockIdx.x] += tot;
     }
     return;
   }
-  const int bid = (int)blockIdx.x - (loss ? 1 : 0);
+  const int bid = (int)blockIdx.x - lb;
   if (bid >= long_blocks + item_blocks) {  // users with several triplets
     const int m = (bid - long_blocks - item_blocks) * NG + grp;
     // indices clamped into the batch's record arrays (B/2 user records, 2B item records): the
     // groups past the count read a valid record and return
     const int4 r0 = reinterpret_cast<const int4*>(bv.mrec + (int64_t)min(m, max(B / 2 - 1, 0)) * kRec)[0];
     const int n_multi = bv.meta[4];
+    SSTAMP(1, 1);
+    SROLE(1, 3);
     if (m >= n_multi) return;
     const int32_t u = r0.x;
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
@@ -236,16 +321,20 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     for (int k = 0; k < S; ++k) cur[k] = ld4(pw + 4 * G4 * k);
     const int32_t su = P.stamp[u];
     sum_rows<G4, S>(g, ugrad, r0.y, r0.z, ld, sub);
+    SSTAMP(1, 2);
     const float f = decay_pow(hp.log2a, t - 1 - su);
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4(pw + 4 * G4 * k, sgd4(scale4(cur[k], f), g[k], hp.lr, hp.wd));
+    for (int k = 0; k < S; ++k) st4o<WT>(pw + 4 * G4 * k, sgd4(scale4(cur[k], f), g[k], hp.lr, hp.wd));
     if (sub == 0) P.stamp[u] = t;
+    SSTAMP(1, 3);
     return;
   }
   if (bid < long_blocks) {
     __shared__ float4 part[NG][G4 * S];
     const int4 r0 = reinterpret_cast<const int4*>(bv.lrec + (int64_t)bid * kRec)[0];
     const int n_long = bv.meta[3];
+    SSTAMP(1, 1);
+    SROLE(1, 1);
     if (bid >= n_long) return;  // uniform over the block
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
@@ -292,8 +381,10 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     if (grp == 0) {
 #pragma unroll
       for (int k = 0; k < S; ++k) g[k] = part[0][sub + G4 * k];
-      finish_item<G4, S, SH>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
+      SSTAMP(1, 2);
+      finish_item<G4, S, SH, WT>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
     }
+    SSTAMP(1, 3);
     return;
   }
   const int s = (bid - long_blocks) * NG + grp;
@@ -301,22 +392,28 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
   const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
   const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
   const int n_iseg = bv.meta[2];
-  if (s >= n_iseg || r1.w) return;  // past the batch's items, or a workgroup-served hot item
+  SSTAMP(1, 1);
+  SROLE(1, 2);
+  // record {item, beg | len << 15 | long << 30, refs 0..11 as 16-bit halves} (segment.hip)
+  if (s >= n_iseg || (r0.y >> 30)) return;  // past the batch's items, or a workgroup-served hot item
   const int32_t item = r0.x;
-  const int beg = r0.y, end = r0.z, len = end - beg;
+  const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
   ItemRow<G4, S, SH> row;
   row.load(Q, item, ld, sub);
   float4 g[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (len <= 4) {  // the common case: every ref inline, all rows requested before accumulating
-    float4 rows[4][S];
-    const int32_t rf[4] = {r0.w, r1.x, r1.y, r1.z};
+  if (len <= kInlineRefs) {  // the common case: every ref inline, all rows requested at once
+    const int32_t pk[6] = {r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    float4 rows[kInlineRefs][S];
+    int32_t rf[kInlineRefs];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < kInlineRefs; ++m) {
+      rf[m] = (pk[m >> 1] >> (16 * (m & 1))) & 0xFFFF;
       if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+    }
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < kInlineRefs; ++m)
       if (m < len) acc_ref<S>(g, rows[m], rf[m]);
   } else {  // lanes fetch G4 refs at once; rows requested 8 at a time before accumulating
     const int lane0 = (threadIdx.x & 63) - sub;
@@ -337,7 +434,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
       }
     }
   }
-  finish_item<G4, S, SH>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
+  SSTAMP(1, 2);
+  finish_item<G4, S, SH, WT>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
+  SSTAMP(1, 3);
 }
 
 // Expand BODY for every instantiated float4 geometry (G4_, S_).
@@ -356,47 +455,86 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     default: return hipErrorInvalidValue;                          \
   }
 
+// BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread
+// item-step workgroups (A/B of the two choices; read at launch / capture time)
+static bool use_wt() {
+  const char* e = getenv("BPRMF_WT");
+  return !(e && e[0] == '0');
+}
+
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw,
                      int64_t bstride) {
+  const bool wt = use_wt();
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
-    if (item_rows)
-      k_user_step<G4_, S_, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                           contrib, ugrad, item_rows, pw,
-                                                           bstride, B);
+    if (item_rows && wt)
+      k_user_step<G4_, S_, true, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
+                                                                 contrib, ugrad, item_rows, pw, bstride, B);
+    else if (item_rows)
+      k_user_step<G4_, S_, true, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
+                                                                  contrib, ugrad, item_rows, pw, bstride, B);
+    else if (wt)
+      k_user_step<G4_, S_, false, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
+                                                                  contrib, ugrad, nullptr, pw, bstride, B);
     else
-      k_user_step<G4_, S_, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                            contrib, ugrad, nullptr, pw,
-                                                            bstride, B);
+      k_user_step<G4_, S_, false, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
+                                                                   contrib, ugrad, nullptr, pw, bstride, B);
   }));
   return hipGetLastError();
 }
 
+int k1_triplets_per_block(const Geom& g) { return kBlock / g.G4; }
+
 int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg + 1)); }
 
+template <int G4, int S, int KB>
+static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, Table Q,
+                                   const Hyper& hp, const int32_t* tbase, int step,
+                                   const float* contrib, const float* ugrad, float* grads,
+                                   hipStream_t s, const float* xloss, double* loss,
+                                   int64_t bstride, bool wt) {
+  constexpr int NG = KB / G4;
+  const int long_blocks = item_long_blocks(B);
+  const int item_blocks = (int)((2LL * B + NG - 1) / NG);
+  // segments K2 finishes span K1 workgroups: at most one per workgroup boundary, and B/2
+  const int tpb = kBlock / G4;
+  const int k2_users = (int)std::min<int64_t>(B / 2, (B + tpb - 1) / tpb);
+  const int user_blocks = (k2_users + NG - 1) / NG;
+  const int lb = loss ? (B + KB - 1) / KB : 0;  // <= kSegLossSlots
+  const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks + lb);
+#define BPRMF_K2(SH_, WT_)                                                                     \
+  k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib, \
+                                                        ugrad, long_blocks, item_blocks, grads,  \
+                                                        xloss, loss, bstride, B)
+  if (grads && wt) BPRMF_K2(true, true);
+  else if (grads) BPRMF_K2(true, false);
+  else if (wt) BPRMF_K2(false, true);
+  else BPRMF_K2(false, false);
+#undef BPRMF_K2
+  return hipGetLastError();
+}
+
+// K2 workgroups of 256 threads: a step's K2 dispatches ~1,300 of them in well under a microsecond,
+// where 1024-thread workgroups (round 1) took ~2.4 us to be dispatched (per-workgroup stamps,
+// tools/ubench_step_stamps.py); a hot item then has 8 lane groups (d <= 128), each keeping 8
+// contribution rows in flight.
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss, double* loss,
                      int64_t bstride) {
-  const int long_blocks = item_long_blocks(B);
   if (!xloss) loss = nullptr;
+  const bool wt = use_wt();
+  const char* kb = getenv("BPRMF_K2_BLOCK");
+  const bool big = kb && atoi(kb) == 1024;
   BPRMF_DISPATCH4(g, ({
-    constexpr int KB = S_ == 1 ? 1024 : 512;
-    constexpr int NG = KB / G4_;
-    const int item_blocks = (int)((2LL * B + NG - 1) / NG);
-    const int user_blocks = (int)((B / 2 + NG - 1) / NG);  // multi-triplet users <= B/2
-    const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks + (loss ? 1 : 0));
-    if (grads)
-      k_item_step<G4_, S_, true, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib,
-                                                           ugrad, long_blocks, item_blocks, grads,
-                                                           xloss, loss, bstride, B);
-    else
-      k_item_step<G4_, S_, false, KB><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step,
-                                                            contrib, ugrad, long_blocks,
-                                                            item_blocks, nullptr, xloss, loss,
-                                                            bstride, B);
+    if (big)
+      return launch_item_step<G4_, S_, (S_ == 1 ? 1024 : 512)>(g, bv, B, P, Q, hp, tbase, step,
+                                                               contrib, ugrad, grads, s, xloss,
+                                                               loss, bstride, wt);
+    return launch_item_step<G4_, S_, 256>(g, bv, B, P, Q, hp, tbase, step, contrib, ugrad, grads,
+                                          s, xloss, loss, bstride, wt);
   }));
   return hipGetLastError();
 }

@@ -1,0 +1,90 @@
+"""Per-workgroup phase timing of the two step kernels from a diagnostic build with
+s_memrealtime stamps (-DBPRMF_STEP_STAMPS): ml-20m shape, d = 128, B = 4096, the last step of a
+64-step chunk.  Stamps: entry, record loaded, rows loaded / contributions summed, stores drained
+(thread 0 of each workgroup waits for its own memory operations before each stamp).
+
+  python tools/ubench_step_stamps.py build    # here: compile tools/libbprmf_step_stamps.so
+  python tools/ubench_step_stamps.py          # GPU box
+"""
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIB = os.path.join(ROOT, "tools", "libbprmf_step_stamps.so")
+
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    b = importlib.import_module("recommend-lib_amd.build")
+    print(b.build(force=True, defines=("BPRMF_STEP_STAMPS",), out=LIB))
+    sys.exit(0)
+
+os.environ["BPRMF_DIAG_LIB"] = LIB
+import ctypes  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+rl = importlib.import_module("recommend-lib_amd")
+syn = importlib.import_module("recommend-lib_amd.synthetic")
+L = rl._lib.load()
+L.bprmf_debug_step_stamps.argtypes = [ctypes.c_void_p]
+U, I, d, B = 138493, 26744, 128, 4096
+pos = syn.make_positives(U, I, 10_000_000, 20261015)
+m = rl.BPRMF(U, I, d, batch_size=B, seed=1, device=0)
+m.set_train(pos)
+m.train_steps(0, 0, 256)
+out = {}
+samples = []
+for rep in range(8):
+    m.train_steps(0, 256 + 64 * rep, 64)
+    st = np.zeros((2, 8192, 6), np.uint64)
+    assert L.bprmf_debug_step_stamps(st.ctypes.data) == 0
+    samples.append(st.astype(np.int64))
+roles = {0: "loss", 1: "long item", 2: "item", 3: "multi user"}
+
+
+def summarize(st, k1_blocks, k2_blocks):
+    res = {}
+    k1 = st[0, :k1_blocks]
+    k2 = st[1, :k2_blocks]
+    t0 = k1[:, 0].min()
+    us = lambda x: round(float(x) * 0.01, 2)  # 100 MHz ticks -> us
+    res["K1 first start -> last start"] = us(k1[:, 0].max() - t0)
+    res["K1 record (median, max)"] = [us(np.median(k1[:, 1] - k1[:, 0])), us((k1[:, 1] - k1[:, 0]).max())]
+    res["K1 rows (median, max)"] = [us(np.median(k1[:, 2] - k1[:, 1])), us((k1[:, 2] - k1[:, 1]).max())]
+    res["K1 stores (median, max)"] = [us(np.median(k1[:, 3] - k1[:, 2])), us((k1[:, 3] - k1[:, 2]).max())]
+    res["K1 last end"] = us(k1[:, 3].max() - t0)
+    res["K2 first start"] = us(k2[:, 0].min() - t0)
+    res["K2 last start"] = us(k2[:, 0].max() - t0)
+    for r, name in roles.items():
+        sel = k2[:, 5] == r
+        if r == 0:
+            sel = np.zeros(len(k2), bool)
+            sel[0] = True
+        if not sel.any():
+            continue
+        x = k2[sel]
+        live = x[:, 3] >= x[:, 0]
+        if not live.any():
+            continue
+        x = x[live]
+        res[f"K2 {name}: n"] = int(live.sum())
+        res[f"K2 {name}: record (median, max)"] = [us(np.median(x[:, 1] - x[:, 0])), us((x[:, 1] - x[:, 0]).max())]
+        res[f"K2 {name}: sums (median, max)"] = [us(np.median(x[:, 2] - x[:, 1])), us((x[:, 2] - x[:, 1]).max())]
+        res[f"K2 {name}: stores (median, max)"] = [us(np.median(x[:, 3] - x[:, 2])), us((x[:, 3] - x[:, 2]).max())]
+        res[f"K2 {name}: last end"] = us(x[:, 3].max() - t0)
+    return res
+
+
+k1_blocks = B // (256 // 32)
+KB = int(os.environ.get("BPRMF_K2_BLOCK", "256"))
+NG = KB // 32
+k2_blocks = 1 + 64 + (2 * B) // NG + (B // 2) // NG
+for n, st in enumerate(samples[2:]):
+    # the last step's stamps: clear stale rows (their stamps are older than this K1's start)
+    st = st.copy()
+    t0 = st[0, :k1_blocks, 0].min()
+    st[1, :k2_blocks][st[1, :k2_blocks, 0] < t0] = 0
+    out[f"rep{n}"] = summarize(st, k1_blocks, k2_blocks)
+print(json.dumps(out, indent=1))

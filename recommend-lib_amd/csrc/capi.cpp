@@ -472,7 +472,7 @@ static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
   return 0;
 }
 
-static int capture_step_graph(bprmf_handle* h, int64_t n, StepGraph* out) {
+static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGraph* out) {
   const int B = h->cfg.batch_size;
   const BatchBuf bb{h->d_batch, B};
   const BatchView v0 = bb.view(0);
@@ -487,7 +487,7 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, StepGraph* out) {
                     h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss, stride);
     if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph launch: %s", hipGetErrorString(e));
   }
-  if (!rc) {
+  if (!rc && advance) {
     const hipError_t e = advance_cursor(h->d_tbase, (int32_t)n, h->stream);
     if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph cursor: %s", hipGetErrorString(e));
   }
@@ -498,6 +498,7 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, StepGraph* out) {
     return rc ? rc : fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e2));
   }
   out->n = n;
+  out->advance = advance;
   const hipError_t e = hipGraphInstantiate(&out->exec, graph, nullptr, nullptr, 0);
   hipGraphDestroy(graph);
   if (e != hipSuccess) {
@@ -511,9 +512,9 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, StepGraph* out) {
 static int ensure_step_graphs(bprmf_handle* h) {
   if ((int)h->graphs.size() == kGraphKinds) return 0;
   drop_graphs(h);
-  for (int g = 0; g < kGraphKinds; ++g) {
+  for (int g = 0; g < kGraphKinds; ++g) {  // graphs[2 * size + advance]
     StepGraph sg;
-    if (int r = capture_step_graph(h, kGraphSizes[g], &sg)) {
+    if (int r = capture_step_graph(h, kGraphSizes[g / 2], g & 1, &sg)) {
       drop_graphs(h);
       return r;
     }
@@ -522,11 +523,33 @@ static int ensure_step_graphs(bprmf_handle* h) {
   return 0;
 }
 
-// the cursor holds {h->t, 0}: nb steps as replays of the largest graphs that fit
+// The cursor holds {h->t, 0}.  nb steps = whole 64-step graphs, whole 16-step graphs, then the
+// last < 16 steps launched eagerly (a graph replay costs a cursor launch and a graph-to-graph gap
+// of ~13 us on the GPU, more than the host takes to launch a few steps while the GPU is busy).
+// Every graph but the last advances the cursor; the eager steps index their batch absolutely and
+// their optimizer step relative to the cursor.
 static int launch_step_graph(bprmf_handle* h, int64_t nb) {
   if (int r = ensure_step_graphs(h)) return r;
-  for (int g = 0; g < kGraphKinds; ++g)
-    for (; nb >= h->graphs[g].n; nb -= h->graphs[g].n) HIPCHK(hipGraphLaunch(h->graphs[g].exec, h->stream));
+  const int64_t n64 = nb / kGraphSizes[0], n16 = (nb % kGraphSizes[0]) / kGraphSizes[1];
+  const int64_t ng = n64 + n16;
+  int64_t base = 0, done = 0;  // steps under the advanced cursor / steps launched
+  for (int64_t q = 0; q < ng; ++q) {
+    const int size = q < n64 ? 0 : 1;
+    const bool adv = q + 1 < ng;
+    const StepGraph& g = h->graphs[2 * size + (adv ? 1 : 0)];
+    HIPCHK(hipGraphLaunch(g.exec, h->stream));
+    done += g.n;
+    if (adv) base += g.n;
+  }
+  const int B = h->cfg.batch_size;
+  const BatchBuf bb{h->d_batch, B};
+  for (int64_t k = done; k < nb; ++k) {
+    const BatchView v = bb.view(k);
+    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)(k - base), h->d_xloss,
+                     h->d_contrib, h->d_ugrad, nullptr, h->stream));
+    HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)(k - base), h->d_contrib,
+                     h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss));
+  }
   return 0;
 }
 
@@ -556,7 +579,9 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   }
   if (int r = ensure_seg(h, nb)) return r;
   BatchBuf bb{h->d_batch, (int)B};
-  {  // the batches first: the GPU starts on them while the host enqueues the rest
+  // the cursor (and the call's loss slots) first: cheap, and off the path between build and steps
+  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
+  {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     if (!ru && split_build(nb)) {
       if (int r = ensure_trip(h, n)) return r;
@@ -571,7 +596,6 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
                            h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     }
   }
-  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
   if (h->use_graphs) {
     // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
     // the step kernels and their gaps; per-kernel splits come from rocprofv3)

@@ -21,12 +21,15 @@ int fail(int code, const char* fmt, ...);
   } while (0)
 
 // position-independent step graphs (launch_step_graph): a graph of n steps runs the batches and
-// optimizer steps the device cursor d_tbase = {t, k} names, then advances it by n; any chunk is
-// a sum of these sizes, so no chunk length or offset ever triggers a capture after the first
-constexpr int64_t kGraphSizes[] = {64, 16, 4, 1};
-constexpr int kGraphKinds = 4;
+// optimizer steps the device cursor d_tbase = {t, k} names, then (advancing variant) advances it
+// by n; a chunk is whole 64- and 16-step graphs plus fewer than 16 eagerly launched steps, so no
+// chunk length or offset ever triggers a capture after the first
+constexpr int64_t kGraphSizes[] = {64, 16};
+constexpr int kGraphSizeKinds = 2;
+constexpr int kGraphKinds = 2 * kGraphSizeKinds;  // each size with and without the advance
 struct StepGraph {
-  int64_t n = 0;  // steps per replay
+  int64_t n = 0;         // steps per replay
+  bool advance = false;  // ends by advancing the cursor (a later graph of the chunk follows)
   hipGraphExec_t exec = nullptr;
 };
 constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th step

@@ -398,6 +398,9 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
   if (s >= n_iseg || (r0.y >> 30)) return;  // past the batch's items, or a workgroup-served hot item
   const int32_t item = r0.x;
   const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
+#ifdef BPRMF_STEP_STAMPS
+  if (threadIdx.x == 0) g_step_stamps[1][blockIdx.x][4] = (uint64_t)len;
+#endif
   ItemRow<G4, S, SH> row;
   row.load(Q, item, ld, sub);
   float4 g[S];

@@ -66,6 +66,8 @@ static __device__ __forceinline__ uint32_t bounded(uint64_t q, uint32_t epoch, u
 }
 
 // j = the k-th item id NOT in the sorted positive list a[0..n): m = #{x : a[x]-x <= k}, j = k+m.
+// (A 9-ary search with 8 pivot loads per round measured no faster on the short-chunk sampler and
+// slower on long chunks: the sampler's time is its Philox work, not this chain.)
 static __device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restrict__ a, int64_t n, int64_t k) {
   int64_t lo = 0, hi = n;
   while (lo < hi) {

@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include "device_common.h"
 

@@ -186,6 +186,22 @@ def test_sampler_bit_exact_ml100k(rl, golden):
         assert np.array_equal(x, y)
 
 
+def test_sampler_deep_lists_bit_exact(rl):
+    """Users with thousands of positives (several rounds of the 9-ary search for the k-th
+    non-positive) draw exactly the oracle's triplets."""
+    syn = __import__("importlib").import_module("recommend-lib_amd.synthetic")
+    U, I = 20000, 5000
+    pos = syn.make_positives(U, I, 2_000_000, seed=5)
+    m = _model(rl, U, I, 8, 4096, seed=321)
+    m.set_train(pos)
+    got = m.sample(2, 12345, 300_000)
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    assert int(np.diff(indptr).max()) >= 500  # several rounds of the 9-ary search
+    want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 321, 2, 12345, 300_000)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)
+
+
 def test_sampler_bit_exact_sharded(rl, golden):
     pos, U, I = _ml100k_pos(golden)
     world, seed = 3, 77

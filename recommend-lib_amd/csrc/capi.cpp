@@ -140,6 +140,11 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   }
   h->stream = h->own_stream;
   h->use_graphs = getenv("BPRMF_NO_GRAPH") == nullptr;
+  {  // the fused step needs the write-through row stores (its hand-off protocol)
+    const char* f = getenv("BPRMF_FUSED");
+    const char* w = getenv("BPRMF_WT");
+    h->fused = !(f && f[0] == '0') && !(w && w[0] == '0');
+  }
   const int64_t ld = g.ld;
   TRY(dalloc(&h->P.W, h->U * ld));
   TRY(dalloc(&h->P.stamp, h->U));
@@ -186,7 +191,8 @@ int bprmf_destroy(bprmf_handle* h) {
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
-                  h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase};
+                  h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
+                  h->d_pend_q, h->d_pend_p};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -381,6 +387,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
+    if (e & 8) return fail(BPRMF_E_HIP, "fused step: a row's owner never published it (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
     return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
   }
@@ -412,9 +419,14 @@ bool bprmf::seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSe
 int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   const int64_t B = h->cfg.batch_size;
   if (!h->d_contrib) {
-    if (int r = dalloc(&h->d_contrib, B * h->geom.ld)) return r;
-    if (int r = dalloc(&h->d_ugrad, B * h->geom.ld)) return r;
-    if (int r = dalloc(&h->d_xloss, B)) return r;
+    if (int r = dalloc(&h->d_contrib, 2 * B * h->geom.ld)) return r;
+    if (int r = dalloc(&h->d_ugrad, 2 * B * h->geom.ld)) return r;
+    if (int r = dalloc(&h->d_xloss, 2 * B)) return r;
+    if (int r = dalloc(&h->d_pend_q, 2 * h->I)) return r;
+    if (int r = dalloc(&h->d_pend_p, 2 * h->U)) return r;
+    // no step has marked a row yet (steps are >= 1; -1 never matches)
+    if (h->I) HIPCHK(hipMemsetAsync(h->d_pend_q, 0xFF, sizeof(int32_t) * 2 * h->I, h->stream));
+    if (h->U) HIPCHK(hipMemsetAsync(h->d_pend_p, 0xFF, sizeof(int32_t) * 2 * h->U, h->stream));
     if (int r = dalloc(&h->d_tbase, 4)) return r;
   }
   if (n_batches <= h->batch_cap) return 0;
@@ -448,45 +460,59 @@ extern "C" {
 static int run_steps(bprmf_handle* h, const int32_t* tu, const int32_t* ti, const int32_t* tj,
                      int64_t n, int64_t* steps_done);
 
-// The step launches of a chunk.  Graph path: position-independent graphs of kGraphSizes steps,
-// each captured once per batch buffer (kernels take batch 0's view plus the batch stride and read
-// the batch and the step from the cursor d_tbase, which each replay's last node advances), so a
-// chunk of any length at any offset replays at most a few of them and never captures again.
+}  // extern "C"
+
+StepBufs bprmf::step_bufs(const bprmf_handle* h) {
+  StepBufs b;
+  b.contrib = h->d_contrib;
+  b.ugrad = h->d_ugrad;
+  b.xloss = h->d_xloss;
+  b.pstride = (int64_t)h->cfg.batch_size * h->geom.ld;
+  b.pend_q = h->d_pend_q;
+  b.pend_p = h->d_pend_p;
+  b.qrows = h->I;
+  b.prows = h->U;
+  return b;
+}
+
+extern "C" {
+
+// The step launches of a chunk of nb steps, all indexed by the device cursor d_tbase = {t, k}
+// (kernels take batch 0's view plus the batch stride, and a step index relative to the cursor).
+// A "unit" is one launch group at relative index r:
+//   fused (default):  K2 of step r and K1 of step r + 1 in one launch (k_fused_step); the chunk
+//                     is K1(0), units 0 .. nb-2, K2(nb-1): nb + 1 launches;
+//   unfused:          K1(r) then K2(r): 2 nb launches.
+// Units run as replays of position-independent graphs of 64 and 16 units (captured once per
+// batch buffer; every graph but the chunk's last ends by advancing the cursor) plus fewer than 16
+// eager units; the eager launches and the epilogue index the cursor as the graphs left it.
 static void drop_graphs(bprmf_handle* h) {
   for (auto& ge : h->graphs)
     if (ge.exec) hipGraphExecDestroy(ge.exec);
   h->graphs.clear();
 }
 
-// eager launches of steps [k0, k1) of the chunk (bv of each batch, cursor {t, 0})
-static int step_launches(bprmf_handle* h, int64_t k0, int64_t k1) {
+static int launch_unit(bprmf_handle* h, int64_t r) {
   const int B = h->cfg.batch_size;
-  const BatchBuf bb{h->d_batch, B};
-  for (int64_t k = k0; k < k1; ++k) {
-    const BatchView v = bb.view(k);
-    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss, h->d_contrib,
-                     h->d_ugrad, nullptr, h->stream));
-    HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->d_ugrad,
-                     nullptr, h->stream, h->d_xloss, h->d_loss));
+  const BatchView v0 = BatchBuf{h->d_batch, B}.view(0);
+  const int64_t stride = BatchBuf::stride_for(B);
+  const StepBufs sb = step_bufs(h);
+  if (h->fused) {
+    HIPCHK(fused_step(h->geom, v0, stride, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, sb, h->d_loss,
+                      h->d_err, h->stream));
+    return 0;
   }
+  HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, nullptr, nullptr, nullptr,
+                   nullptr, h->stream, PeerWait{}, stride, &sb));
+  HIPCHK(item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, nullptr, nullptr, nullptr,
+                   h->stream, nullptr, h->d_loss, stride, &sb));
   return 0;
 }
 
 static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGraph* out) {
-  const int B = h->cfg.batch_size;
-  const BatchBuf bb{h->d_batch, B};
-  const BatchView v0 = bb.view(0);
-  const int64_t stride = BatchBuf::stride_for(B);
   HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   int rc = 0;
-  for (int64_t r = 0; r < n && !rc; ++r) {
-    hipError_t e = user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, h->d_xloss,
-                             h->d_contrib, h->d_ugrad, nullptr, h->stream, PeerWait{}, stride);
-    if (e == hipSuccess)
-      e = item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)r, h->d_contrib,
-                    h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss, stride);
-    if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph launch: %s", hipGetErrorString(e));
-  }
+  for (int64_t r = 0; r < n && !rc; ++r) rc = launch_unit(h, r);
   if (!rc && advance) {
     const hipError_t e = advance_cursor(h->d_tbase, (int32_t)n, h->stream);
     if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "step graph cursor: %s", hipGetErrorString(e));
@@ -508,7 +534,7 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
   return 0;
 }
 
-// capture every graph size once (batch buffer and contrib buffers must exist: ensure_seg)
+// capture every graph once (batch buffer and step buffers must exist: ensure_seg)
 static int ensure_step_graphs(bprmf_handle* h) {
   if ((int)h->graphs.size() == kGraphKinds) return 0;
   drop_graphs(h);
@@ -523,36 +549,45 @@ static int ensure_step_graphs(bprmf_handle* h) {
   return 0;
 }
 
-// The cursor holds {h->t, 0}.  nb steps = whole 64-step graphs, whole 16-step graphs, then the
-// last < 16 steps launched eagerly (a graph replay costs a cursor launch and a graph-to-graph gap
-// of ~13 us on the GPU, more than the host takes to launch a few steps while the GPU is busy).
-// Every graph but the last advances the cursor; the eager steps index their batch absolutely and
-// their optimizer step relative to the cursor.
-static int launch_step_graph(bprmf_handle* h, int64_t nb) {
-  if (int r = ensure_step_graphs(h)) return r;
-  const int64_t n64 = nb / kGraphSizes[0], n16 = (nb % kGraphSizes[0]) / kGraphSizes[1];
-  const int64_t ng = n64 + n16;
-  int64_t base = 0, done = 0;  // steps under the advanced cursor / steps launched
-  for (int64_t q = 0; q < ng; ++q) {
-    const int size = q < n64 ? 0 : 1;
-    const bool adv = q + 1 < ng;
-    const StepGraph& g = h->graphs[2 * size + (adv ? 1 : 0)];
-    HIPCHK(hipGraphLaunch(g.exec, h->stream));
-    done += g.n;
-    if (adv) base += g.n;
+// n units from the cursor: whole 64- and 16-unit graphs, then the rest eagerly (a graph replay
+// costs a cursor launch and a graph-to-graph gap of ~13 us on the GPU, more than the host takes
+// to launch a few units while the GPU is busy).  Returns the cursor's advance (*base).
+static int run_units(bprmf_handle* h, int64_t n, int64_t* base) {
+  *base = 0;
+  int64_t done = 0;
+  if (h->use_graphs) {
+    if (int r = ensure_step_graphs(h)) return r;
+    const int64_t n64 = n / kGraphSizes[0], n16 = (n % kGraphSizes[0]) / kGraphSizes[1];
+    const int64_t ng = n64 + n16;
+    for (int64_t q = 0; q < ng; ++q) {
+      const int size = q < n64 ? 0 : 1;
+      const bool adv = q + 1 < ng;
+      const StepGraph& g = h->graphs[2 * size + (adv ? 1 : 0)];
+      HIPCHK(hipGraphLaunch(g.exec, h->stream));
+      done += g.n;
+      if (adv) *base += g.n;
+    }
   }
-  const int B = h->cfg.batch_size;
-  const BatchBuf bb{h->d_batch, B};
-  for (int64_t k = done; k < nb; ++k) {
-    const BatchView v = bb.view(k);
-    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)(k - base), h->d_xloss,
-                     h->d_contrib, h->d_ugrad, nullptr, h->stream));
-    HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)(k - base), h->d_contrib,
-                     h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss));
-  }
+  for (int64_t k = done; k < n; ++k)
+    if (int r = launch_unit(h, k - *base)) return r;
   return 0;
 }
 
+// the chunk's nb steps (cursor {h->t, 0}, batches built)
+static int launch_steps(bprmf_handle* h, int64_t nb) {
+  int64_t base = 0;
+  if (!h->fused) return run_units(h, nb, &base);
+  const int B = h->cfg.batch_size;
+  const BatchView v0 = BatchBuf{h->d_batch, B}.view(0);
+  const int64_t stride = BatchBuf::stride_for(B);
+  const StepBufs sb = step_bufs(h);
+  HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, 0, nullptr, nullptr, nullptr,
+                   nullptr, h->stream, PeerWait{}, stride, &sb));
+  if (int r = run_units(h, nb - 1, &base)) return r;
+  HIPCHK(item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)(nb - 1 - base), nullptr,
+                   nullptr, nullptr, h->stream, nullptr, h->d_loss, stride, &sb));
+  return 0;
+}
 
 // One chunk of whole steps: slots [first_slot, first_slot + n) of `epoch` from the device sampler
 // (ru == nullptr) or replayed device ids ru/ri/rj[0..n).  Segmented path for B <= kMaxSegBatch:
@@ -596,35 +631,18 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
                            h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
     }
   }
-  if (h->use_graphs) {
-    // profiling: one event pair around each replay of whole steps (GPU-bound, so the pair brackets
+  {
+    // profiling: one event pair around the chunk's step launches (GPU-bound, so the pair brackets
     // the step kernels and their gaps; per-kernel splits come from rocprofv3)
     hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
     if (ea) HIPCHK(hipEventRecord(ea, h->stream));
-    if (int r = launch_step_graph(h, nb)) return r;
+    if (int r = launch_steps(h, nb)) return r;
     if (ea) {
       hipEvent_t eb = prof_event(h);
       if (eb) {
         HIPCHK(hipEventRecord(eb, h->stream));
         h->prof_rec[BPRMF_KPROF_STEPS].push_back({ea, eb});
         h->prof_weight[BPRMF_KPROF_STEPS] += nb - 1;  // one pair covers nb steps
-      }
-    }
-  } else {
-    // eager; while profiling, an event pair brackets the kernels of every kProfStride-th step only,
-    // so the host stays ahead of the GPU and the events time the kernels, not launch latency
-    for (int64_t k = 0; k < nb; ++k) {
-      const BatchView v = bb.view(k);
-      const bool sampled = ((h->t + k) % kProfStride) == 0;
-      {
-        ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
-        HIPCHK(user_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss,
-                         h->d_contrib, h->d_ugrad, nullptr, h->stream));
-      }
-      {
-        ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
-        HIPCHK(item_step(h->geom, v, (int)B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
-                         h->d_ugrad, nullptr, h->stream, h->d_xloss, h->d_loss));
       }
     }
   }

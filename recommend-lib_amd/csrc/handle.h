@@ -58,9 +58,12 @@ struct bprmf_handle {
   // segmented step (batch_size <= kMaxSegBatch): per-batch sorted layouts + per-triplet c*P_u
   int32_t* d_batch = nullptr;  // batch_cap * BatchBuf::stride_for(B) int32
   int64_t batch_cap = 0;
-  float* d_contrib = nullptr;  // [B, ld] c*P_u per triplet (K1 -> K2)
-  float* d_ugrad = nullptr;    // [B, ld] user gradient per triplet of multi-triplet users
-  float* d_xloss = nullptr;    // [B] x per triplet (K1 -> K2's loss workgroup)
+  float* d_contrib = nullptr;  // [2][B, ld] c*P_u per triplet (K1 -> K2), halves by step parity
+  float* d_ugrad = nullptr;    // [2][B, ld] user gradient per triplet of multi-triplet users
+  float* d_xloss = nullptr;    // [2][B] x per triplet (K1 -> K2's loss workgroups)
+  int32_t* d_pend_q = nullptr;  // [2][I] step that last marked an item row (fused step)
+  int32_t* d_pend_p = nullptr;  // [2][U] the same for user rows K2 finishes
+  bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;
@@ -120,6 +123,7 @@ struct ProfScope {
 };
 int ensure_trip(bprmf_handle* h, int64_t n);
 int ensure_seg(bprmf_handle* h, int64_t n_batches);
+StepBufs step_bufs(const bprmf_handle* h);  // the single-GPU step buffers (both halves, pend)
 int ensure_grad(bprmf_handle* h);
 bool seg_mode(const bprmf_handle* h);
 // a sampled chunk of nb batches draws its triplets with the grid-wide sampler before the builder

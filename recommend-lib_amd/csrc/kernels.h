@@ -132,6 +132,20 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb);
 // triplets per K1 workgroup for a geometry (the builder marks user segments that lie in one)
 int k1_triplets_per_block(const Geom& g);
+// Per-step buffers of the step kernels.  pstride != 0 (single GPU): contrib / ugrad / xloss hold
+// two halves, step t uses half t & 1 (contrib, ugrad: pstride floats each; xloss: B floats), so
+// K1 of step t+1 can write while K2 of step t still reads (the fused step).  pend_q [2][qrows],
+// pend_p [2][prows] (single GPU, fused step): K1 of step t marks half t & 1 of the rows step t
+// updates with t.
+struct StepBufs {
+  float* contrib = nullptr;
+  float* ugrad = nullptr;
+  float* xloss = nullptr;
+  int64_t pstride = 0;
+  int32_t* pend_q = nullptr;
+  int32_t* pend_p = nullptr;
+  int64_t qrows = 0, prows = 0;
+};
 // sharded K1 over the IPC transport: wait for the peers' row flags first (flags == null: none)
 struct PeerWait {
   const int32_t* flags = nullptr;
@@ -146,7 +160,7 @@ struct PeerWait {
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw = PeerWait{},
-                     int64_t bstride = 0);
+                     int64_t bstride = 0, const StepBufs* sb = nullptr);
 // K2: item segments (fixed-order sums of contrib) and multi-triplet user segments (of ugrad).
 // grads != null: sharded K2 (per-slot item gradients [slots, ld] instead of applying the items).
 // loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
@@ -155,7 +169,13 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss = nullptr,
-                     double* loss = nullptr, int64_t bstride = 0);
+                     double* loss = nullptr, int64_t bstride = 0, const StepBufs* sb = nullptr);
+// (sb != null: its buffers replace contrib / ugrad / xloss)
+// K2 of step t = tbase[0] + step + 1 on batch tbase[1] + step, and K1 of step t + 1 on the next
+// batch, in one launch (bv0: batch 0's view; single GPU, sb with both halves and pend arrays)
+hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
+                      const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
+                      double* loss, int32_t* err, hipStream_t s);
 int item_long_blocks(int B);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,

@@ -92,26 +92,73 @@ static __device__ __forceinline__ float4 sgd4(float4 v, float4 g, float lr, floa
                      fmaf(-lr, fmaf(wd, v.z, g.z), v.z), fmaf(-lr, fmaf(wd, v.w, g.w), v.w));
 }
 
-// K1, one lane group per triplet p (sorted by user).  SH (sharded): i/j are slots of item_rows,
-// the rows the owners sent for this step, already brought to step t-1 by the owner (no stamps).
-template <int G4, int S, bool SH, bool WT>
-__global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
-                                                      int ld, const int32_t* __restrict__ tbase,
-                                                      int step, float* __restrict__ xloss,
-                                                      float* __restrict__ contrib,
-                                                      float* __restrict__ ugrad,
-                                                      const float* __restrict__ item_rows,
-                                                      PeerWait pw, int64_t bstride, int B) {
+// One row segment (16 B per lane) read with sc1 loads: past this CU's L1, so a row another XCD
+// just wrote is seen once its stamp is (the fused step's hand-off, MI355X_MICROARCH.md "Valid
+// forms": sc1 payload stores + vmcnt(0) + sc1 flag store; sc1 poll + sc1 payload loads).
+static __device__ __forceinline__ float4 ld4_sc1(const float* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                     __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+}
+
+// Wait (sc1 polls) until a row's stamp reaches step tp, i.e. its owner in the same launch has
+// stored the row and then the stamp.  Bounded: after ~10 s err bit 8 is raised and the wait gives
+// up (the call then fails) instead of hanging the queue.
+static __device__ __forceinline__ void wait_stamp(const int32_t* stamp, int32_t tp, int32_t* err) {
+  if (__hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tp) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t polls = 0;
+    while (__hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tp) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++polls & 255) == 0) {  // a wait that already timed out elsewhere ends this one too
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 100 MHz: 10 s
+          atomicOr(err, 8);
+          break;
+        }
+      }
+    }
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the row loads stay after the poll
+}
+
+// Publish a row's step stamp after the row: every lane's (write-through) row stores acknowledged,
+// then an sc1 stamp store.  A lane group lies within one wave (G4 <= 64), so the wave's own wait
+// covers the whole row.
+template <bool PUB>
+static __device__ __forceinline__ void put_stamp(int32_t* stamp, int32_t t, bool writer) {
+  if constexpr (PUB) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (writer) __hip_atomic_store(stamp, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (writer) *stamp = t;
+  }
+}
+
+// K1 of step t, one lane group per triplet p (sorted by user).  SH (sharded): i/j are slots of
+// item_rows, the rows the owners sent for this step, already brought to step t-1 by the owner (no
+// stamps).  WAIT (fused step, k_fused_step): this K1 runs beside K2 of step t-1, so a row that
+// step t-1 updates (pend[(t-1)&1][row] == t-1, written by K1 of step t-1 in the previous launch)
+// is read only after its owner publishes stamp t-1.  pend (single GPU): every triplet marks its
+// rows with t (users: only those K2 finishes), for K1 of step t+1.
+template <int G4, int S, bool SH, bool WT, bool WAIT>
+static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Table& P, const Table& Q,
+                                               const Hyper& hp, int ld, int32_t t,
+                                               const StepBufs& sb, const float* __restrict__ item_rows,
+                                               int B, int32_t* err) {
   SSTAMP(0, 0);
   const int sub = threadIdx.x & (G4 - 1);
-  const int p = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
-  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
-  if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
-  // independent loads: the record, the triplet count, the step base.  The grid covers B rounded
-  // up to whole blocks: the index is clamped into the batch's B records (never read past them)
+  const int p = blk * (kBlock / G4) + threadIdx.x / G4;
+  // independent loads: the record and the triplet count.  The grid covers B rounded up to whole
+  // blocks: the index is clamped into the batch's B records (never read past them)
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[min(p, B - 1)];
   const int n = bv.meta[0];
-  const int32_t t = *tbase + step + 1;
+  const int64_t par = sb.pstride ? (int64_t)(t & 1) : 0;  // this step's half of the buffers
+  float* contrib = sb.contrib + par * sb.pstride;
+  float* ugrad = sb.ugrad + par * sb.pstride;
+  float* xloss = sb.xloss ? sb.xloss + par * B : nullptr;
   SSTAMP(0, 1);
   // kept past the workgroup barrier for an in-workgroup segment head (w >= 2)
   float4 pu[S];
@@ -124,19 +171,37 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
     u = r.z;
     w = r.w;
     prow = P.W + (int64_t)u * ld + 4 * sub;
+    if (sb.pend_q && sub == 0) {  // this step's rows, for the next step's fused K1
+      const int64_t o = (int64_t)(t & 1);
+      sb.pend_q[o * sb.qrows + i] = t;
+      sb.pend_q[o * sb.qrows + j] = t;
+      if (w == 0) sb.pend_p[o * sb.prows + u] = t;
+    }
+    bool wi = false, wj = false, wu = false;
+    const int32_t tp = t - 1;
+    if (WAIT) {
+      const int64_t o = (int64_t)(tp & 1);
+      wi = sb.pend_q[o * sb.qrows + i] == tp;
+      wj = sb.pend_q[o * sb.qrows + j] == tp;
+      wu = sb.pend_p[o * sb.prows + u] == tp;
+      if (wi) wait_stamp(Q.stamp + i, tp, err);
+      if (wj) wait_stamp(Q.stamp + j, tp, err);
+      if (wu) wait_stamp(P.stamp + u, tp, err);
+    }
     const float* qbase = SH ? item_rows : Q.W;
     const float* qi = qbase + (int64_t)i * ld + 4 * sub;
     const float* qj = qbase + (int64_t)j * ld + 4 * sub;
     float4 vi[S], vj[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      pu[k] = ld4(prow + 4 * G4 * k);
-      vi[k] = ld4(qi + 4 * G4 * k);
-      vj[k] = ld4(qj + 4 * G4 * k);
+      pu[k] = wu ? ld4_sc1(prow + 4 * G4 * k) : ld4(prow + 4 * G4 * k);
+      vi[k] = wi ? ld4_sc1(qi + 4 * G4 * k) : ld4(qi + 4 * G4 * k);
+      vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4(qj + 4 * G4 * k);
     }
-    const int32_t su = P.stamp[u];
-    const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[i]);
-    const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - Q.stamp[j]);
+    // a row just published is current at tp (no pending decay); the others read their stamps
+    const int32_t su = wu ? tp : P.stamp[u];
+    const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wi ? tp : Q.stamp[i]));
+    const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wj ? tp : Q.stamp[j]));
     const float fu = decay_pow(hp.log2a, t - 1 - su);
     float di = 0.f, dj = 0.f;
 #pragma unroll
@@ -190,6 +255,18 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
   SSTAMP(0, 3);
 }
 
+template <int G4, int S, bool SH, bool WT>
+__global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Table Q, Hyper hp,
+                                                      int ld, const int32_t* __restrict__ tbase,
+                                                      int step, StepBufs sb,
+                                                      const float* __restrict__ item_rows,
+                                                      PeerWait pw, int64_t bstride, int B) {
+  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
+  if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
+  k1_body<G4, S, SH, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, item_rows, B,
+                                nullptr);
+}
+
 // an item row and its stamp, loaded as soon as the segment's record is known so the loads run
 // alongside the contribution gathers instead of after them (single GPU only; sharded K2 emits the
 // gradient and reads no item row)
@@ -223,7 +300,7 @@ static __device__ __forceinline__ void acc_ref(float4 (&g)[S], const float4 (&ro
 
 // finish one item segment: apply W = V - lr (g + wd V) to the preloaded row (single GPU) or hand
 // the gradient to the exchange (sharded)
-template <int G4, int S, bool SH, bool WT>
+template <int G4, int S, bool SH, bool WT, bool PUB>
 static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int slot,
                                                    const float4 (&g)[S], const ItemRow<G4, S, SH>& row,
                                                    const Hyper& hp, int ld, int32_t t, int sub,
@@ -237,7 +314,7 @@ static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int sl
     const float f = decay_pow(hp.log2a, t - 1 - row.stamp);
 #pragma unroll
     for (int k = 0; k < S; ++k) st4o<WT>(w + 4 * G4 * k, sgd4(scale4(row.x[k], f), g[k], hp.lr, hp.wd));
-    if (sub == 0) Q.stamp[item] = t;
+    put_stamp<PUB>(Q.stamp + item, t, sub == 0);
   }
 }
 
@@ -267,31 +344,33 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
   }
 }
 
-// KB threads per block: 1024 (512 for rows over 1 KB) so a hot item's workgroup has 16-32 lane
-// groups fetching its references in parallel
-template <int G4, int S, bool SH, int KB, bool WT>
-__global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp, int ld,
-                                                  const int32_t* __restrict__ tbase, int step,
-                                                  const float* __restrict__ contrib,
-                                                  const float* __restrict__ ugrad, int long_blocks,
-                                                  int item_blocks, float* __restrict__ grads,
-                                                  const float* __restrict__ xloss,
-                                                  double* __restrict__ loss, int64_t bstride,
-                                                  int B) {
+// K2 of step t, workgroup `blk` of its grid: loss workgroups, hot items (whole workgroups), item
+// segments (one lane group each), user segments spanning K1 workgroups.  PUB (fused step): every
+// updated row's stamp is published after the row (put_stamp), for K1 of step t+1 in the same
+// launch.
+template <int G4, int S, bool SH, int KB, bool WT, bool PUB>
+static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Table& P, const Table& Q,
+                                               const Hyper& hp, int ld, int32_t t,
+                                               const StepBufs& sb, int long_blocks, int item_blocks,
+                                               float* __restrict__ grads, double* __restrict__ loss,
+                                               int B) {
   constexpr int NG = KB / G4;
   SSTAMP(1, 0);
-  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
-  const int32_t t = *tbase + step + 1;
+  const int64_t par = sb.pstride ? (int64_t)(t & 1) : 0;  // the half K1 of step t wrote
+  const float* __restrict__ contrib = sb.contrib + par * sb.pstride;
+  const float* __restrict__ ugrad = sb.ugrad + par * sb.pstride;
+  const float* __restrict__ xloss = sb.xloss ? sb.xloss + par * B : nullptr;
+  if (!xloss) loss = nullptr;
   // the step's loss: the first loss_blocks(B, KB) workgroups (dispatched first, off the tail) each
   // sum log(1 + e^-x) over KB triplets, one per thread, in a fixed tree, and add it to their own
   // slot loss[b] (one writer per slot per launch; the host adds the slots once per call)
   const int lb = loss ? (B + KB - 1) / KB : 0;
-  if ((int)blockIdx.x < lb) {
+  if (blk < lb) {
     __shared__ double red[KB / 64];
     const int n = bv.meta[0];
-    const int p = blockIdx.x * KB + threadIdx.x;
+    const int p = blk * KB + threadIdx.x;
     double acc = p < n ? (double)softplus(-xloss[p]) : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);  // fixed butterfly
@@ -300,11 +379,11 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     if (threadIdx.x == 0) {
       double tot = 0.0;
       for (int w = 0; w < KB / 64; ++w) tot += red[w];
-      loss[blockIdx.x] += tot;
+      loss[blk] += tot;
     }
     return;
   }
-  const int bid = (int)blockIdx.x - lb;
+  const int bid = blk - lb;
   if (bid >= long_blocks + item_blocks) {  // users with several triplets
     const int m = (bid - long_blocks - item_blocks) * NG + grp;
     // indices clamped into the batch's record arrays (B/2 user records, 2B item records): the
@@ -325,7 +404,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     const float f = decay_pow(hp.log2a, t - 1 - su);
 #pragma unroll
     for (int k = 0; k < S; ++k) st4o<WT>(pw + 4 * G4 * k, sgd4(scale4(cur[k], f), g[k], hp.lr, hp.wd));
-    if (sub == 0) P.stamp[u] = t;
+    put_stamp<PUB>(P.stamp + u, t, sub == 0);
     SSTAMP(1, 3);
     return;
   }
@@ -382,7 +461,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
 #pragma unroll
       for (int k = 0; k < S; ++k) g[k] = part[0][sub + G4 * k];
       SSTAMP(1, 2);
-      finish_item<G4, S, SH, WT>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
+      finish_item<G4, S, SH, WT, PUB>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
     }
     SSTAMP(1, 3);
     return;
@@ -438,8 +517,41 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
     }
   }
   SSTAMP(1, 2);
-  finish_item<G4, S, SH, WT>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
+  finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
   SSTAMP(1, 3);
+}
+
+template <int G4, int S, bool SH, int KB, bool WT>
+__global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q, Hyper hp, int ld,
+                                                  const int32_t* __restrict__ tbase, int step,
+                                                  StepBufs sb, int long_blocks, int item_blocks,
+                                                  float* __restrict__ grads, double* __restrict__ loss,
+                                                  int64_t bstride, int B) {
+  if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
+  k2_body<G4, S, SH, KB, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, long_blocks,
+                                    item_blocks, grads, loss, B);
+}
+
+// The fused step: K2 of step t (batch c[1] + step) and K1 of step t + 1 (the next batch) in one
+// launch.  K2's workgroups come first in the grid, so every one of them is dispatched before any
+// K1 workgroup that may wait on it (bounded waits besides).  K1 of step t+1 reads the rows step t
+// does not touch at once and the others after their owners publish them; a chunk of n steps is
+// then K1, n - 1 fused launches and K2: one kernel boundary per step instead of two.
+template <int G4, int S, int KB>
+__global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table Q, Hyper hp, int ld,
+                                                   const int32_t* __restrict__ tbase, int step,
+                                                   StepBufs sb, int long_blocks, int item_blocks,
+                                                   int k2_blocks, double* __restrict__ loss,
+                                                   int64_t bstride, int B, int32_t* err) {
+  static_assert(KB == kBlock, "K1 and K2 workgroups share the launch's block size");
+  const int32_t t = tbase[0] + step + 1;
+  const int64_t kb = (int64_t)tbase[1] + step;
+  if ((int)blockIdx.x < k2_blocks)
+    k2_body<G4, S, false, KB, true, true>(blockIdx.x, bv0.shifted(kb * bstride), P, Q, hp, ld, t, sb,
+                                          long_blocks, item_blocks, nullptr, loss, B);
+  else
+    k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
+                                      hp, ld, t + 1, sb, nullptr, B, err);
 }
 
 // Expand BODY for every instantiated float4 geometry (G4_, S_).
@@ -465,25 +577,35 @@ static bool use_wt() {
   return !(e && e[0] == '0');
 }
 
+static StepBufs plain_bufs(float* contrib, float* ugrad, float* xloss, const StepBufs* sb) {
+  if (sb) return *sb;
+  StepBufs b;
+  b.contrib = contrib;
+  b.ugrad = ugrad;
+  b.xloss = xloss;
+  return b;
+}
+
 hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw,
-                     int64_t bstride) {
+                     int64_t bstride, const StepBufs* sbp) {
   const bool wt = use_wt();
+  const StepBufs sb = plain_bufs(contrib, ugrad, xloss, sbp);
   BPRMF_DISPATCH4(g, ({
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
     if (item_rows && wt)
-      k_user_step<G4_, S_, true, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                                 contrib, ugrad, item_rows, pw, bstride, B);
+      k_user_step<G4_, S_, true, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
+                                                                 item_rows, pw, bstride, B);
     else if (item_rows)
-      k_user_step<G4_, S_, true, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                                  contrib, ugrad, item_rows, pw, bstride, B);
+      k_user_step<G4_, S_, true, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
+                                                                  item_rows, pw, bstride, B);
     else if (wt)
-      k_user_step<G4_, S_, false, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                                  contrib, ugrad, nullptr, pw, bstride, B);
+      k_user_step<G4_, S_, false, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
+                                                                  nullptr, pw, bstride, B);
     else
-      k_user_step<G4_, S_, false, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, xloss,
-                                                                   contrib, ugrad, nullptr, pw, bstride, B);
+      k_user_step<G4_, S_, false, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
+                                                                   nullptr, pw, bstride, B);
   }));
   return hipGetLastError();
 }
@@ -492,25 +614,36 @@ int k1_triplets_per_block(const Geom& g) { return kBlock / g.G4; }
 
 int item_long_blocks(int B) { return std::min(kMaxLongItems, (2 * B) / (kLongSeg + 1)); }
 
-template <int G4, int S, int KB>
-static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, Table Q,
-                                   const Hyper& hp, const int32_t* tbase, int step,
-                                   const float* contrib, const float* ugrad, float* grads,
-                                   hipStream_t s, const float* xloss, double* loss,
-                                   int64_t bstride, bool wt) {
+// K2's grid: [loss workgroups][hot items][item segments][user segments spanning K1 workgroups]
+struct K2Grid {
+  int lb, long_blocks, item_blocks, user_blocks;
+  int total() const { return lb + long_blocks + item_blocks + user_blocks; }
+};
+template <int G4, int KB>
+static K2Grid k2_grid(int B, bool loss) {
   constexpr int NG = KB / G4;
-  const int long_blocks = item_long_blocks(B);
-  const int item_blocks = (int)((2LL * B + NG - 1) / NG);
+  K2Grid k;
+  k.long_blocks = item_long_blocks(B);
+  k.item_blocks = (int)((2LL * B + NG - 1) / NG);
   // segments K2 finishes span K1 workgroups: at most one per workgroup boundary, and B/2
   const int tpb = kBlock / G4;
   const int k2_users = (int)std::min<int64_t>(B / 2, (B + tpb - 1) / tpb);
-  const int user_blocks = (k2_users + NG - 1) / NG;
-  const int lb = loss ? (B + KB - 1) / KB : 0;  // <= kSegLossSlots
-  const unsigned blocks = (unsigned)(long_blocks + item_blocks + user_blocks + lb);
-#define BPRMF_K2(SH_, WT_)                                                                     \
-  k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, contrib, \
-                                                        ugrad, long_blocks, item_blocks, grads,  \
-                                                        xloss, loss, bstride, B)
+  k.user_blocks = (k2_users + NG - 1) / NG;
+  k.lb = loss ? (B + KB - 1) / KB : 0;  // <= kSegLossSlots
+  return k;
+}
+
+template <int G4, int S, int KB>
+static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, Table Q,
+                                   const Hyper& hp, const int32_t* tbase, int step,
+                                   const StepBufs& sb, float* grads, hipStream_t s, double* loss,
+                                   int64_t bstride, bool wt) {
+  const K2Grid k = k2_grid<G4, KB>(B, loss != nullptr);
+  const unsigned blocks = (unsigned)k.total();
+#define BPRMF_K2(SH_, WT_)                                                                        \
+  k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,       \
+                                                        k.long_blocks, k.item_blocks, grads, loss, \
+                                                        bstride, B)
   if (grads && wt) BPRMF_K2(true, true);
   else if (grads) BPRMF_K2(true, false);
   else if (wt) BPRMF_K2(false, true);
@@ -526,18 +659,34 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss, double* loss,
-                     int64_t bstride) {
-  if (!xloss) loss = nullptr;
+                     int64_t bstride, const StepBufs* sbp) {
+  const StepBufs sb = plain_bufs(const_cast<float*>(contrib), const_cast<float*>(ugrad),
+                                 const_cast<float*>(xloss), sbp);
+  if (!sb.xloss) loss = nullptr;
   const bool wt = use_wt();
   const char* kb = getenv("BPRMF_K2_BLOCK");
   const bool big = kb && atoi(kb) == 1024;
   BPRMF_DISPATCH4(g, ({
     if (big)
-      return launch_item_step<G4_, S_, (S_ == 1 ? 1024 : 512)>(g, bv, B, P, Q, hp, tbase, step,
-                                                               contrib, ugrad, grads, s, xloss,
-                                                               loss, bstride, wt);
-    return launch_item_step<G4_, S_, 256>(g, bv, B, P, Q, hp, tbase, step, contrib, ugrad, grads,
-                                          s, xloss, loss, bstride, wt);
+      return launch_item_step<G4_, S_, (S_ == 1 ? 1024 : 512)>(g, bv, B, P, Q, hp, tbase, step, sb,
+                                                               grads, s, loss, bstride, wt);
+    return launch_item_step<G4_, S_, 256>(g, bv, B, P, Q, hp, tbase, step, sb, grads, s, loss,
+                                          bstride, wt);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
+                      const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
+                      double* loss, int32_t* err, hipStream_t s) {
+  if (!sb.pend_q || !sb.pend_p || !sb.pstride || !bstride) return hipErrorInvalidValue;
+  if (!sb.xloss) loss = nullptr;
+  BPRMF_DISPATCH4(g, ({
+    const K2Grid k = k2_grid<G4_, kBlock>(B, loss != nullptr);
+    const int k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
+    k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
+        bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,
+        bstride, B, err);
   }));
   return hipGetLastError();
 }

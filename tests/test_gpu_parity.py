@@ -291,6 +291,33 @@ def test_replay_bucket_builder_empty_slots_and_duplicates(rl, monkeypatch):
     np.testing.assert_allclose(outs[0][1], Q, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("d,B", [(32, 4096), (128, 1000), (384, 256), (8, 64)])
+def test_fused_step_equals_separate_kernels_bitwise(rl, golden, monkeypatch, d, B):
+    """The fused launch (K2 of step t beside K1 of step t+1, rows handed over by published stamps)
+    gives the separate K1 / K2 launches' result bit for bit: same arithmetic, only the schedule
+    differs.  Chunks of odd lengths put the hand-off at every graph / eager boundary."""
+    pos, U, I = _ml100k_pos(golden)
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BPRMF_FUSED", fused)
+        m = _model(rl, U, I, d, B, seed=11)
+        m.set_train(pos)
+        n = m.epoch_size()[1]
+        first = 0
+        for c in (1, 2, 17, 40, 85):
+            c = min(c, n - first)
+            if c <= 0:
+                break
+            m.train_steps(0, first, c)
+            first += c
+        st = m.train_steps(1, 0, min(n, 33))
+        outs.append((m.get_weights(), st["loss"]))
+    (P0, Q0), l0 = outs[0]
+    (P1, Q1), l1 = outs[1]
+    assert np.array_equal(P0, P1) and np.array_equal(Q0, Q1)
+    assert l0 == l1
+
+
 def test_step_graphs_equal_eager_launches(rl, golden, monkeypatch):
     """Position-independent step graphs (sizes 64/16/4/1 replayed from the device cursor) give
     the same result as eager launches for chunks of any length at any offset."""

@@ -468,8 +468,8 @@ StepBufs bprmf::step_bufs(const bprmf_handle* h) {
   b.ugrad = h->d_ugrad;
   b.xloss = h->d_xloss;
   b.pstride = (int64_t)h->cfg.batch_size * h->geom.ld;
-  b.pend_q = h->d_pend_q;
-  b.pend_p = h->d_pend_p;
+  b.pend_q = h->fused ? h->d_pend_q : nullptr;  // only the fused step reads the marks
+  b.pend_p = h->fused ? h->d_pend_p : nullptr;
   b.qrows = h->I;
   b.prows = h->U;
   return b;

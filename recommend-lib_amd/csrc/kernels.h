@@ -31,7 +31,8 @@ struct Table {
 
 // One batch of a step, as laid out by k_build_batches (int32, positions within the batch).  Every
 // step kernel reaches its rows after ONE dependent load of a 16- or 32-byte record:
-//   trec  [B][4]    per triplet, sorted by (local) user row: {i, j, u, w}; w = 1: the user has no
+//   trec  [B][4]    per triplet, sorted by (local) user row: {i, j, u, w}; bit 31 of i (of j): this
+//                   triplet holds the item's first reference in the batch; w = 1: the user has no
 //                   other triplet in the batch (K1 updates the user row itself); w >= 2: head of the
 //                   user's segment of w triplets, all in one K1 workgroup (K1 sums it in LDS and
 //                   updates the row); w = -1: another member of such a segment; w = 0: a segment

@@ -346,7 +346,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] == kNone) continue;
-      if (r == 0 || s_key[r - 1] != ik[k]) {
+      const bool head = r == 0 || s_key[r - 1] != ik[k];
+      if (head) {
         ++s;
         v.ioff[s] = r;
         if (BUCKET) s_ioff[s] = r;
@@ -355,7 +356,15 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
           atomicAdd(&s_own[ik[k] / (uint32_t)iloc], 1);
         }
       }
-      if (slots) (iv[k] & 1 ? s_j : s_i)[iv[k] >> 1] = s;  // triplet side -> its item slot
+      // triplet side -> its item slot (sharded); bit 31: this reference is its item's first in
+      // the batch (K1 marks the item for the next step's fused K1 from that triplet only: one
+      // mark per distinct item instead of one per reference on hot addresses).  Each (triplet,
+      // side) belongs to exactly one reference, so the writes need no atomics.
+      int32_t& side = (iv[k] & 1 ? s_j : s_i)[iv[k] >> 1];
+      if (slots)
+        side = s | (head ? (int32_t)0x80000000 : 0);
+      else if (head)
+        side |= (int32_t)0x80000000;
     }
   }
   if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
@@ -446,8 +455,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   for (int k = 0; k < IPT; ++k) {
     const int p = tid * IPT + k;
     if (key[k] == kNone) continue;
-    const int ri_ = slots ? slot_of(s_i[p]) : s_i[p];
-    const int rj_ = slots ? slot_of(s_j[p]) : s_j[p];
+    const int32_t hi = s_i[p] & (int32_t)0x80000000, hj = s_j[p] & (int32_t)0x80000000;
+    const int ri_ = slots ? (slot_of(s_i[p] & 0x7FFFFFFF) | hi) : s_i[p];
+    const int rj_ = slots ? (slot_of(s_j[p] & 0x7FFFFFFF) | hj) : s_j[p];
     reinterpret_cast<int4*>(v.trec)[p] = make_int4(ri_, rj_, (int)key[k], uw[k]);
     if (uhead[k] && uw[k] == 0) {  // a segment K2 finishes
       store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], p, uend[k], 0, 0, 0, 0, 0);

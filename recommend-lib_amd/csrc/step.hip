@@ -33,12 +33,12 @@ __device__ uint64_t g_step_stamps[2][8192][6];
   do {                                                                            \
     if (threadIdx.x == 0) {                                                       \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
-      g_step_stamps[kern][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();      \
+      g_step_stamps[kern][blk][k] = __builtin_amdgcn_s_memrealtime();             \
     }                                                                             \
   } while (0)
 #define SROLE(kern, r)                                                            \
   do {                                                                            \
-    if (threadIdx.x == 0) g_step_stamps[kern][blockIdx.x][5] = (r);               \
+    if (threadIdx.x == 0) g_step_stamps[kern][blk][5] = (r);                      \
   } while (0)
 extern "C" int bprmf_debug_step_stamps(uint64_t* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)) == hipSuccess ? 0 : -3;
@@ -167,15 +167,20 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
   int32_t u = 0;
   __shared__ float4 s_g[S * kBlock];  // per-triplet user gradients of in-workgroup segments
   if (p < n) {
-    const int32_t i = r.x, j = r.y;
+    const int32_t i = r.x & 0x7FFFFFFF, j = r.y & 0x7FFFFFFF;  // bit 31: the item's first ref
     u = r.z;
     w = r.w;
     prow = P.W + (int64_t)u * ld + 4 * sub;
     if (sb.pend_q && sub == 0) {  // this step's rows, for the next step's fused K1
+      // one mark per distinct item (from the triplet holding its first reference) and per user
+      // K2 finishes; write-through (sc1), so no dirty partial lines wait for the kernel boundary
       const int64_t o = (int64_t)(t & 1);
-      sb.pend_q[o * sb.qrows + i] = t;
-      sb.pend_q[o * sb.qrows + j] = t;
-      if (w == 0) sb.pend_p[o * sb.prows + u] = t;
+      if (r.x < 0)
+        __hip_atomic_store(sb.pend_q + o * sb.qrows + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r.y < 0)
+        __hip_atomic_store(sb.pend_q + o * sb.qrows + j, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0)
+        __hip_atomic_store(sb.pend_p + o * sb.prows + u, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     bool wi = false, wj = false, wu = false;
     const int32_t tp = t - 1;
@@ -188,6 +193,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       if (wj) wait_stamp(Q.stamp + j, tp, err);
       if (wu) wait_stamp(P.stamp + u, tp, err);
     }
+    SSTAMP(0, 4);
     const float* qbase = SH ? item_rows : Q.W;
     const float* qi = qbase + (int64_t)i * ld + 4 * sub;
     const float* qj = qbase + (int64_t)j * ld + 4 * sub;
@@ -429,16 +435,17 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
       const int ridx = base + NG * sub;
       const int32_t myref = ridx < end ? bv.refs[ridx] : 0;
       const int cnt = min(G4, (end - base + NG - 1) / NG);
-      for (int m0 = 0; m0 < cnt; m0 += 8) {
-        float4 rows[8][S];
-        int32_t rf[8];
+      constexpr int F = S == 1 ? 16 : 8;  // rows in flight per group (a hot item has ~80 refs)
+      for (int m0 = 0; m0 < cnt; m0 += F) {
+        float4 rows[F][S];
+        int32_t rf[F];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
+        for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
           if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
+        for (int m = 0; m < F; ++m)
           if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
       }
     }
@@ -478,7 +485,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const int32_t item = r0.x;
   const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
 #ifdef BPRMF_STEP_STAMPS
-  if (threadIdx.x == 0) g_step_stamps[1][blockIdx.x][4] = (uint64_t)len;
+  if (threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
 #endif
   ItemRow<G4, S, SH> row;
   row.load(Q, item, ld, sub);

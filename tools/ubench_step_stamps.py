@@ -41,27 +41,27 @@ for rep in range(8):
     st = np.zeros((2, 8192, 6), np.uint64)
     assert L.bprmf_debug_step_stamps(st.ctypes.data) == 0
     samples.append(st.astype(np.int64))
-roles = {0: "loss", 1: "long item", 2: "item", 3: "multi user"}
+roles = {1: "long item", 2: "item", 3: "multi user"}
 
 
 def summarize(st, k1_blocks, k2_blocks):
     res = {}
     k1 = st[0, :k1_blocks]
     k2 = st[1, :k2_blocks]
-    t0 = k1[:, 0].min()
+    # fused launch: K2 (step t) and K1 (step t+1) share the launch; time from its first start
+    t0 = min(k1[:, 0].min(), k2[k2[:, 0] > 0][:, 0].min())
     us = lambda x: round(float(x) * 0.01, 2)  # 100 MHz ticks -> us
-    res["K1 first start -> last start"] = us(k1[:, 0].max() - t0)
+    res["K1 first start"] = us(k1[:, 0].min() - t0)
+    res["K1 first start -> last start"] = us(k1[:, 0].max() - k1[:, 0].min())
     res["K1 record (median, max)"] = [us(np.median(k1[:, 1] - k1[:, 0])), us((k1[:, 1] - k1[:, 0]).max())]
-    res["K1 rows (median, max)"] = [us(np.median(k1[:, 2] - k1[:, 1])), us((k1[:, 2] - k1[:, 1]).max())]
+    res["K1 wait (median, max)"] = [us(np.median(k1[:, 4] - k1[:, 1])), us((k1[:, 4] - k1[:, 1]).max())]
+    res["K1 rows (median, max)"] = [us(np.median(k1[:, 2] - k1[:, 4])), us((k1[:, 2] - k1[:, 4]).max())]
     res["K1 stores (median, max)"] = [us(np.median(k1[:, 3] - k1[:, 2])), us((k1[:, 3] - k1[:, 2]).max())]
     res["K1 last end"] = us(k1[:, 3].max() - t0)
     res["K2 first start"] = us(k2[:, 0].min() - t0)
     res["K2 last start"] = us(k2[:, 0].max() - t0)
     for r, name in roles.items():
         sel = k2[:, 5] == r
-        if r == 0:
-            sel = np.zeros(len(k2), bool)
-            sel[0] = True
         if not sel.any():
             continue
         x = k2[sel]
@@ -80,11 +80,30 @@ def summarize(st, k1_blocks, k2_blocks):
 k1_blocks = B // (256 // 32)
 KB = int(os.environ.get("BPRMF_K2_BLOCK", "256"))
 NG = KB // 32
-k2_blocks = 1 + 64 + (2 * B) // NG + (B // 2) // NG
+lb = (B + KB - 1) // KB
+k2_users = min(B // 2, B // 8)
+k2_blocks = lb + 64 + (2 * B) // NG + (k2_users + NG - 1) // NG
+def by_len(st, k2_blocks):
+    k2 = st[1, :k2_blocks]
+    sel = (k2[:, 5] == 2) & (k2[:, 3] >= k2[:, 0]) & (k2[:, 2] > 0)
+    x = k2[sel]
+    t0 = st[0, :, 0][st[0, :, 0] > 0].min()
+    out = {}
+    for lo, hi in ((1, 4), (5, 8), (9, 12), (13, 16), (17, 10**6)):
+        m = (x[:, 4] >= lo) & (x[:, 4] <= hi)
+        if m.any():
+            out[f"len {lo}-{hi}"] = dict(n=int(m.sum()), sums_med=round(float(np.median(x[m, 2] - x[m, 1])) * 0.01, 2),
+                                         sums_max=round(float((x[m, 2] - x[m, 1]).max()) * 0.01, 2),
+                                         end_max=round(float(x[m, 3].max() - t0) * 0.01, 2))
+    return out
+
+
 for n, st in enumerate(samples[2:]):
     # the last step's stamps: clear stale rows (their stamps are older than this K1's start)
     st = st.copy()
+    # the last launch: K1 stamps of its step; K2 stamps of the same launch (within ~50 us)
     t0 = st[0, :k1_blocks, 0].min()
-    st[1, :k2_blocks][st[1, :k2_blocks, 0] < t0] = 0
+    st[1, :k2_blocks][st[1, :k2_blocks, 0] < t0 - 5000] = 0
     out[f"rep{n}"] = summarize(st, k1_blocks, k2_blocks)
+    out[f"rep{n}"]["items by length"] = by_len(st, k2_blocks)
 print(json.dumps(out, indent=1))

@@ -17,7 +17,8 @@ LIB = os.path.join(ROOT, "tools", "libbprmf_step_stamps.so")
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     b = importlib.import_module("recommend-lib_amd.build")
-    print(b.build(force=True, defines=("BPRMF_STEP_STAMPS",), out=LIB))
+    # fused launches only: the chunk's epilogue K2 would overwrite the last fused launch's K2
+    print(b.build(force=True, defines=("BPRMF_STEP_STAMPS", "BPRMF_FUSED_STAMPS_ONLY=1"), out=LIB))
     sys.exit(0)
 
 os.environ["BPRMF_DIAG_LIB"] = LIB

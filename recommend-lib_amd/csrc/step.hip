@@ -29,16 +29,21 @@ namespace bprmf {
 // drained (thread 0; the waits serialise that thread, so the stamps bound each phase from above).
 #ifdef BPRMF_STEP_STAMPS
 __device__ uint64_t g_step_stamps[2][8192][6];
+#ifdef BPRMF_FUSED_STAMPS_ONLY  // only the fused launches stamp (the chunk's last K2 would overwrite)
+constexpr bool kFusedStampsOnly = true;
+#else
+constexpr bool kFusedStampsOnly = false;
+#endif
 #define SSTAMP(kern, k)                                                           \
   do {                                                                            \
-    if (threadIdx.x == 0) {                                                       \
+    if (kStampHere && threadIdx.x == 0) {                                         \
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
       g_step_stamps[kern][blk][k] = __builtin_amdgcn_s_memrealtime();             \
     }                                                                             \
   } while (0)
 #define SROLE(kern, r)                                                            \
   do {                                                                            \
-    if (threadIdx.x == 0) g_step_stamps[kern][blk][5] = (r);                      \
+    if (kStampHere && threadIdx.x == 0) g_step_stamps[kern][blk][5] = (r);        \
   } while (0)
 extern "C" int bprmf_debug_step_stamps(uint64_t* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)) == hipSuccess ? 0 : -3;
@@ -148,6 +153,9 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, const float* __restrict__ item_rows,
                                                int B, int32_t* err) {
+#ifdef BPRMF_STEP_STAMPS
+  constexpr bool kStampHere = WAIT || !kFusedStampsOnly;
+#endif
   SSTAMP(0, 0);
   const int sub = threadIdx.x & (G4 - 1);
   const int p = blk * (kBlock / G4) + threadIdx.x / G4;
@@ -361,6 +369,9 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
                                                float* __restrict__ grads, double* __restrict__ loss,
                                                int B) {
   constexpr int NG = KB / G4;
+#ifdef BPRMF_STEP_STAMPS
+  constexpr bool kStampHere = PUB || !kFusedStampsOnly;
+#endif
   SSTAMP(1, 0);
   const int sub = threadIdx.x & (G4 - 1);
   const int grp = threadIdx.x / G4;
@@ -485,7 +496,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const int32_t item = r0.x;
   const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
 #ifdef BPRMF_STEP_STAMPS
-  if (threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
+  if (kStampHere && threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
 #endif
   ItemRow<G4, S, SH> row;
   row.load(Q, item, ld, sub);

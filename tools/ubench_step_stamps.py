@@ -104,7 +104,7 @@ for n, st in enumerate(samples[2:]):
     st = st.copy()
     # the last launch: K1 stamps of its step; K2 stamps of the same launch (within ~50 us)
     t0 = st[0, :k1_blocks, 0].min()
-    st[1, :k2_blocks][st[1, :k2_blocks, 0] < t0 - 5000] = 0
+    st[1, :k2_blocks][st[1, :k2_blocks, 0] < t0 - 500] = 0
     out[f"rep{n}"] = summarize(st, k1_blocks, k2_blocks)
     out[f"rep{n}"]["items by length"] = by_len(st, k2_blocks)
 print(json.dumps(out, indent=1))

@@ -150,7 +150,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
-  const size_t status_bytes = 16 + sizeof(double) * kLossSlots;
+  // {err, dist words, loss slots[kLossSlots], call sequence number}
+  const size_t status_bytes = 16 + sizeof(double) * kLossSlots + 8;
   TRY(dalloc(&h->d_status, (int64_t)status_bytes));
   if (hipHostMalloc((void**)&h->h_status, status_bytes, hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&h->h_status_dev, h->h_status, 0) != hipSuccess) {
@@ -159,6 +160,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     bprmf_destroy(h);
     return fail(BPRMF_E_HIP, "hipHostMalloc (mapped status) failed");
   }
+  memset(h->h_status, 0, status_bytes);  // no stale call sequence number
   h->d_err = reinterpret_cast<int32_t*>(h->d_status);
   h->d_loss = reinterpret_cast<double*>(h->d_status + 16);
   h->P.rows = h->U;
@@ -379,10 +381,30 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   if (h->call_slots) {
     HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * kLossSlots,
                           hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
   } else {
-    HIPCHK(status_out(h->d_status, h->h_status_dev, 2 + kSegLossSlots, h->stream));
+    // the status words, then this call's sequence number, written into mapped host memory; the
+    // host spins on that word (a blocking stream synchronisation wakes up tens of microseconds
+    // later), and falls back to synchronising if the stream ends or fails without it
+    const size_t seq_off = 16 + sizeof(double) * kLossSlots;
+    const uint64_t seq = ++h->status_seq;
+    HIPCHK(status_out(h->d_status, h->h_status_dev, 2 + kSegLossSlots, h->stream,
+                      h->h_status_dev + seq_off, seq));
+    const volatile uint64_t* hs = reinterpret_cast<const volatile uint64_t*>(h->h_status + seq_off);
+    bool seen = false;
+    for (uint32_t spin = 1;; ++spin) {
+      if (*hs == seq) {
+        seen = true;
+        break;
+      }
+      if ((spin & 4095) == 0 && hipStreamQuery(h->stream) != hipErrorNotReady) {
+        seen = *hs == seq;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    if (!seen) HIPCHK(hipStreamSynchronize(h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
   const int32_t e = *reinterpret_cast<const volatile int32_t*>(h->h_status);
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
@@ -483,9 +505,10 @@ extern "C" {
 //   fused (default):  K2 of step r and K1 of step r + 1 in one launch (k_fused_step); the chunk
 //                     is K1(0), units 0 .. nb-2, K2(nb-1): nb + 1 launches;
 //   unfused:          K1(r) then K2(r): 2 nb launches.
-// Units run as replays of position-independent graphs of 64 and 16 units (captured once per
-// batch buffer; every graph but the chunk's last ends by advancing the cursor) plus fewer than 16
-// eager units; the eager launches and the epilogue index the cursor as the graphs left it.
+// Chunks of 64 units or more run as replays of position-independent graphs of 64 and 16 units
+// (captured once per batch buffer; every graph but the chunk's last ends by advancing the cursor)
+// plus fewer than 16 eager units; the eager launches and the epilogue index the cursor as the
+// graphs left it.  Shorter chunks launch every unit eagerly.
 static void drop_graphs(bprmf_handle* h) {
   for (auto& ge : h->graphs)
     if (ge.exec) hipGraphExecDestroy(ge.exec);
@@ -555,7 +578,9 @@ static int ensure_step_graphs(bprmf_handle* h) {
 static int run_units(bprmf_handle* h, int64_t n, int64_t* base) {
   *base = 0;
   int64_t done = 0;
-  if (h->use_graphs) {
+  // short chunks launch eagerly: a graph's end costs ~8 us before the next launch starts, more
+  // than the host needs per launch (~4 us) while each fused launch runs ~10 us on the GPU
+  if (h->use_graphs && n >= kGraphSizes[0]) {
     if (int r = ensure_step_graphs(h)) return r;
     const int64_t n64 = n / kGraphSizes[0], n16 = (n % kGraphSizes[0]) / kGraphSizes[1];
     const int64_t ng = n64 + n16;
@@ -614,8 +639,17 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   }
   if (int r = ensure_seg(h, nb)) return r;
   BatchBuf bb{h->d_batch, (int)B};
-  // the cursor (and the call's loss slots) first: cheap, and off the path between build and steps
-  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
+  // the cursor and the call's loss slots: set by the builder's first workgroup (one launch fewer
+  // per call), or by their own launch when every per-wave slot needs zeroing
+  CursorInit ci;
+  ci.cursor = h->d_tbase;
+  ci.t = h->t;
+  ci.loss = h->d_loss;
+  ci.nloss = loss_zero_slots(h);
+  if (ci.nloss > kSegLossSlots) {
+    HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, ci.nloss));
+    ci = CursorInit{};
+  }
   {
     ProfScope ps(h, BPRMF_KPROF_SAMPLE);
     if (!ru && split_build(nb)) {
@@ -625,10 +659,11 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
       HIPCHK(build_batches(sampler_args(h), epoch, 0, n, (int)B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, 1, false, 0, nb, bb,
-                           h->d_err, h->stream, k1_triplets_per_block(h->geom)));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
-                           h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
+                           h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream,
+                           k1_triplets_per_block(h->geom), ci));
     }
   }
   {

@@ -72,6 +72,7 @@ struct bprmf_handle {
   unsigned char* d_status = nullptr;
   unsigned char* h_status = nullptr;      // pinned, mapped host mirror
   unsigned char* h_status_dev = nullptr;  // its device address (k_status_out writes there)
+  uint64_t status_seq = 0;                // sequence number of the last call's status block
   double* d_loss = nullptr;               // = d_status + 16
   int32_t* d_err = nullptr;               // = d_status
   bool loss_pending = false;    // a call began: the loss slots are zeroed before the first step

@@ -109,8 +109,10 @@ struct SamplerArgs {
 // (loss != null: also zero loss[0 .. nloss))
 hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, double* loss = nullptr,
                       int nloss = 0);
-// copy `words` 8-byte words of device memory into mapped host memory (one tiny kernel)
-hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s);
+// copy `words` (<= 64) 8-byte words of device memory into mapped host memory (one tiny kernel);
+// seq_dev != null: then store seq there (mapped host memory) after those words are written
+hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s,
+                      void* seq_dev = nullptr, uint64_t seq = 0);
 hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s);
 hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
                        uint32_t table_tag, int world, int rank, hipStream_t s);
@@ -127,10 +129,18 @@ hipError_t apply_refs(const Geom& g, const int32_t* tu, const int32_t* ti, const
 // ru/ri/rj are GLOBAL ids (users are mapped to local rows u / world).  i_rows = global item count.
 // slots: write item slots (sharded exchange) instead of item rows into ij/urec and irec/lrec:
 // the item segment index (slot_stride 0) or owner * slot_stride + index within the owner's range.
+// cursor != null: the builder's first workgroup also does set_cursor's work (one launch fewer)
+struct CursorInit {
+  int32_t* cursor = nullptr;
+  int32_t t = 0, k = 0;
+  double* loss = nullptr;
+  int nloss = 0;
+};
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
-                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb);
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
+                         const CursorInit& ci = CursorInit{});
 // triplets per K1 workgroup for a geometry (the builder marks user segments that lie in one)
 int k1_triplets_per_block(const Geom& g);
 // Per-step buffers of the step kernels.  pstride != 0 (single GPU): contrib / ugrad / xloss hold

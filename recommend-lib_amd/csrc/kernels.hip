@@ -360,10 +360,17 @@ __global__ void k_advance_cursor(int32_t* __restrict__ c, int32_t n) {
   c[1] += n;
 }
 // the call's status words straight into mapped host memory (system-scope stores), so the host
-// reads them after one stream synchronisation without a copy command
-__global__ void k_status_out(const uint64_t* __restrict__ src, uint64_t* dst, int n) {
+// reads them without a copy command; then (seq_dst) the call's sequence number, once every lane's
+// stores are acknowledged: the host spins on that word instead of synchronising the stream
+__global__ void k_status_out(const uint64_t* __restrict__ src, uint64_t* dst, int n, uint64_t* seq_dst,
+                             uint64_t seq) {
   const int i = threadIdx.x;
   if (i < n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (seq_dst) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (i == 0) __hip_atomic_store(seq_dst, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, double* loss, int nloss) {
@@ -371,9 +378,12 @@ hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, doub
   return hipGetLastError();
 }
 
-hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s) {
+hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s,
+                      void* seq_dev, uint64_t seq) {
+  if (words > 64) return hipErrorInvalidValue;
   k_status_out<<<1, 64, 0, s>>>(static_cast<const uint64_t*>(d_status),
-                                static_cast<uint64_t*>(h_status_dev), words);
+                                static_cast<uint64_t*>(h_status_dev), words,
+                                static_cast<uint64_t*>(seq_dev), seq);
   return hipGetLastError();
 }
 

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
     int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int slot_stride,
-    int user_bits, int item_bits, int tpb, BatchBuf bb, int32_t* __restrict__ err) {
+    int user_bits, int item_bits, int tpb, BatchBuf bb, int32_t* __restrict__ err, CursorInit ci) {
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -186,6 +186,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
   const BatchView v = bb.view(batch);
   if (tid < kMaxWorld) s_own[tid] = 0;
+  if (batch == 0 && ci.cursor) {  // set_cursor's work (kernels.hip k_set_cursor)
+    if (tid == 0) {
+      ci.cursor[0] = ci.t;
+      ci.cursor[1] = ci.k;
+    }
+    if (ci.loss && tid < ci.nloss) ci.loss[tid] = 0.0;
+  }
   BSTAMP(0);
 
   // 1. the batch's triplets in slot order, keyed by local user row
@@ -490,8 +497,10 @@ static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
-                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb) {
+                         int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
+                         const CursorInit& ci) {
   if (n_batches <= 0) return hipSuccess;
+  if (ci.cursor && ci.loss && ci.nloss > kBuildThreads) return hipErrorInvalidValue;
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
   const int64_t iloc = (i_rows + world - 1) / world;
   if ((uint64_t)iloc * (uint64_t)world >= 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -502,15 +511,15 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   if (B <= kBuildThreads * 4 && !radix)
     k_build_batches<4, true><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
   else if (B <= kBuildThreads * 4)
     k_build_batches<4, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
   else
     k_build_batches<8, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err);
+        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
   return hipGetLastError();
 }
 

@@ -319,8 +319,9 @@ def test_fused_step_equals_separate_kernels_bitwise(rl, golden, monkeypatch, d, 
 
 
 def test_step_graphs_equal_eager_launches(rl, golden, monkeypatch):
-    """Position-independent step graphs (sizes 64/16/4/1 replayed from the device cursor) give
-    the same result as eager launches for chunks of any length at any offset."""
+    """Position-independent step graphs (sizes 64/16 replayed from the device cursor; chunks of
+    64 units or more) give the same result as eager launches for chunks of any length at any
+    offset."""
     pos, U, I = _ml100k_pos(golden)
     outs = []
     for eager in (False, True):

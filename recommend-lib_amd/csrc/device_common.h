@@ -22,8 +22,10 @@ static __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint
                                          uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    // one 32x32->64 multiply each (v_mad_u64_u32) instead of a mul_lo + mul_hi pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0;
     c1 = lo1;
@@ -56,13 +58,18 @@ static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int h
 // unbiased Lemire reduction into [0, n), n >= 1; retries draw fresh counters (attempt in tag).
 static __device__ __forceinline__ uint32_t bounded(uint64_t q, uint32_t epoch, uint32_t n, uint32_t k0,
                                             uint32_t k1) {
-  const uint32_t thresh = (uint32_t)((0x100000000ull - n) % n);
+  const uint32_t thresh = (0u - n) % n;  // (2^32 - n) mod n in 32-bit arithmetic
   for (uint32_t a = 0;; ++a) {
     uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = epoch, c3 = TAG_NEG | a;
     philox10(c0, c1, c2, c3, k0, k1);
     const uint64_t m = (uint64_t)c0 * n;
     if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
   }
+}
+
+// q / d for the sampler's triplet -> positive map: 32-bit division when q fits (the usual case)
+static __device__ __forceinline__ int64_t div_small(uint64_t q, uint32_t d) {
+  return q >> 32 ? (int64_t)(q / d) : (int64_t)((uint32_t)q / d);
 }
 
 // j = the k-th item id NOT in the sorted positive list a[0..n): m = #{x : a[x]-x <= k}, j = k+m.

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(kBlock) void k_sample(SamplerArgs a, uint32_t epoch
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count;
        s += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t q = permute((uint64_t)(first + s), N, a.feistel_h, a.k0, a.k1, epoch);
-    const int64_t p = (int64_t)(q / (uint64_t)a.num_ng);
+    const int64_t p = div_small(q, (uint32_t)a.num_ng);
     const int32_t u = a.pos_u[p];
     const int32_t i = a.pos_i[p];
     const int64_t ul = u / a.world;

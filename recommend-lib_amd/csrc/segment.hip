@@ -72,7 +72,18 @@ struct BucketScratch {
 template <int T, int E, class KeyOf, class ValOf>
 static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t (&val)[E], int bits,
                                                    const BucketScratch<T>& sc, KeyOf key_of,
-                                                   ValOf val_of) {
+                                                   ValOf val_of, int sb = -1) {
+  // sb >= 0 (diagnostic build): stamps sb .. sb+4 after count, scan, scatter, rank, gather
+#ifdef BPRMF_BUILD_STAMPS
+#define BSTAMP_SORT(k) \
+  do {                 \
+    if (sb >= 0) BSTAMP(sb + (k)); \
+  } while (0)
+#else
+#define BSTAMP_SORT(k) \
+  do {                 \
+  } while (0)
+#endif
   using Scan = rocprim::block_scan<int, T>;
   static_assert(kBuckets % T == 0, "buckets per thread");
   constexpr int PB = kBuckets / T;
@@ -86,6 +97,7 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
   for (int k = 0; k < E; ++k)
     li[k] = key[k] != kNone ? atomicAdd(&sc.start[key[k] >> shift], 1) : -1;
   __syncthreads();
+  BSTAMP_SORT(0);
   int c[PB], sum = 0;
 #pragma unroll
   for (int m = 0; m < PB; ++m) {
@@ -101,6 +113,7 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
   }
   if (tid == 0) sc.start[kBuckets] = total;
   __syncthreads();
+  BSTAMP_SORT(1);
 #pragma unroll
   for (int k = 0; k < E; ++k) {
     const int q = tid * E + k;
@@ -110,6 +123,7 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
       sc.srt[total + atomicAdd(sc.ninv, 1)] = q;
   }
   __syncthreads();
+  BSTAMP_SORT(2);
   for (int x = tid; x < total; x += T) {
     const uint64_t me = sc.bk[x];
     const int b = (int)((uint32_t)(me >> 32) >> shift);
@@ -123,6 +137,7 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
     sc.srt[bs + rank] = (int32_t)(uint32_t)me;
   }
   __syncthreads();
+  BSTAMP_SORT(3);
 #pragma unroll
   for (int k = 0; k < E; ++k) {
     const int pos = tid * E + k;
@@ -136,6 +151,8 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
     }
   }
   __syncthreads();  // the caller reuses the scratch (its sorted keys alias bk)
+  BSTAMP_SORT(4);
+#undef BSTAMP_SORT
 }
 
 // BUCKET: bucket sorts (B <= kBuildThreads * 4); else rocPRIM block radix sorts.  Both give the
@@ -211,7 +228,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         j = rj[b0 + p];
       } else {
         const uint64_t q = permute((uint64_t)(first_slot + b0 + p), N, a.feistel_h, a.k0, a.k1, epoch);
-        const int64_t pp = (int64_t)(q / (uint64_t)a.num_ng);
+        const int64_t pp = div_small(q, (uint32_t)a.num_ng);
         const int64_t ul = a.pos_u[pp] / a.world;
         i = a.pos_i[pp];
         const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
@@ -326,7 +343,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
           const uint32_t item = (uint32_t)(r < nv ? s_i[r] : s_j[r - nv]);
           return (item % (uint32_t)world) * (uint32_t)iloc + item / (uint32_t)world;
         },
-        [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); });
+        [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, 9);
   } else {
     SortI().sort(ik, iv, reinterpret_cast<RadixSmem*>(s_sort)->si, 0, item_bits);
     __syncthreads();  // also: every read of s_i/s_j above is done

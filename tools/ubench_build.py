@@ -31,8 +31,8 @@ L = rl._lib.load()
 L.bprmf_debug_build_stamps.argtypes = [ctypes.c_void_p]
 pos = syn.make_positives(138493, 26744, 10_000_000, 20261015)
 res = {}
-for radix in ("0", "1"):
-    for split in ("1", "0"):
+for radix in ("0",) if "--quick" in sys.argv else ("0", "1"):
+    for split in ("1",) if "--quick" in sys.argv else ("1", "0"):
         os.environ["BPRMF_SPLIT_BUILD"] = split
         if radix == "1":
             os.environ["BPRMF_RADIX_BUILD"] = "1"
@@ -46,10 +46,15 @@ for radix in ("0", "1"):
             st = np.zeros(16, np.uint64)
             assert L.bprmf_debug_build_stamps(st.ctypes.data) == 0
             d = np.diff(st[:9].astype(np.int64)) * 0.01  # 100 MHz -> us
-            rows.append(d)
+            x = st.astype(np.int64)
+            sub = np.diff(np.concatenate([x[3:4], x[9:14]])) * 0.01 if radix == "0" else np.zeros(5)
+            rows.append(np.concatenate([d, sub]))
         med = np.median(np.array(rows[1:]), axis=0)
         key = f"radix={radix} split={split}"
-        res[key] = {p: round(float(v), 2) for p, v in zip(PHASES, med)}
-        res[key]["total"] = round(float(med.sum()), 2)
+        res[key] = {p: round(float(v), 2) for p, v in zip(PHASES, med[:8])}
+        res[key]["total"] = round(float(med[:8].sum()), 2)
+        if radix == "0":  # the item bucket sort's own phases
+            res[key]["item sort phases"] = {p: round(float(v), 2) for p, v in zip(
+                ("keys+count", "scan", "scatter", "rank", "gather"), med[8:])}
         m.close()
 print(json.dumps(res, indent=1))

@@ -201,8 +201,9 @@ def main():
             if "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
-            elif "step_graph" in us:  # events around graph replays of whole steps (GPU-bound)
-                step_us, what = us["step_graph"], "step graph: user_step + item_step (+ their gap)"
+            elif "step_graph" in us:  # events around each chunk's step launches (GPU-bound)
+                step_us, what = us["step_graph"], ("fused step launches (K2 of step t + K1 of step "
+                                                   "t+1 per launch; a chunk is K1, n-1 fused, K2)")
             else:  # eager (sharded): events around the two kernels of sampled steps
                 step_us, what = us["user_step"] + us["item_step"], "user_step + item_step"
             ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9

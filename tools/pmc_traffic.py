@@ -3,8 +3,8 @@
   python tools/pmc_traffic.py KEY FETCH_DIR WRITE_DIR [--out profiles/pmc_traffic.json]
 
 FETCH_SIZE and WRITE_SIZE (KB per dispatch) are averaged per kernel over all dispatches; the step
-traffic is the sum over the step kernels (user_step + item_step; + owner-side kernels when
-sharded).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half the bytes
+traffic is one fused launch's (single GPU, fused step), else the sum over the step kernels
+(user_step + item_step; + owner-side kernels when sharded).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half the bytes
 of a wide coalesced (16 B/lane) read, so it is doubled; WRITE_SIZE is exact for 16-B/lane stores.
 Infinity-Cache hits are counted by these counters (they are L2-miss requests), so for tables that
 fit the 256 MiB MALL this is L2-miss traffic, not strictly DRAM bytes.
@@ -16,7 +16,8 @@ import glob
 import json
 import os
 
-STEP_KERNELS = ("k_user_step", "k_item_step", "k_gather_rows", "k_add_rows", "k_apply_rows")
+STEP_KERNELS = ("k_fused_step", "k_user_step", "k_item_step", "k_gather_rows", "k_add_rows",
+                "k_apply_rows")
 
 
 def per_kernel(d, counter):
@@ -46,7 +47,12 @@ def main():
     kernels = {k: dict(fetch_kb_raw=round(fetch.get(k, 0.0), 1), write_kb=round(write.get(k, 0.0), 1),
                        bytes=round((2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024))
                for k in sorted(set(fetch) | set(write))}
-    total = sum(v["bytes"] for v in kernels.values())
+    # single GPU, fused (default): one k_fused_step launch = K2 of a step + K1 of the next, so
+    # one launch's traffic is one step's (the chunk's lone K1 and K2 launches are its two ends)
+    if "k_fused_step" in kernels:
+        total = kernels["k_fused_step"]["bytes"]
+    else:
+        total = sum(v["bytes"] for v in kernels.values())
     alg = a.batch * (24 * a.factor + 12)
     entry = dict(hbm_bytes_per_step=total, algorithmic_bytes_per_step=alg,
                  ratio_to_algorithmic=round(total / alg, 3), kernels=kernels,

@@ -150,8 +150,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
-  // {err, dist words, loss slots[kLossSlots], call sequence number}
-  const size_t status_bytes = 16 + sizeof(double) * kLossSlots + 8;
+  // {err, dist words, loss slots[kLossSlots], two call sequence numbers}
+  const size_t status_bytes = kSeqCapOff + 8;
   TRY(dalloc(&h->d_status, (int64_t)status_bytes));
   if (hipHostMalloc((void**)&h->h_status, status_bytes, hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&h->h_status_dev, h->h_status, 0) != hipSuccess) {
@@ -375,6 +375,17 @@ int bprmf::begin_call(bprmf_handle* h) {
 
 // one status read per call: {err, loss} written into mapped host memory by one tiny kernel (the
 // f32-atomic path's per-wave slots: one copy), then one stream synchronisation
+int bprmf::wait_mapped_seq(bprmf_handle* h, size_t off, uint64_t seq) {
+  const volatile uint64_t* hs = reinterpret_cast<const volatile uint64_t*>(h->h_status + off);
+  for (uint32_t spin = 1;; ++spin) {
+    if (*hs == seq) return 0;
+    if ((spin & 4095) == 0 && hipStreamQuery(h->stream) != hipErrorNotReady && *hs != seq) break;
+    __builtin_ia32_pause();
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   const bool ran = !h->loss_pending;
   h->loss_pending = false;
@@ -383,27 +394,11 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
                           hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
   } else {
-    // the status words, then this call's sequence number, written into mapped host memory; the
-    // host spins on that word (a blocking stream synchronisation wakes up tens of microseconds
-    // later), and falls back to synchronising if the stream ends or fails without it
-    const size_t seq_off = 16 + sizeof(double) * kLossSlots;
+    // the status words, then this call's sequence number, written into mapped host memory
     const uint64_t seq = ++h->status_seq;
     HIPCHK(status_out(h->d_status, h->h_status_dev, 2 + kSegLossSlots, h->stream,
-                      h->h_status_dev + seq_off, seq));
-    const volatile uint64_t* hs = reinterpret_cast<const volatile uint64_t*>(h->h_status + seq_off);
-    bool seen = false;
-    for (uint32_t spin = 1;; ++spin) {
-      if (*hs == seq) {
-        seen = true;
-        break;
-      }
-      if ((spin & 4095) == 0 && hipStreamQuery(h->stream) != hipErrorNotReady) {
-        seen = *hs == seq;
-        break;
-      }
-      __builtin_ia32_pause();
-    }
-    if (!seen) HIPCHK(hipStreamSynchronize(h->stream));
+                      h->h_status_dev + kSeqEndOff, seq));
+    if (int r = wait_mapped_seq(h, kSeqEndOff, seq)) return r;
   }
   const int32_t e = *reinterpret_cast<const volatile int32_t*>(h->h_status);
   if (e) {

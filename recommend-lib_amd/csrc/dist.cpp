@@ -557,11 +557,12 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   HIPCHK(hipMemsetAsync(d->d_cap, 0, 4, h->stream));
   HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
   if (int r = d->tr->max_i32(h, d->d_cap, d->vals + par * W, seq)) return r;
-  // cap and the error word back in one synchronisation (pinned staging in the status block)
-  int32_t* hv = reinterpret_cast<int32_t*>(h->h_status + 8);
-  HIPCHK(hipMemcpyAsync(hv, d->d_cap, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipMemcpyAsync(hv + 1, h->d_err, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  // cap and the error word back in one wait: a tiny kernel writes them and then a sequence
+  // number into the mapped status block, and the host spins on that number
+  volatile int32_t* hv = reinterpret_cast<volatile int32_t*>(h->h_status + 8);
+  const uint64_t cseq = ++h->status_seq;
+  HIPCHK(pair_out(d->d_cap, h->d_err, h->h_status_dev + 8, h->h_status_dev + kSeqCapOff, cseq, h->stream));
+  if (int r = wait_mapped_seq(h, kSeqCapOff, cseq)) return r;
   int32_t cap = hv[0];
   if (hv[1]) {
     if (int r = check_err_flag(h)) return r;

@@ -137,5 +137,13 @@ int read_loss(bprmf_handle* h, double* loss);
 int loss_zero_slots(bprmf_handle* h);
 int begin_call(bprmf_handle* h);
 int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps);
+// mapped status block: byte offsets of the two call sequence words (end_call, the sharded
+// runner's capacity read-back)
+constexpr size_t kSeqEndOff = 16 + sizeof(double) * kLossSlots;
+constexpr size_t kSeqCapOff = kSeqEndOff + 8;
+// spin until a kernel has stored seq into the mapped word at byte offset `off` of h_status (a
+// blocking stream sync wakes up tens of microseconds later); synchronise the stream instead if
+// it ends or fails without that store
+int wait_mapped_seq(bprmf_handle* h, size_t off, uint64_t seq);
 
 }  // namespace bprmf

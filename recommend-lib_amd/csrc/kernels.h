@@ -114,6 +114,9 @@ hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, doub
 hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s,
                       void* seq_dev = nullptr, uint64_t seq = 0);
 hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s);
+// a[0] and b[0] into mapped host memory dst[0..1], then seq into seq_dev (mapped)
+hipError_t pair_out(const int32_t* a, const int32_t* b, void* dst_dev, void* seq_dev, uint64_t seq,
+                    hipStream_t s);
 hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
                        uint32_t table_tag, int world, int rank, hipStream_t s);
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,

@@ -378,6 +378,23 @@ hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, doub
   return hipGetLastError();
 }
 
+// two int32 device words (a[0], b[0]) into mapped host memory dst[0..1], then seq (as k_status_out)
+__global__ void k_pair_out(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int32_t* dst,
+                           uint64_t* seq_dst, uint64_t seq) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(dst, *a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, *b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(seq_dst, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t pair_out(const int32_t* a, const int32_t* b, void* dst_dev, void* seq_dev, uint64_t seq,
+                    hipStream_t s) {
+  k_pair_out<<<1, 64, 0, s>>>(a, b, static_cast<int32_t*>(dst_dev), static_cast<uint64_t*>(seq_dev), seq);
+  return hipGetLastError();
+}
+
 hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s,
                       void* seq_dev, uint64_t seq) {
   if (words > 64) return hipErrorInvalidValue;

@@ -1,5 +1,6 @@
-"""GPU-side timeline of the last library call in a rocprofv3 kernel trace (from its k_set_cursor
-launch on): start, duration and the gap before each kernel, in microseconds.
+"""GPU-side timeline of the last library call in a rocprofv3 kernel trace (from its sampler or,
+without one, its batch-builder launch on): start, duration and the gap before each kernel, in
+microseconds.
 
   python tools/trace_call.py gpurun_out/<tag>/prof/run_kernel_trace.csv
 """
@@ -7,7 +8,10 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-first = [k for k, r in enumerate(rows) if "k_set_cursor" in r["Kernel_Name"]][-1]
+starts = [k for k, r in enumerate(rows) if "k_build_batches" in r["Kernel_Name"]]
+first = starts[-1]
+if first > 0 and "k_sample" in rows[first - 1]["Kernel_Name"]:
+    first -= 1
 t0 = prev = int(rows[first]["Start_Timestamp"])
 for r in rows[first:]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

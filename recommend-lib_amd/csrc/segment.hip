@@ -282,37 +282,47 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     s_j[p] = my_j[k];
     if (key[k] != kNone) heads += (p == 0 || s_key[p - 1] != key[k]);
   }
-  int seg0 = 0, n_useg = 0, vpre = 0, nvalid = 0;
-  Scan().exclusive_scan(heads, seg0, 0, n_useg, sscan, rocprim::plus<int>());
+  // one scan for both counts: segment heads in the high half, valid triplets in the low
+  int pre = 0, tot = 0;
+  Scan().exclusive_scan((heads << 16) | valid, pre, 0, tot, sscan, rocprim::plus<int>());
+  const int seg0 = pre >> 16, n_useg = tot >> 16, nvalid = tot & 0xFFFF;
+  // segment starts in LDS (the upper half of the sort scratch, free after the user sort), so each
+  // position finds its segment's bounds with two reads instead of scanning its neighbours
+  int32_t* s_seg = reinterpret_cast<int32_t*>(s_sort) + T * IPT;
+  {
+    int s = seg0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
+      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) {
+        v.useg[s] = p;
+        s_seg[s++] = p;
+      }
+    }
+  }
   __syncthreads();
-  Scan().exclusive_scan(valid, vpre, 0, nvalid, sscan, rocprim::plus<int>());
   bool uhead[IPT];
-  int uend[IPT];  // a head's segment end (users repeat a few times per batch at most)
+  int uend[IPT];  // a head's segment end
   // trec.w: 1 = the user's only triplet; >= 2 = head of a segment of that length that lies in one
   // K1 workgroup (tpb consecutive positions: K1 sums it in LDS and updates the user); -1 = another
   // member of such a segment; 0 = a segment across workgroups (K2 sums its ugrad rows, mrec)
   int uw[IPT];
   {
-    int s = seg0;
+    int s = seg0 - 1;  // segment of this thread's first position if that is not a head
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
       uhead[k] = key[k] != kNone && (p == 0 || s_key[p - 1] != key[k]);
       uend[k] = p + 1;
       uw[k] = 0;
-      if (uhead[k]) {
-        v.useg[s++] = p;
-        while (uend[k] < nvalid && s_key[uend[k]] == key[k]) ++uend[k];
-      }
-      if (key[k] != kNone) {  // this position's segment, searched at most tpb positions each way
-        int b = p, e = p + 1;
-        while (b > 0 && p - b < tpb && s_key[b - 1] == key[k]) --b;
-        while (e < nvalid && e - p < tpb && s_key[e] == key[k]) ++e;
-        const bool whole = !(b > 0 && s_key[b - 1] == key[k]) && !(e < nvalid && s_key[e] == key[k]);
+      if (key[k] != kNone) {
+        if (uhead[k]) ++s;
+        const int b = s_seg[s], e = s + 1 < n_useg ? s_seg[s + 1] : nvalid;
+        uend[k] = e;
         const int len = e - b;
         if (len == 1)
           uw[k] = 1;
-        else if (whole && b / tpb == (e - 1) / tpb)
+        else if (b / tpb == (e - 1) / tpb)
           uw[k] = p == b ? len : -1;
       }
     }

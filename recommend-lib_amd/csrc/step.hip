@@ -75,6 +75,14 @@ static __device__ __forceinline__ void st4o(float* p, float4 v) {
     *reinterpret_cast<float4*>(p) = v;
   }
 }
+// a 4-byte word the next kernel reads: write-through (sc1) like st4o, so it leaves no dirty line
+template <bool WT>
+static __device__ __forceinline__ void st_word(int32_t* p, int32_t v) {
+  if constexpr (WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
 static __device__ __forceinline__ float4 scale4(float4 a, float s) {
   return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }
@@ -231,7 +239,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     const float x = di - dj;
     SSTAMP(0, 2);
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
-    if (sub == 0 && xloss) xloss[p] = x;  // K2 sums the loss terms
+    if (sub == 0 && xloss) st_word<WT>(reinterpret_cast<int32_t*>(xloss) + p, __float_as_int(x));  // K2 sums the loss terms
     float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
     for (int k = 0; k < S; ++k) st4o<WT>(cb + 4 * G4 * k, scale4(pu[k], c));
@@ -239,7 +247,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
 #pragma unroll
       for (int k = 0; k < S; ++k)
         st4o<WT>(prow + 4 * G4 * k, sgd4(pu[k], scale4(sub4(vi[k], vj[k]), -c), hp.lr, hp.wd));
-      if (sub == 0) P.stamp[u] = t;
+      if (sub == 0) st_word<WT>(P.stamp + u, t);
     } else if (w == 0) {  // a segment across workgroups: K2 sums its gradients in position order
       float* ub = ugrad + (int64_t)p * ld + 4 * sub;
 #pragma unroll
@@ -264,7 +272,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       }
       st4o<WT>(prow + 4 * G4 * k, sgd4(pu[k], g, hp.lr, hp.wd));
     }
-    if (sub == 0) P.stamp[u] = t;
+    if (sub == 0) st_word<WT>(P.stamp + u, t);
   }
   SSTAMP(0, 3);
 }

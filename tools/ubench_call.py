@@ -56,6 +56,8 @@ for c in range(N):
     first = e * n_steps + s + K
 w = np.array(walls[5:]) * 1e6 / K
 i = np.array(inner[5:]) * 1e6 / K
-print(json.dumps({"steps_per_call": K, "calls": len(w), "us_per_step_median": round(float(np.median(w)), 3),
+first_calls = [round(x * 1e6 / K, 2) for x in walls[:6]]
+print(json.dumps({"steps_per_call": K, "calls": len(w), "first_calls_us_per_step": first_calls,
+                  "us_per_step_median": round(float(np.median(w)), 3),
                   "us_per_step_min": round(float(w.min()), 3),
                   "library_us_per_step_median": round(float(np.median(i)), 3)}))

@@ -43,26 +43,30 @@ void oracle_philox(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out
   memcpy(out, c, sizeof c);
 }
 
+/* domain bits b >= 2 with 2^b >= n */
 int oracle_feistel_bits(uint64_t n) {
-  int h = 1;
-  while (h < 32 && (1ull << (2 * h)) < n) ++h;
-  return h;
+  int b = 2;
+  while (b < 63 && (1ull << b) < n) ++b;
+  return b;
 }
 
+/* 6-round alternating Feistel on b bits (left ceil(b/2) high bits, right floor(b/2) low bits;
+   even rounds L ^= F(R), odd rounds R ^= F(L)), cycle-walking into [0, n) */
 uint64_t oracle_permute(uint64_t x, uint64_t n, uint64_t seed, uint32_t epoch) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const int h = oracle_feistel_bits(n);
-  const uint64_t mask = (h >= 32) ? 0xFFFFFFFFull : ((1ull << h) - 1);
+  const int b = oracle_feistel_bits(n), hr = b >> 1, hl = b - hr;
+  const uint64_t mr = (1ull << hr) - 1, ml = (1ull << hl) - 1;
   do {
-    uint64_t L = x >> h, R = x & mask;
+    uint64_t L = x >> hr, R = x & mr;
     for (uint32_t r = 0; r < 6; ++r) {
-      uint32_t c[4] = {(uint32_t)R, r, epoch, TAG_PERM | r};
+      uint32_t c[4] = {(uint32_t)((r & 1) ? L : R), r, epoch, TAG_PERM | r};
       philox(c, k0, k1);
-      uint64_t nl = R;
-      R = L ^ ((uint64_t)c[0] & mask);
-      L = nl;
+      if (r & 1)
+        R ^= (uint64_t)c[0] & mr;
+      else
+        L ^= (uint64_t)c[0] & ml;
     }
-    x = (L << h) | R;
+    x = (L << hr) | R;
   } while (x >= n);
   return x;
 }

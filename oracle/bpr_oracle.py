@@ -105,28 +105,39 @@ def _seed_key(seed):
 
 
 def feistel_bits(n):
-    """Half-width h of the balanced Feistel domain [0, 4^h) >= n (h >= 1)."""
-    h = 1
-    while (1 << (2 * h)) < n:
-        h += 1
-    return h
+    """Domain bits b >= 2 of the Feistel permutation: the smallest with 2^b >= n."""
+    b = 2
+    while (1 << b) < n:
+        b += 1
+    return b
 
 
 def permute(q, n, seed, epoch):
-    """Keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle-walking."""
+    """Keyed bijection of [0,n): 6-round alternating Feistel on b bits + cycle-walking.
+
+    Left half = the ceil(b/2) high bits, right half = the floor(b/2) low bits; even rounds
+    L ^= F(R), odd rounds R ^= F(L), F = Philox4x32-10 word 0 of (half, round, epoch, tag|round)."""
     k0, k1 = _seed_key(seed)
-    h = feistel_bits(n)
-    mask = np.uint64((1 << h) - 1)
+    b = feistel_bits(n)
+    hr = b >> 1
+    hl = b - hr
+    mr = np.uint64((1 << hr) - 1)
+    ml = np.uint64((1 << hl) - 1)
     x = np.asarray(q, dtype=np.uint64).copy()
     todo = np.ones(x.shape, dtype=bool)
     while todo.any():
         y = x[todo]
-        L = y >> np.uint64(h)
-        R = y & mask
+        L = y >> np.uint64(hr)
+        R = y & mr
         for r in range(FEISTEL_ROUNDS):
-            f = philox4x32_10(R, np.uint64(r), np.uint64(epoch), np.uint64(TAG_PERM | r), k0, k1)[0]
-            L, R = R, (L ^ (f & mask))
-        y = (L << np.uint64(h)) | R
+            src = L if r & 1 else R
+            f = philox4x32_10(src & np.uint64(0xFFFFFFFF), np.uint64(r), np.uint64(epoch),
+                              np.uint64(TAG_PERM | r), k0, k1)[0]
+            if r & 1:
+                R = R ^ (f & mr)
+            else:
+                L = L ^ (f & ml)
+        y = (L << np.uint64(hr)) | R
         x[todo] = y
         todo[todo] = y >= np.uint64(n)
     return x.astype(np.int64)

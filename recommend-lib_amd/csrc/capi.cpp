@@ -297,9 +297,7 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
     HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
   h->npos = n;
   const uint64_t N = (uint64_t)n * (uint64_t)h->cfg.num_ng;
-  int hb = 1;
-  while (hb < 32 && (1ull << (2 * hb)) < N) ++hb;
-  h->feistel_h = hb;
+  h->feistel_h = feistel_domain_bits(N);
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
   // the first calls (a larger chunk later would reallocate and recapture)
   if (seg_mode(h)) {

@@ -36,21 +36,27 @@ static __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint
   }
 }
 
-// keyed bijection of [0, n): balanced Feistel on 2h bits, cycle-walking back into range.
-static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int h, uint32_t k0, uint32_t k1,
+// keyed bijection of [0, n): a 6-round alternating Feistel network on the b = ceil(log2 n) bits
+// of x (left half ceil(b/2) high bits, right half floor(b/2) low bits; even rounds L ^= F(R), odd
+// rounds R ^= F(L), F = Philox keyed by the seed and tagged by round and epoch), cycle-walking
+// back into range.  The domain 2^b is < 2n, so a walk takes < 2 rounds on average and its tail
+// is short (a balanced network on 4^h >= n could be up to 4n: ~2 passes on average at ml-20m).
+static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int b, uint32_t k0, uint32_t k1,
                                             uint32_t epoch) {
-  const uint64_t mask = (h >= 32) ? 0xFFFFFFFFull : ((1ull << h) - 1);
+  const int hr = b >> 1, hl = b - hr;
+  const uint64_t mr = (1ull << hr) - 1, ml = (1ull << hl) - 1;
   do {
-    uint64_t L = x >> h, R = x & mask;
+    uint64_t L = x >> hr, R = x & mr;
 #pragma unroll
     for (uint32_t r = 0; r < 6; ++r) {
-      uint32_t c0 = (uint32_t)R, c1 = r, c2 = epoch, c3 = TAG_PERM | r;
+      uint32_t c0 = (uint32_t)((r & 1) ? L : R), c1 = r, c2 = epoch, c3 = TAG_PERM | r;
       philox10(c0, c1, c2, c3, k0, k1);
-      const uint64_t nl = R;
-      R = L ^ ((uint64_t)c0 & mask);
-      L = nl;
+      if (r & 1)
+        R ^= (uint64_t)c0 & mr;
+      else
+        L ^= (uint64_t)c0 & ml;
     }
-    x = (L << h) | R;
+    x = (L << hr) | R;
   } while (x >= n);
   return x;
 }

@@ -93,13 +93,21 @@ struct Hyper {
   double log2a;  // log2(alpha): decay over k steps = exp2(k * log2a)
 };
 
+// domain bits of the sampler's Feistel permutation (device_common.h permute) for n triplets: the
+// smallest b >= 2 with 2^b >= n
+inline int feistel_domain_bits(uint64_t n) {
+  int b = 2;
+  while (b < 63 && (1ull << b) < n) ++b;
+  return b;
+}
+
 struct SamplerArgs {
   const int32_t* pos_u;   // [npos] global user id, features order
   const int32_t* pos_i;   // [npos] global item id
   const int64_t* indptr;  // [local_users+1]
   const int32_t* indices; // sorted positives per local user
   int64_t npos, item_num;
-  int32_t num_ng, world, feistel_h;
+  int32_t num_ng, world, feistel_h;  // feistel_h: permute's domain bits (feistel_domain_bits)
   uint32_t k0, k1;        // Philox key (shard seed)
 };
 

@@ -463,9 +463,7 @@ int ncf_set_train(ncf_handle* h, const int32_t* users, const int32_t* items, int
     HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
   h->npos = nnz;
   const uint64_t N = (uint64_t)nnz * (uint64_t)(1 + h->cfg.num_ng);
-  int hb = 1;
-  while (hb < 32 && (1ull << (2 * hb)) < N) ++hb;
-  h->feistel_h = hb;
+  h->feistel_h = feistel_domain_bits(N);
   return 0;
 }
 

@@ -43,30 +43,37 @@ void oracle_philox(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out
   memcpy(out, c, sizeof c);
 }
 
-/* domain bits b >= 2 with 2^b >= n */
-int oracle_feistel_bits(uint64_t n) {
-  int b = 2;
-  while (b < 63 && (1ull << b) < n) ++b;
-  return b;
+/* domain Z_a x Z_c: c = ceil(sqrt(n)), a = ceil(n / c) */
+void oracle_feistel_dims(uint64_t n, uint32_t* a, uint32_t* c) {
+  if (n <= 1) {
+    *a = *c = 1;
+    return;
+  }
+  uint64_t r = (uint64_t)sqrtl((long double)n);
+  while (r * r > n) --r;
+  while ((r + 1) * (r + 1) <= n) ++r;
+  const uint64_t cc = r * r == n ? r : r + 1;
+  *c = (uint32_t)cc;
+  *a = (uint32_t)((n + cc - 1) / cc);
 }
 
-/* 6-round alternating Feistel on b bits (left ceil(b/2) high bits, right floor(b/2) low bits;
-   even rounds L ^= F(R), odd rounds R ^= F(L)), cycle-walking into [0, n) */
+/* 6-round alternating Feistel on Z_a x Z_c (x = L*c + R; even rounds L = (L + hi32(F(R)*a)) mod a,
+   odd rounds R = (R + hi32(F(L)*c)) mod c), cycle-walking into [0, n) */
 uint64_t oracle_permute(uint64_t x, uint64_t n, uint64_t seed, uint32_t epoch) {
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const int b = oracle_feistel_bits(n), hr = b >> 1, hl = b - hr;
-  const uint64_t mr = (1ull << hr) - 1, ml = (1ull << hl) - 1;
+  uint32_t fa, fc;
+  oracle_feistel_dims(n, &fa, &fc);
   do {
-    uint64_t L = x >> hr, R = x & mr;
+    uint64_t L = x / fc, R = x % fc;
     for (uint32_t r = 0; r < 6; ++r) {
       uint32_t c[4] = {(uint32_t)((r & 1) ? L : R), r, epoch, TAG_PERM | r};
       philox(c, k0, k1);
       if (r & 1)
-        R ^= (uint64_t)c[0] & mr;
+        R = (R + (((uint64_t)c[0] * fc) >> 32)) % fc;
       else
-        L ^= (uint64_t)c[0] & ml;
+        L = (L + (((uint64_t)c[0] * fa) >> 32)) % fa;
     }
-    x = (L << hr) | R;
+    x = L * fc + R;
   } while (x >= n);
   return x;
 }

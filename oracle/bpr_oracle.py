@@ -27,6 +27,8 @@ Two parts:
    This module restates that spec independently of the HIP code; GPU output must match it bit-for-bit.
    Distributional parity with the reference sampler is pinned by tests/golden/ng_sample_ml100k.npz (F3).
 """
+import math
+
 import numpy as np
 
 # ----------------------------------------------------------------------------------------------
@@ -104,40 +106,40 @@ def _seed_key(seed):
     return seed & 0xFFFFFFFF, seed >> 32
 
 
-def feistel_bits(n):
-    """Domain bits b >= 2 of the Feistel permutation: the smallest with 2^b >= n."""
-    b = 2
-    while (1 << b) < n:
-        b += 1
-    return b
+def feistel_dims(n):
+    """Domain Z_a x Z_c of the Feistel permutation: c = ceil(sqrt(n)), a = ceil(n / c)."""
+    n = int(n)
+    if n <= 1:
+        return 1, 1
+    c = math.isqrt(n)
+    if c * c < n:
+        c += 1
+    return (n + c - 1) // c, c
 
 
 def permute(q, n, seed, epoch):
-    """Keyed bijection of [0,n): 6-round alternating Feistel on b bits + cycle-walking.
+    """Keyed bijection of [0,n): 6-round alternating Feistel on Z_a x Z_c + cycle-walking.
 
-    Left half = the ceil(b/2) high bits, right half = the floor(b/2) low bits; even rounds
-    L ^= F(R), odd rounds R ^= F(L), F = Philox4x32-10 word 0 of (half, round, epoch, tag|round)."""
+    x = L*c + R (feistel_dims); even rounds L = (L + (F(R)*a >> 32)) mod a, odd rounds
+    R = (R + (F(L)*c >> 32)) mod c, F = Philox4x32-10 word 0 of (half, round, epoch, tag|round)."""
     k0, k1 = _seed_key(seed)
-    b = feistel_bits(n)
-    hr = b >> 1
-    hl = b - hr
-    mr = np.uint64((1 << hr) - 1)
-    ml = np.uint64((1 << hl) - 1)
+    fa, fc = feistel_dims(n)
+    ua, uc = np.uint64(fa), np.uint64(fc)
     x = np.asarray(q, dtype=np.uint64).copy()
     todo = np.ones(x.shape, dtype=bool)
     while todo.any():
         y = x[todo]
-        L = y >> np.uint64(hr)
-        R = y & mr
+        L = y // uc
+        R = y % uc
         for r in range(FEISTEL_ROUNDS):
             src = L if r & 1 else R
             f = philox4x32_10(src & np.uint64(0xFFFFFFFF), np.uint64(r), np.uint64(epoch),
                               np.uint64(TAG_PERM | r), k0, k1)[0]
             if r & 1:
-                R = R ^ (f & mr)
+                R = (R + ((f * uc) >> np.uint64(32))) % uc
             else:
-                L = L ^ (f & ml)
-        y = (L << np.uint64(hr)) | R
+                L = (L + ((f * ua) >> np.uint64(32))) % ua
+        y = L * uc + R
         x[todo] = y
         todo[todo] = y >= np.uint64(n)
     return x.astype(np.int64)

@@ -297,7 +297,7 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
     HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
   h->npos = n;
   const uint64_t N = (uint64_t)n * (uint64_t)h->cfg.num_ng;
-  h->feistel_h = feistel_domain_bits(N);
+  feistel_dims(N, &h->feistel_a, &h->feistel_c);
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
   // the first calls (a larger chunk later would reallocate and recapture)
   if (seg_mode(h)) {
@@ -332,7 +332,8 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   a.item_num = h->cfg.item_num;
   a.num_ng = h->cfg.num_ng;
   a.world = h->cfg.world;
-  a.feistel_h = h->feistel_h;
+  a.feistel_a = h->feistel_a;
+  a.feistel_c = h->feistel_c;
   a.k0 = h->k0;
   a.k1 = h->k1;
   return a;

@@ -36,41 +36,66 @@ static __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint
   }
 }
 
-// keyed bijection of [0, n): a 6-round alternating Feistel network on the b = ceil(log2 n) bits
-// of x (left half ceil(b/2) high bits, right half floor(b/2) low bits; even rounds L ^= F(R), odd
-// rounds R ^= F(L), F = Philox keyed by the seed and tagged by round and epoch), cycle-walking
-// back into range.  The domain 2^b is < 2n, so a walk takes < 2 rounds on average and its tail
-// is short (a balanced network on 4^h >= n could be up to 4n: ~2 passes on average at ml-20m).
-static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, int b, uint32_t k0, uint32_t k1,
-                                            uint32_t epoch) {
-  const int hr = b >> 1, hl = b - hr;
-  const uint64_t mr = (1ull << hr) - 1, ml = (1ull << hl) - 1;
+// keyed bijection of [0, n): a 6-round alternating Feistel network on Z_a x Z_c (x = L*c + R,
+// c = ceil(sqrt(n)), a = ceil(n/c); feistel_dims), F = Philox keyed by the seed and tagged by
+// round and epoch: even rounds L = (L + hi32(F(R)*a)) mod a, odd rounds R = (R + hi32(F(L)*c))
+// mod c; cycle-walking back into [0, n).  a*c - n < c, so a walk is needed with probability below
+// 1/sqrt(n) (a power-of-two domain 2^b < 2n made ~86 % of 64-lane waves run a second pass at
+// ml-20m, and the wave waits for its slowest lane).
+static __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, uint32_t fa, uint32_t fc,
+                                                   uint32_t k0, uint32_t k1, uint32_t epoch) {
   do {
-    uint64_t L = x >> hr, R = x & mr;
+    uint32_t L, R;
+    if (x >> 32) {
+      L = (uint32_t)(x / fc);
+      R = (uint32_t)(x - (uint64_t)L * fc);
+    } else {
+      L = (uint32_t)x / fc;
+      R = (uint32_t)x - L * fc;
+    }
 #pragma unroll
     for (uint32_t r = 0; r < 6; ++r) {
-      uint32_t c0 = (uint32_t)((r & 1) ? L : R), c1 = r, c2 = epoch, c3 = TAG_PERM | r;
+      uint32_t c0 = (r & 1) ? L : R, c1 = r, c2 = epoch, c3 = TAG_PERM | r;
       philox10(c0, c1, c2, c3, k0, k1);
-      if (r & 1)
-        R ^= (uint64_t)c0 & mr;
-      else
-        L ^= (uint64_t)c0 & ml;
+      if (r & 1) {
+        R += __umulhi(c0, fc);
+        if (R >= fc) R -= fc;
+      } else {
+        L += __umulhi(c0, fa);
+        if (L >= fa) L -= fa;
+      }
     }
-    x = (L << hr) | R;
+    x = (uint64_t)L * fc + R;
   } while (x >= n);
   return x;
 }
 
 // unbiased Lemire reduction into [0, n), n >= 1; retries draw fresh counters (attempt in tag).
+// Split in two so a caller can draw attempt 0 (bounded_draw0: depends on q only) while the loads
+// that give n are in flight, then finish with bounded_from.
+static __device__ __forceinline__ uint32_t bounded_draw(uint64_t q, uint32_t epoch, uint32_t att,
+                                                        uint32_t k0, uint32_t k1) {
+  uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = epoch, c3 = TAG_NEG | att;
+  philox10(c0, c1, c2, c3, k0, k1);
+  return c0;
+}
+static __device__ __forceinline__ uint32_t bounded_draw0(uint64_t q, uint32_t epoch, uint32_t k0,
+                                                         uint32_t k1) {
+  return bounded_draw(q, epoch, 0, k0, k1);
+}
+static __device__ __forceinline__ uint32_t bounded_from(uint32_t d0, uint64_t q, uint32_t epoch,
+                                                        uint32_t n, uint32_t k0, uint32_t k1) {
+  const uint32_t thresh = (0u - n) % n;  // (2^32 - n) mod n in 32-bit arithmetic
+  uint32_t d = d0;
+  for (uint32_t a = 1;; ++a) {
+    const uint64_t m = (uint64_t)d * n;
+    if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
+    d = bounded_draw(q, epoch, a, k0, k1);
+  }
+}
 static __device__ __forceinline__ uint32_t bounded(uint64_t q, uint32_t epoch, uint32_t n, uint32_t k0,
                                             uint32_t k1) {
-  const uint32_t thresh = (0u - n) % n;  // (2^32 - n) mod n in 32-bit arithmetic
-  for (uint32_t a = 0;; ++a) {
-    uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32), c2 = epoch, c3 = TAG_NEG | a;
-    philox10(c0, c1, c2, c3, k0, k1);
-    const uint64_t m = (uint64_t)c0 * n;
-    if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
-  }
+  return bounded_from(bounded_draw0(q, epoch, k0, k1), q, epoch, n, k0, k1);
 }
 
 // q / d for the sampler's triplet -> positive map: 32-bit division when q fits (the usual case)

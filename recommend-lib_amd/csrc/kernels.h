@@ -2,6 +2,7 @@
 // Internal to libbprmf_amd.so; the public ABI is include/bprmf.h.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 namespace bprmf {
@@ -93,12 +94,19 @@ struct Hyper {
   double log2a;  // log2(alpha): decay over k steps = exp2(k * log2a)
 };
 
-// domain bits of the sampler's Feistel permutation (device_common.h permute) for n triplets: the
-// smallest b >= 2 with 2^b >= n
-inline int feistel_domain_bits(uint64_t n) {
-  int b = 2;
-  while (b < 63 && (1ull << b) < n) ++b;
-  return b;
+// domain Z_a x Z_c of the sampler's Feistel permutation (device_common.h permute) for n items:
+// c = ceil(sqrt(n)), a = ceil(n / c), so a*c >= n and a*c - n < c
+inline void feistel_dims(uint64_t n, uint32_t* a, uint32_t* c) {
+  if (n <= 1) {
+    *a = *c = 1;
+    return;
+  }
+  uint64_t r = (uint64_t)sqrt((double)n);
+  while (r * r > n) --r;
+  while ((r + 1) * (r + 1) <= n) ++r;  // r = isqrt(n)
+  const uint64_t cc = r * r == n ? r : r + 1;
+  *c = (uint32_t)cc;
+  *a = (uint32_t)((n + cc - 1) / cc);
 }
 
 struct SamplerArgs {
@@ -107,7 +115,8 @@ struct SamplerArgs {
   const int64_t* indptr;  // [local_users+1]
   const int32_t* indices; // sorted positives per local user
   int64_t npos, item_num;
-  int32_t num_ng, world, feistel_h;  // feistel_h: permute's domain bits (feistel_domain_bits)
+  int32_t num_ng, world;
+  uint32_t feistel_a, feistel_c;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0, k1;        // Philox key (shard seed)
 };
 

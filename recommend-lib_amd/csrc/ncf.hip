@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) void k_ncf_sample(SamplerArgs a, uint32_t epoc
   const uint64_t npos = (uint64_t)a.npos, N = npos * (uint64_t)(1 + a.num_ng);
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count;
        s += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t q = permute((uint64_t)(first + s), N, a.feistel_h, a.k0, a.k1, epoch);
+    const uint64_t q = permute((uint64_t)(first + s), N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
     if (q < npos) {
       ou[s] = a.pos_u[q];
       oi[s] = a.pos_i[q];

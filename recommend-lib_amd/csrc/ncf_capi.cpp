@@ -43,7 +43,7 @@ struct ncf_handle {
   int64_t npos = 0;
   int32_t *d_pos_u = nullptr, *d_pos_i = nullptr, *d_indices = nullptr;
   int64_t* d_indptr = nullptr;
-  int feistel_h = 1;
+  uint32_t feistel_a = 1, feistel_c = 1;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0 = 0, k1 = 0;
   // sample chunk
   int32_t *d_u = nullptr, *d_i = nullptr;
@@ -140,7 +140,8 @@ static SamplerArgs ncf_sampler(ncf_handle* h) {
   a.item_num = h->cfg.item_num;
   a.num_ng = h->cfg.num_ng;
   a.world = 1;
-  a.feistel_h = h->feistel_h;
+  a.feistel_a = h->feistel_a;
+  a.feistel_c = h->feistel_c;
   a.k0 = h->k0;
   a.k1 = h->k1;
   return a;
@@ -463,7 +464,7 @@ int ncf_set_train(ncf_handle* h, const int32_t* users, const int32_t* items, int
     HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
   h->npos = nnz;
   const uint64_t N = (uint64_t)nnz * (uint64_t)(1 + h->cfg.num_ng);
-  h->feistel_h = feistel_domain_bits(N);
+  feistel_dims(N, &h->feistel_a, &h->feistel_c);
   return 0;
 }
 

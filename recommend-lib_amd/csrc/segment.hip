@@ -227,15 +227,16 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         i = ri[b0 + p];
         j = rj[b0 + p];
       } else {
-        const uint64_t q = permute((uint64_t)(first_slot + b0 + p), N, a.feistel_h, a.k0, a.k1, epoch);
+        const uint64_t q = permute((uint64_t)(first_slot + b0 + p), N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
         const int64_t pp = div_small(q, (uint32_t)a.num_ng);
         const int64_t ul = a.pos_u[pp] / a.world;
         i = a.pos_i[pp];
+        const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
         const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
         const int64_t nfree = a.item_num - deg;
         j = -1;
         if (nfree > 0) {
-          const uint32_t kk = bounded(q, epoch, (uint32_t)nfree, a.k0, a.k1);
+          const uint32_t kk = bounded_from(d0, q, epoch, (uint32_t)nfree, a.k0, a.k1);
           j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)kk);
         } else {
           sampled_ok = false;

@@ -67,6 +67,16 @@ def test_permutation_is_bijection(n):
         assert C.lib().oracle_permute(s, n, 987654321, 7) == q[s]
 
 
+@pytest.mark.parametrize("n", [2, 3, 15, 16, 17, 32_557_604, 548_000_000, 10**12 + 7])
+def test_feistel_domain_is_tight(n):
+    # Z_a x Z_c covers [0, n) with fewer than c extra points: a walk past n is rare (< 1/sqrt(n))
+    a, c = O.feistel_dims(n)
+    assert a * c >= n and a * c - n < c and (c - 1) ** 2 < n <= c * c
+    x = np.arange(min(n, 200_000), dtype=np.int64) * (n // min(n, 200_000))
+    q = O.permute(x, n, 11, 3)
+    assert (q >= 0).all() and (q < n).all() and len(np.unique(q)) == len(q)
+
+
 def test_kth_nonmember_bruteforce():
     g = np.random.default_rng(3)
     I = 50

@@ -41,8 +41,21 @@ pos = syn.make_positives(U, I, 10_000_000, 20260101)
 m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=20260101, device=0)
 m.set_train(pos)
 n_steps = m.epoch_size()[1]
-m.train_steps(0, 0, 5)
-first, walls, inner = 5, [], []
+W = int(os.environ.get("UB_WARM", "5"))
+if os.environ.get("UB_WARM_SPLIT"):  # the same W warm-up steps as two calls
+    m.train_steps(0, 0, W // 2)
+    m.train_steps(0, W // 2, W - W // 2)
+else:
+    m.train_steps(0, 0, W)
+first, walls, inner = W, [], []
+if os.environ.get("UB_SPIN"):  # busy the GPU for ~UB_SPIN ms of unrelated work before the first call
+    x = torch.randn(2048, 2048, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < float(os.environ["UB_SPIN"]) * 1e-3:
+        x = x @ x
+        x = x / x.norm()
+        torch.cuda.synchronize()
 for c in range(N):
     e, s = divmod(first, n_steps)
     if s + K > n_steps:
@@ -57,7 +70,9 @@ for c in range(N):
 w = np.array(walls[5:]) * 1e6 / K
 i = np.array(inner[5:]) * 1e6 / K
 first_calls = [round(x * 1e6 / K, 2) for x in walls[:6]]
+first_inner = [round(x * 1e6 / K, 2) for x in inner[:6]]
 print(json.dumps({"steps_per_call": K, "calls": len(w), "first_calls_us_per_step": first_calls,
+                  "first_calls_library_us_per_step": first_inner,
                   "us_per_step_median": round(float(np.median(w)), 3),
                   "us_per_step_min": round(float(w.min()), 3),
                   "library_us_per_step_median": round(float(np.median(i)), 3)}))

@@ -200,14 +200,24 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     }
     bool wi = false, wj = false, wu = false;
     const int32_t tp = t - 1;
+    int32_t si = 0, sj = 0, su0 = 0;  // WAIT: the three stamps, loaded beside the marks
     if (WAIT) {
+      // marks and stamps in ONE round of loads (sc1 stamps: the first poll of a marked row); a
+      // marked row whose stamp is not yet tp is then polled alone, so a triplet with two or three
+      // rows already published pays one load latency here instead of one per row
       const int64_t o = (int64_t)(tp & 1);
-      wi = sb.pend_q[o * sb.qrows + i] == tp;
-      wj = sb.pend_q[o * sb.qrows + j] == tp;
-      wu = sb.pend_p[o * sb.prows + u] == tp;
-      if (wi) wait_stamp(Q.stamp + i, tp, err);
-      if (wj) wait_stamp(Q.stamp + j, tp, err);
-      if (wu) wait_stamp(P.stamp + u, tp, err);
+      const int32_t mi = sb.pend_q[o * sb.qrows + i], mj = sb.pend_q[o * sb.qrows + j];
+      const int32_t mu = sb.pend_p[o * sb.prows + u];
+      si = __hip_atomic_load(Q.stamp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sj = __hip_atomic_load(Q.stamp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      su0 = __hip_atomic_load(P.stamp + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wi = mi == tp;
+      wj = mj == tp;
+      wu = mu == tp;
+      if (wi && si != tp) wait_stamp(Q.stamp + i, tp, err);
+      if (wj && sj != tp) wait_stamp(Q.stamp + j, tp, err);
+      if (wu && su0 != tp) wait_stamp(P.stamp + u, tp, err);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the row loads stay after the stamp reads
     }
     SSTAMP(0, 4);
     const float* qbase = SH ? item_rows : Q.W;
@@ -221,9 +231,10 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4(qj + 4 * G4 * k);
     }
     // a row just published is current at tp (no pending decay); the others read their stamps
-    const int32_t su = wu ? tp : P.stamp[u];
-    const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wi ? tp : Q.stamp[i]));
-    const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wj ? tp : Q.stamp[j]));
+    // (WAIT: an unmarked row's stamp, read above, is stable in this launch)
+    const int32_t su = wu ? tp : (WAIT ? su0 : P.stamp[u]);
+    const float fi = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wi ? tp : (WAIT ? si : Q.stamp[i])));
+    const float fj = SH ? 1.f : decay_pow(hp.log2a, t - 1 - (wj ? tp : (WAIT ? sj : Q.stamp[j])));
     const float fu = decay_pow(hp.log2a, t - 1 - su);
     float di = 0.f, dj = 0.f;
 #pragma unroll

@@ -201,7 +201,19 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     bool wi = false, wj = false, wu = false;
     const int32_t tp = t - 1;
     int32_t si = 0, sj = 0, su0 = 0;  // WAIT: the three stamps, loaded beside the marks
+    const float* qbase = SH ? item_rows : Q.W;
+    const float* qi = qbase + (int64_t)i * ld + 4 * sub;
+    const float* qj = qbase + (int64_t)j * ld + 4 * sub;
+    float4 vi[S], vj[S];
     if (WAIT) {
+      // the rows too, speculatively in the same round: a row step t-1 does not update is final
+      // here; a marked one is read again (sc1) once its stamp says it is published
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        pu[k] = ld4(prow + 4 * G4 * k);
+        vi[k] = ld4(qi + 4 * G4 * k);
+        vj[k] = ld4(qj + 4 * G4 * k);
+      }
       // marks and stamps in ONE round of loads (sc1 stamps: the first poll of a marked row); a
       // marked row whose stamp is not yet tp is then polled alone, so a triplet with two or three
       // rows already published pays one load latency here instead of one per row
@@ -220,15 +232,20 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the row loads stay after the stamp reads
     }
     SSTAMP(0, 4);
-    const float* qbase = SH ? item_rows : Q.W;
-    const float* qi = qbase + (int64_t)i * ld + 4 * sub;
-    const float* qj = qbase + (int64_t)j * ld + 4 * sub;
-    float4 vi[S], vj[S];
+    if (WAIT) {
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
-      pu[k] = wu ? ld4_sc1(prow + 4 * G4 * k) : ld4(prow + 4 * G4 * k);
-      vi[k] = wi ? ld4_sc1(qi + 4 * G4 * k) : ld4(qi + 4 * G4 * k);
-      vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4(qj + 4 * G4 * k);
+      for (int k = 0; k < S; ++k) {
+        if (wu) pu[k] = ld4_sc1(prow + 4 * G4 * k);
+        if (wi) vi[k] = ld4_sc1(qi + 4 * G4 * k);
+        if (wj) vj[k] = ld4_sc1(qj + 4 * G4 * k);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        pu[k] = ld4(prow + 4 * G4 * k);
+        vi[k] = ld4(qi + 4 * G4 * k);
+        vj[k] = ld4(qj + 4 * G4 * k);
+      }
     }
     // a row just published is current at tp (no pending decay); the others read their stamps
     // (WAIT: an unmarked row's stamp, read above, is stable in this launch)

@@ -551,21 +551,24 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
 #pragma unroll
     for (int m = 0; m < kInlineRefs; ++m)
       if (m < len) acc_ref<S>(g, rows[m], rf[m]);
-  } else {  // lanes fetch G4 refs at once; rows requested 8 at a time before accumulating
+  } else {  // lanes fetch G4 refs at once; rows requested F at a time before accumulating
+    // (F = 16 at S = 1, as on the hot-item path: a 13..16-reference item, the slowest K2 lane
+    // groups, then needs one round of row loads instead of two; the order of the sum is the same)
+    constexpr int F = S == 1 ? 16 : 8;
     const int lane0 = (threadIdx.x & 63) - sub;
     for (int base = beg; base < end; base += G4) {
       const int32_t myref = base + sub < end ? bv.refs[base + sub] : 0;
       const int cnt = min(G4, end - base);
-      for (int m0 = 0; m0 < cnt; m0 += 8) {
-        float4 rows[8][S];
-        int32_t rf[8];
+      for (int m0 = 0; m0 < cnt; m0 += F) {
+        float4 rows[F][S];
+        int32_t rf[F];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
+        for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
           if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
+        for (int m = 0; m < F; ++m)
           if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
       }
     }

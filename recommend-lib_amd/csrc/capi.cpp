@@ -343,6 +343,23 @@ static double host_seconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// diagnostic (BPRMF_HOST_TRACE=1): host timestamps of the first calls' phases, to stderr
+static int g_trace_calls = -1;
+static double g_trace_t[8];
+static int g_trace_n = 0;
+static void trace_mark() {
+  if (g_trace_calls < 0) g_trace_calls = getenv("BPRMF_HOST_TRACE") ? 0 : 1 << 30;
+  if (g_trace_calls < 12 && g_trace_n < 8) g_trace_t[g_trace_n++] = host_seconds();
+}
+static void trace_flush() {
+  if (g_trace_calls >= 12 || g_trace_n == 0) return;
+  fprintf(stderr, "host trace call %d:", g_trace_calls);
+  for (int k = 1; k < g_trace_n; ++k) fprintf(stderr, " %.1f", (g_trace_t[k] - g_trace_t[0]) * 1e6);
+  fprintf(stderr, " us\n");
+  ++g_trace_calls;
+  g_trace_n = 0;
+}
+
 // sum of every per-wave loss slot (the Python-orchestrated sharded step)
 int bprmf::read_loss(bprmf_handle* h, double* loss) {
   HIPCHK(hipMemcpyAsync(h->h_status + 16, h->d_loss, sizeof(double) * kLossSlots,
@@ -651,9 +668,11 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
       int32_t* tu = h->d_trip;
       HIPCHK(sample(sampler_args(h), epoch, first_slot, n, tu, tu + h->trip_cap,
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
+      trace_mark();
       HIPCHK(build_batches(sampler_args(h), epoch, 0, n, (int)B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, 1, false, 0, nb, bb,
                            h->d_err, h->stream, k1_triplets_per_block(h->geom), ci));
+      trace_mark();
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,
                            h->cfg.item_num, 1, false, 0, nb, bb, h->d_err, h->stream,
@@ -720,12 +739,17 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   const int64_t B = h->cfg.batch_size;
   const int64_t chunk = chunk_triplets(h);
   const int64_t beg = first_step * B, end = std::min(N, (first_step + n_steps) * B);
+  trace_mark();
   if (int r = begin_call(h)) return r;
   int64_t steps = 0;
   for (int64_t off = beg; off < end; off += chunk)
     if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps))
       return r;
-  return end_call(h, st, end - beg, steps);
+  trace_mark();
+  const int rc_end = end_call(h, st, end - beg, steps);
+  trace_mark();
+  trace_flush();
+  return rc_end;
 }
 
 int bprmf_train_epoch(bprmf_handle* h, uint32_t epoch, bprmf_stats* st) {

@@ -75,6 +75,8 @@ def test_feistel_domain_is_tight(n):
     x = np.arange(min(n, 200_000), dtype=np.int64) * (n // min(n, 200_000))
     q = O.permute(x, n, 11, 3)
     assert (q >= 0).all() and (q < n).all() and len(np.unique(q)) == len(q)
+    for k in (0, len(x) // 2, len(x) - 1):  # the C restatement agrees at this size too
+        assert C.lib().oracle_permute(int(x[k]), n, 11, 3) == q[k]
 
 
 def test_kth_nonmember_bruteforce():

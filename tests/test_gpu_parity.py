@@ -202,6 +202,23 @@ def test_sampler_deep_lists_bit_exact(rl):
         assert np.array_equal(x, y)
 
 
+def test_sampler_bit_exact_bench_shape(rl):
+    """The bench workload's epoch (ml-20m shape, N ~ 3.3e7 slots, Feistel domain Z_a x Z_c):
+    slots at both ends of the epoch order equal the C oracle's."""
+    syn = __import__("importlib").import_module("recommend-lib_amd.synthetic")
+    U, I = 138493, 26744
+    pos = syn.make_positives(U, I, 10_000_000, 20261015)
+    m = _model(rl, U, I, 8, 4096, seed=20261015)
+    m.set_train(pos)
+    N = m.epoch_size()[0]
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    for first in (0, N - 40_000):
+        got = m.sample(1, first, 40_000)
+        want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 20261015, 1, first, 40_000)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y)
+
+
 def test_sampler_bit_exact_sharded(rl, golden):
     pos, U, I = _ml100k_pos(golden)
     world, seed = 3, 77

@@ -47,7 +47,8 @@ struct Table {
 //                   at most 2B/(kLongSeg+1) < B/8 of them)
 //   refs  [2B]      (triplet position << 1) | (1 if the item is the negative j, 0 if the positive i),
 //                   sorted by item then position (fixed summation order)
-//   useg  [B+1], ioff [2B+1]   builder scratch (segment starts)
+//   useg  [B+1], ioff [2B+1]   builder scratch (ioff: the radix build's item segment starts;
+//                   the bucket build keeps both in LDS and stores neither)
 //   ukey  [2B]      sharded mode: the distinct items as the owner's local row, segment order
 //   meta  [8]       {triplets, user segments, item segments, long item segments, multi user segs}
 //   own   [64]      sharded mode: item segments per owner rank (segments are owner-major)

@@ -295,10 +295,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
-      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) {
-        v.useg[s] = p;
-        s_seg[s++] = p;
-      }
+      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) s_seg[s++] = p;
     }
   }
   __syncthreads();
@@ -328,7 +325,6 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       }
     }
   }
-  if (tid == 0) v.useg[n_useg] = nvalid;
   __syncthreads();  // useg visible block-wide; s_i/s_j sorted; s_key free for the item keys
   BSTAMP(3);
 
@@ -384,8 +380,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       const bool head = r == 0 || s_key[r - 1] != ik[k];
       if (head) {
         ++s;
-        v.ioff[s] = r;
-        if (BUCKET) s_ioff[s] = r;
+        if (BUCKET)
+          s_ioff[s] = r;
+        else
+          v.ioff[s] = r;  // radix build: the segment starts go through global memory
         if (slots) {
           v.ukey[s] = (int32_t)(ik[k] % (uint32_t)iloc);
           atomicAdd(&s_own[ik[k] / (uint32_t)iloc], 1);
@@ -402,8 +400,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         side |= (int32_t)0x80000000;
     }
   }
-  if (tid == 0) v.ioff[n_iseg] = 2 * nvalid;
-  if (BUCKET && tid == 0) s_ioff[n_iseg] = 2 * nvalid;
+  if (tid == 0) (BUCKET ? s_ioff : v.ioff)[n_iseg] = 2 * nvalid;
   auto ioff_at = [&](int seg) { return BUCKET ? s_ioff[seg] : v.ioff[seg]; };
   auto ref_at = [&](int r) { return BUCKET ? s_refs[r] : v.refs[r]; };
   __syncthreads();  // ioff, refs, slots, s_own visible block-wide

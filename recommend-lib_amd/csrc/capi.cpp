@@ -343,16 +343,19 @@ static double host_seconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// diagnostic (BPRMF_HOST_TRACE=1): host timestamps of the first calls' phases, to stderr
-static int g_trace_calls = -1;
-static double g_trace_t[8];
-static int g_trace_n = 0;
+// diagnostic (BPRMF_HOST_TRACE=1): host timestamps of a thread's first calls' phases, to stderr
+static bool trace_on() {
+  static const bool on = getenv("BPRMF_HOST_TRACE") != nullptr;  // initialised once, thread-safe
+  return on;
+}
+static thread_local int g_trace_calls = 0;
+static thread_local double g_trace_t[8];
+static thread_local int g_trace_n = 0;
 static void trace_mark() {
-  if (g_trace_calls < 0) g_trace_calls = getenv("BPRMF_HOST_TRACE") ? 0 : 1 << 30;
-  if (g_trace_calls < 12 && g_trace_n < 8) g_trace_t[g_trace_n++] = host_seconds();
+  if (trace_on() && g_trace_calls < 12 && g_trace_n < 8) g_trace_t[g_trace_n++] = host_seconds();
 }
 static void trace_flush() {
-  if (g_trace_calls >= 12 || g_trace_n == 0) return;
+  if (!trace_on() || g_trace_calls >= 12 || g_trace_n == 0) return;
   fprintf(stderr, "host trace call %d:", g_trace_calls);
   for (int k = 1; k < g_trace_n; ++k) fprintf(stderr, " %.1f", (g_trace_t[k] - g_trace_t[0]) * 1e6);
   fprintf(stderr, " us\n");
@@ -739,6 +742,7 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   const int64_t B = h->cfg.batch_size;
   const int64_t chunk = chunk_triplets(h);
   const int64_t beg = first_step * B, end = std::min(N, (first_step + n_steps) * B);
+  g_trace_n = 0;  // a failed earlier call may have left marks
   trace_mark();
   if (int r = begin_call(h)) return r;
   int64_t steps = 0;

@@ -56,7 +56,10 @@ typedef struct {
   int64_t triplets;     /* triplets processed by the call */
   int64_t steps;        /* optimizer steps taken by the call */
   double loss;          /* sum over the call of -log(sigmoid(pred_i - pred_j)) (BPRMFRecommender.py:174) */
-  double seconds;       /* device wall time of the call (HIP events) */
+  double seconds;       /* HOST wall-clock time of the call, from entry to the status read that
+                           ends it: host launch and capture time, the final wait, and any work
+                           already queued on a shared caller stream are included.  Device time
+                           per kernel kind: bprmf_profile / bprmf_profile_read (HIP events). */
 } bprmf_stats;
 
 /* live kernel timing (HIP events around every launch of each kind while enabled) */
@@ -106,6 +109,12 @@ int bprmf_epoch_size(bprmf_handle* h, int64_t* n_triplets, int64_t* n_steps);
 int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q);
 int bprmf_get_weights(bprmf_handle* h, float* P, float* Q);
 int bprmf_local_rows(bprmf_handle* h, int64_t* users, int64_t* items);
+/* Rows of one table as of the current step (the pending weight decay applied on the way out; the
+ * table itself is not flushed): table 0 = embed_user, 1 = embed_item; rows are local row ids
+ * (global id / world); out [n, factor_num] fp32.  The embedding lookup of BPR.forward
+ * (BPRMFRecommender.py:45-47) for callers that need the vectors, not the scores, and the way to
+ * read a table too large to copy whole (C5: 112.6 GB). */
+int bprmf_get_rows(bprmf_handle* h, int32_t table, const int32_t* rows, int64_t n, float* out);
 int bprmf_step_count(bprmf_handle* h, int64_t* steps);
 
 /* ---- training ----------------------------------------------------------------------------- */

@@ -9,7 +9,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle_bpr.so")
+# BPRMF_ORACLE_LIB_DIR: prebuilt variants of the same sources (tests/sanitize: ASan + UBSan)
+LIB_DIR = os.environ.get("BPRMF_ORACLE_LIB_DIR") or HERE
+LIB = os.path.join(LIB_DIR, "liboracle_bpr.so")
 _lib = None
 
 _i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
@@ -19,7 +21,7 @@ _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 
 def build():
     src = os.path.join(HERE, "bpr_cpu.c")
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    if LIB_DIR == HERE and (not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src)):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
 
@@ -89,8 +91,8 @@ def mf_lib():
     global _mf
     if _mf is None:
         src = os.path.join(HERE, "mf_cpu.c")
-        so = os.path.join(HERE, "liboracle_mf.so")
-        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        so = os.path.join(LIB_DIR, "liboracle_mf.so")
+        if LIB_DIR == HERE and (not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src)):
             subprocess.run(["make", "-s", "-C", HERE], check=True)
         L = ctypes.CDLL(so)
         L.oracle_svd_epochs.argtypes = [ctypes.c_int64, _i32p, _i32p, _f64p, ctypes.c_int,

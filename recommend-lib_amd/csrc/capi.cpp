@@ -24,20 +24,6 @@
 
 using namespace bprmf;
 
-static thread_local std::string g_err;
-
-namespace bprmf {
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-}  // namespace bprmf
-
 static void drop_graphs(bprmf_handle* h);
 static int ensure_step_graphs(bprmf_handle* h);
 
@@ -89,7 +75,6 @@ int bprmf::check_err_flag(bprmf_handle* h) {
 
 extern "C" {
 
-const char* bprmf_last_error(void) { return g_err.c_str(); }
 int bprmf_version(void) { return 1; }
 
 int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
@@ -869,6 +854,32 @@ int bprmf_get_weights(bprmf_handle* h, float* P, float* Q) {
   if (P && h->U) HIPCHK(hipMemcpy2D(P, D * 4, h->P.W, ld * 4, D * 4, h->U, hipMemcpyDeviceToHost));
   if (Q && h->I) HIPCHK(hipMemcpy2D(Q, D * 4, h->Q.W, ld * 4, D * 4, h->I, hipMemcpyDeviceToHost));
   return 0;
+}
+
+int bprmf_get_rows(bprmf_handle* h, int32_t table, const int32_t* rows, int64_t n, float* out) {
+  if (!h || n < 0 || (n > 0 && (!rows || !out)) || (table != 0 && table != 1))
+    return fail(BPRMF_E_INVALID, "bad arguments");
+  const Table& W = table == 0 ? h->P : h->Q;
+  for (int64_t k = 0; k < n; ++k)
+    if (rows[k] < 0 || rows[k] >= W.rows)
+      return fail(BPRMF_E_RANGE, "row %d at %lld out of range [0, %lld)", rows[k], (long long)k,
+                  (long long)W.rows);
+  if (n == 0) return 0;
+  if (int r = set_dev(h)) return r;
+  const size_t D = h->geom.D, ld = h->geom.ld;
+  int32_t* buf = nullptr;
+  if (int r = dalloc(&buf, n + n * (int64_t)ld)) return r;
+  float* o = reinterpret_cast<float*>(buf + n);
+  int rc = 0;
+  // gather_rows(t) brings a row to step t - 1: the rows as of the step count h->t
+  hipError_t e = hipMemcpyAsync(buf, rows, 4 * n, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = gather_rows(h->geom, W, buf, n, h->hp, h->t + 1, o, h->d_err, h->stream);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(out, D * 4, o, ld * 4, D * 4, n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "get_rows: %s", hipGetErrorString(e));
+  hipFree(buf);
+  if (rc) return rc;
+  return check_err_flag(h);
 }
 
 int bprmf_score(bprmf_handle* h, const int32_t* u, const int32_t* i, int64_t n, float* out) {

@@ -9,10 +9,9 @@
 
 #include "../../include/bprmf.h"
 #include "kernels.h"
+#include "status.h"
 
 namespace bprmf {
-
-int fail(int code, const char* fmt, ...);
 
 #define HIPCHK(x)                                                                           \
   do {                                                                                      \

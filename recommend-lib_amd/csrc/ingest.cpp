@@ -32,7 +32,7 @@
 #include <vector>
 
 #include "../../include/bprmf.h"
-#include "handle.h"
+#include "status.h"
 
 using namespace bprmf;
 
@@ -453,12 +453,15 @@ int bprmf_dataset_copy(bprmf_dataset* d, int32_t* users, int32_t* items, float* 
                        int64_t* timestamps, int64_t* user_ids, int64_t* item_ids) {
   if (!d) return fail(BPRMF_E_INVALID, "null dataset");
   const size_t n = d->users.size();
-  if (users) memcpy(users, d->users.data(), 4 * n);
-  if (items) memcpy(items, d->items.data(), 4 * n);
-  if (ratings) memcpy(ratings, d->ratings.data(), 4 * n);
-  if (timestamps) memcpy(timestamps, d->ts.data(), 8 * n);
-  if (user_ids) memcpy(user_ids, d->user_ids.data(), 8 * d->user_ids.size());
-  if (item_ids) memcpy(item_ids, d->item_ids.data(), 8 * d->item_ids.size());
+  // an empty dataset's vectors have no storage (data() may be null: memcpy's source must not be)
+  if (n) {
+    if (users) memcpy(users, d->users.data(), 4 * n);
+    if (items) memcpy(items, d->items.data(), 4 * n);
+    if (ratings) memcpy(ratings, d->ratings.data(), 4 * n);
+    if (timestamps) memcpy(timestamps, d->ts.data(), 8 * n);
+  }
+  if (user_ids && !d->user_ids.empty()) memcpy(user_ids, d->user_ids.data(), 8 * d->user_ids.size());
+  if (item_ids && !d->item_ids.empty()) memcpy(item_ids, d->item_ids.data(), 8 * d->item_ids.size());
   return 0;
 }
 

@@ -88,6 +88,14 @@ struct BatchBuf {
   }
 };
 constexpr int kMaxSegBatch = 8192;  // largest batch the one-workgroup builder handles
+// The record packing above depends on kMaxSegBatch (segment.hip writes, step.hip reads):
+// item records hold beg and len in 15 bits each; inline refs ((pos << 1) | is_j) are 16-bit
+// halves; the builder's packed scan (heads << 16) | valid needs B < 2^16; K2's loss workgroups
+// (one per 256 triplets) each own one of kSegLossSlots slots, all summed by the call's end.
+static_assert(2 * kMaxSegBatch < (1 << 15), "item record beg/len fields are 15 bits");
+static_assert(((2 * kMaxSegBatch - 1) << 1 | 1) <= 0xFFFF, "inline refs are 16-bit halves");
+static_assert(kMaxSegBatch < (1 << 16), "builder packed scan keeps counts in 16 bits");
+static_assert((kMaxSegBatch + 255) / 256 <= kSegLossSlots, "a loss slot per K2 loss workgroup");
 
 struct Hyper {
   float lr, wd;

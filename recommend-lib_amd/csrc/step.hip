@@ -22,6 +22,12 @@
 
 #include "device_common.h"
 
+// The in-launch hand-off below uses gfx94x/gfx950 cache-policy bits (sc1 stores and loads) and
+// the CDNA3/4 L2-per-XCD coherence model; no other target is built or supported.
+#if defined(__HIP_DEVICE_COMPILE__) && !(defined(__gfx950__) || defined(__gfx942__))
+#error "step.hip targets gfx950 (gfx942 also has the sc1 policy bits); build with --offload-arch=gfx950"
+#endif
+
 namespace bprmf {
 
 // diagnostic build only (-DBPRMF_STEP_STAMPS, tools/ubench_step_stamps.py): per workgroup,
@@ -591,7 +597,12 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
 
 // The fused step: K2 of step t (batch c[1] + step) and K1 of step t + 1 (the next batch) in one
 // launch.  K2's workgroups come first in the grid, so every one of them is dispatched before any
-// K1 workgroup that may wait on it (bounded waits besides).  K1 of step t+1 reads the rows step t
+// K1 workgroup that may wait on it (bounded waits besides).  That relies on the command
+// processor dispatching workgroups in blockIdx order, which CDNA hardware does (round-robin over
+// the XCDs, ascending ids) but HIP does not promise: were it ever violated, a K1 wait would end
+// after ~10 s with err bit 8 and the call would fail ("a row's owner never published it"), not
+// hang.  A dynamic ticket (one same-address atomic per workgroup, ~1,700 per step at ~13 ns each
+// when serialised) would cost more than the whole step.  K1 of step t+1 reads the rows step t
 // does not touch at once and the others after their owners publish them; a chunk of n steps is
 // then K1, n - 1 fused launches and K2: one kernel boundary per step instead of two.
 template <int G4, int S, int KB>

@@ -217,6 +217,15 @@ class BPRMF:
         _lib.check(self._L.bprmf_get_weights(self._h, _lib.ptr(P), _lib.ptr(Q)))
         return P, Q
 
+    def get_rows(self, table, rows):
+        """Rows of embed_user (table 'user' / 0) or embed_item ('item' / 1) as of the current step,
+        [len(rows), factor_num] fp32; rows are local row ids.  Reads only those rows (no flush)."""
+        t = {"user": 0, "item": 1}.get(table, table)
+        r = np.ascontiguousarray(np.asarray(rows).reshape(-1), dtype=np.int32)
+        out = np.empty((len(r), self.factor_num), dtype=np.float32)
+        _lib.check(self._L.bprmf_get_rows(self._h, int(t), _lib.ptr(r), len(r), _lib.ptr(out)))
+        return out
+
     def set_weights(self, P, Q):
         U, I = self.local_rows()
         P = np.ascontiguousarray(P, dtype=np.float32)

@@ -1,0 +1,265 @@
+"""GPU parity at every BASELINE.json config shape.
+
+  C2  ml-1m shape (6,040 users x 3,706 items), d=64, B=4096, one GPU: the sampler's whole epoch
+      bit-exact against the C oracle; 20 device-sampled steps bitwise equal to the replay of the
+      oracle's triplets, and within STEP tolerance of the dense reference step (oracle) on the
+      full tables (BPRMFRecommender.py:172-176, util/data_loader.py:680-690).
+  C3  ml-20m shape (138,493 x 26,744), d=128, per-rank B=4096, item-sharded over 2 in-process
+      shards (loopback transport of the C++ runner, sampler mode): equal, to tolerance, to the
+      single-GPU run of the global batches (each step's union of the shards' batches, B=8192),
+      whose sampled triplets are the shard samplers' (bit-exact to the oracle's, tested here).
+  C4  NCF at ml-20m shape, d=64, 3 layers (NCFRecommender.py:27-124,255-260), full-size tables:
+      two batches of forward + gradients + Adam against oracle/ncf_oracle.py, and the NCF
+      sampler (NCFData.ng_sample, util/data_loader.py:931-972) bit-exact on slices.
+  C5  10M users x 100M items, d=256, one GPU (tables 112.6 GB in HBM; row offsets past 2^32
+      floats): sampler slices bit-exact at both ends of the epoch; 3 device-sampled steps
+      against the dense oracle on the touched rows, and untouched rows decayed by exactly
+      (1 - lr*wd)^3 (torch's SGD weight_decay on rows with zero gradient).
+
+Tolerances: the step is fp32 with a different summation order than torch's (SURVEY.md §8c,
+DESIGN.md §4): STEP_ATOL per element after a few steps on values ~1e-2; sharded vs single GPU
+differ only in the order per-peer item gradients are added (SHARD_ATOL).  Sampler and batch
+layout are integer work: bit-exact.
+"""
+import gc
+import importlib
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import bpr_oracle as O
+from oracle import c_oracle as C
+from oracle import ncf_oracle as N
+
+pytestmark = pytest.mark.gpu
+
+STEP_ATOL = 1e-6
+SHARD_ATOL = 1e-6
+DECAY_RTOL = 2e-6
+
+
+def _syn():
+    return importlib.import_module("recommend-lib_amd.synthetic")
+
+
+def _free():
+    gc.collect()
+
+
+# ---- C2: ml-1m shape, d=64 -------------------------------------------------------------------
+def test_c2_ml1m_shape_sampler_and_steps(rl):
+    _free()
+    U, I, d, B, seed = 6040, 3706, 64, 4096, 20261015
+    pos = _syn().make_positives(U, I, 575_000, seed)
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    a = rl.BPRMF(U, I, d, batch_size=B, seed=seed)
+    a.set_train(pos)
+    N_, S = a.epoch_size()
+    assert N_ == 4 * len(pos)
+    # the whole epoch's triplets, bit for bit
+    got = a.sample(0, 0, N_)
+    want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, seed, 0, 0, N_)
+    for x, y in zip(got, want):
+        assert np.array_equal(x, y)
+    # 20 device-sampled steps == replay of the oracle's triplets (bitwise), ~= the dense step
+    P0, Q0 = a.get_weights()
+    b = rl.BPRMF(U, I, d, batch_size=B, seed=seed)
+    b.set_weights(P0, Q0)
+    sa = a.train_steps(0, 0, 20)
+    n = 20 * B
+    sb = b.train_triplets(want[0][:n], want[1][:n], want[2][:n])
+    Pa, Qa = a.get_weights()
+    Pb, Qb = b.get_weights()
+    assert np.array_equal(Pa, Pb) and np.array_equal(Qa, Qb)
+    assert sa["loss"] == sb["loss"] and sa["steps"] == 20
+    ref = C.DenseTrainer(P0, Q0, 0.01, 0.001)
+    loss = 0.0
+    for k in range(20):
+        s = slice(k * B, (k + 1) * B)
+        loss += ref.step(want[0][s], want[1][s], want[2][s])
+    np.testing.assert_allclose(Pa, ref.P, rtol=0, atol=STEP_ATOL)
+    np.testing.assert_allclose(Qa, ref.Q, rtol=0, atol=STEP_ATOL)
+    assert sa["loss"] == pytest.approx(loss, rel=1e-5)
+    a.close()
+    b.close()
+
+
+# ---- C3: ml-20m shape, d=128, per-rank B=4096, 2 item-sharded shards ---------------------------
+def _runner_threads(rl, world, fn):
+    grp = rl.sharded.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            out[r] = fn(rl.sharded.ThreadComm(grp, r), r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    assert all(not t.is_alive() for t in ts), "runner threads did not finish"
+    return out
+
+
+def test_c3_per_rank_shape_sharded_equals_single_gpu_global_batch(rl):
+    _free()
+    U, I, d, B, world, seed, steps = 138493, 26744, 128, 4096, 2, 77, 8
+    pos = _syn().make_positives(U, I, 10_000_000, 20261015)
+    sh = rl.sharded
+    g = np.random.default_rng(3)
+    P0 = (0.01 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.01 * g.standard_normal((I, d))).astype(np.float32)
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, d, batch_size=B, seed=seed, device=0, comm=comm)
+        m.set_train(pos)
+        m.set_weights(sh.shard_rows(P0, r, world), sh.shard_rows(Q0, r, world))
+        m.attach_runner("loopback", key=4301)
+        st = m.train_steps(0, 0, steps)
+        return m.get_weights(), st
+
+    parts = _runner_threads(rl, world, fn)
+    P = sh.unshard_rows([p[0][0] for p in parts], U)
+    Q = sh.unshard_rows([p[0][1] for p in parts], I)
+    # each shard's batches: its own sampler (shard seed), bit-exact to the oracle's
+    shard_trip = []
+    for r in range(world):
+        m = rl.BPRMF(U, I, 8, batch_size=B, seed=seed, rank=r, world=world)
+        m.set_train(pos)
+        t = m.sample(0, 0, steps * B)
+        mine = pos[pos[:, 0] % world == r]
+        indptr, indices = O.build_csr(mine[:, 0], mine[:, 1], U)
+        want = C.sample(mine[:, 0], mine[:, 1], indptr, indices, I, 4,
+                        (seed + r * 0x9E3779B97F4A7C15) & (2**64 - 1), 0, 0, 2 * B)
+        for x, y in zip(t, want):
+            assert np.array_equal(x[:2 * B], y)
+        shard_trip.append(t)
+        m.close()
+    # the single-GPU run of the global batches (B_global = world * B)
+    s = rl.BPRMF(U, I, d, batch_size=world * B, seed=seed)
+    s.set_weights(P0, Q0)
+    cat = [np.concatenate([np.concatenate([t[c][k * B:(k + 1) * B] for t in shard_trip])
+                           for k in range(steps)]) for c in range(3)]
+    ss = s.train_triplets(*cat)
+    assert ss["steps"] == steps
+    Ps, Qs = s.get_weights()
+    np.testing.assert_allclose(P, Ps, rtol=0, atol=SHARD_ATOL)
+    np.testing.assert_allclose(Q, Qs, rtol=0, atol=SHARD_ATOL)
+    assert sum(p[1]["triplets"] for p in parts) == steps * world * B
+    got_loss = sum(p[1]["loss"] for p in parts)
+    assert got_loss == pytest.approx(ss["loss"], rel=1e-5)
+    s.close()
+
+
+# ---- C4: NCF at ml-20m shape, d=64, 3 layers ---------------------------------------------------
+def test_c4_ncf_ml20m_shape_steps_vs_oracle(rl):
+    _free()
+    U, I, d, L, B = 138493, 26744, 64, 3, 256
+    g = np.random.default_rng(44)
+    m = rl.NCF(U, I, d, L, batch_size=B, seed=9)
+    params = m.state_dict()
+    assert params["embed_user_MLP.weight"].shape == (U, d * 2 ** (L - 1))
+    opt = N.Adam(params)
+    for k in range(2):
+        u = g.integers(0, U, B)
+        i = g.integers(0, I, B)
+        u[:20] = 5  # a repeated user and item (summed gradients)
+        i[10:40] = 11
+        y = (g.random(B) < 0.2).astype(np.float32)
+        z = m.predict_logits(u, i)
+        z_ref, _ = N.forward(params, "NeuMF-end", L, u, i)
+        np.testing.assert_allclose(z, z_ref, rtol=1e-4, atol=2e-6)
+        grads, loss = N.grads(params, "NeuMF-end", L, u, i, y)
+        params = opt.step(params, grads)
+        st = m.train_samples(u, i, y)
+        assert abs(st["loss"] - loss) < 1e-5
+    got = m.state_dict()
+    for n in m.names:
+        np.testing.assert_allclose(got[n], params[n], rtol=0, atol=5e-5, err_msg=n)
+    m.close()
+
+
+def test_c4_ncf_sampler_ml20m_shape_bit_exact(rl):
+    _free()
+    U, I = 138493, 26744
+    pos = _syn().make_positives(U, I, 10_000_000, 20261015)
+    m = rl.NCF(U, I, 8, 1, batch_size=256, num_ng=4, seed=13)
+    m.set_train(pos)
+    n = m.epoch_size()[0]
+    assert n == 5 * len(pos)
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    for first in (0, n - 50_000):
+        u, i, y = m.sample(2, first, 50_000)
+        uo, io, yo = N.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, 13, 2, first, 50_000)
+        assert np.array_equal(u, uo) and np.array_equal(i, io) and np.array_equal(y, yo)
+    m.close()
+
+
+# ---- C5: 10M users x 100M items, d=256, one GPU -------------------------------------------------
+def _c5_positives(U, I, n, seed):
+    """n distinct (user, item) pairs over the whole id ranges: users uniform, items half uniform
+    over 1e8 and half from a Zipf-like hot set, so ids near 2^27 and hot rows both occur."""
+    g = np.random.default_rng(seed)
+    u = g.integers(0, U, n)
+    hot = (g.zipf(1.3, n // 2) - 1) % 1000
+    it = np.concatenate([g.integers(0, I, n - n // 2), hot * 99991 % I])
+    key = np.unique(u.astype(np.int64) * I + it)
+    u, it = key // I, key % I
+    order = np.lexsort((it, u))
+    return np.stack([u[order], it[order]], 1)
+
+
+def test_c5_shape_one_gpu_sampler_steps_and_decay(rl):
+    _free()
+    U, I, d, B, seed, steps = 10_000_000, 100_000_000, 256, 4096, 5, 3
+    lr, wd = 0.01, 0.001
+    pos = _c5_positives(U, I, 2_000_000, 55)
+    m = rl.BPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, seed=seed)
+    try:
+        m.set_train(pos)
+        N_, S = m.epoch_size()
+        assert N_ == 4 * len(pos)
+        indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+        for first in (0, N_ - 30_000):
+            got = m.sample(0, first, 30_000)
+            want = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, 4, seed, 0, first, 30_000)
+            for x, y in zip(got, want):
+                assert np.array_equal(x, y)
+        tu, ti, tj = m.sample(0, 0, steps * B)
+        users = np.unique(tu)
+        items = np.unique(np.concatenate([ti, tj]))
+        assert items.max() > 2 ** 26 and users.max() > 2 ** 23  # rows far into both tables
+        g = np.random.default_rng(1)
+        cold_u = np.setdiff1d(g.integers(0, U, 2000), users)
+        cold_i = np.setdiff1d(g.integers(0, I, 2000), items)
+        cold_i = np.concatenate([cold_i, [I - 1]]) if (I - 1) not in set(items.tolist()) else cold_i
+        P0, Q0 = m.get_rows("user", users), m.get_rows("item", items)
+        Pc0, Qc0 = m.get_rows("user", cold_u), m.get_rows("item", cold_i)
+        st = m.train_steps(0, 0, steps)
+        assert st["steps"] == steps
+        P1, Q1 = m.get_rows("user", users), m.get_rows("item", items)
+        Pc1, Qc1 = m.get_rows("user", cold_u), m.get_rows("item", cold_i)
+    finally:
+        m.close()
+        _free()
+    # the dense reference step on the touched rows only (rows interact only through the batch)
+    ref = C.DenseTrainer(P0, Q0, lr, wd)
+    cu = np.searchsorted(users, tu).astype(np.int32)
+    ci = np.searchsorted(items, ti).astype(np.int32)
+    cj = np.searchsorted(items, tj).astype(np.int32)
+    loss = 0.0
+    for k in range(steps):
+        s = slice(k * B, (k + 1) * B)
+        loss += ref.step(cu[s], ci[s], cj[s])
+    np.testing.assert_allclose(P1, ref.P, rtol=0, atol=STEP_ATOL)
+    np.testing.assert_allclose(Q1, ref.Q, rtol=0, atol=STEP_ATOL)
+    assert st["loss"] == pytest.approx(loss, rel=1e-5)
+    alpha = np.float32(1.0) - np.float32(lr) * np.float32(wd)
+    np.testing.assert_allclose(Pc1, Pc0 * alpha ** steps, rtol=DECAY_RTOL)
+    np.testing.assert_allclose(Qc1, Qc0 * alpha ** steps, rtol=DECAY_RTOL)
+    assert np.abs(Qc0).max() > 0  # the init reached the table's last rows

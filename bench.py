@@ -19,7 +19,10 @@ roofline: algorithmic bytes per step = B*(24d+12) (3 rows read + 3 rows written 
   after the timed region over the same number of steps (per-launch events perturb the timing, so
   they are kept out of the timed region); rocprofv3 summaries of the same command: profiles/.
 cpu_baseline: the oracle's C port of the reference step (dense grads + dense weight decay, as torch
-  does) and of the sampler, timed on this host on a bounded sample.
+  does) and of the sampler, timed on this host on a bounded sample; the reference's own torch-CPU
+  step (measured in the build container) is quoted beside it.
+--semantics hogwild: the opt-in relaxed mode (csrc/hogwild.hip; not the reference step) on the
+  same workload, labelled as such in config.semantics; the default line is the exact step.
 """
 import argparse
 import importlib
@@ -73,14 +76,26 @@ def cpu_baseline(pos, U, I, d, B, budget_s=12.0, seed=1):
                        f"value = 1/(1/step + 1/sampler)")
 
 
+# the reference's own torch-CPU BPR step at the ml-20m shape, d=128, B=4096 (SURVEY.md
+# §6): measured in the build container, not on the GPU box (the reference does not travel there)
+REFERENCE_CPU_QUOTED = {"value": 179000.0, "unit": "triplets/s", "threads": 8,
+                        "source": "BASELINE.md: reference torch-CPU step (BPRMFRecommender.py:172-176), "
+                                  "ml-20m shape d=128 B=4096, 8-core build container, not this host"}
+
+
 def load_traffic(cfg_key):
-    """HBM bytes per step measured with rocprofv3 PMC counters (profiles/pmc_traffic.json)."""
+    """Bytes per step from rocprofv3 PMC counters (profiles/pmc_traffic.json): a STATIC number from
+    an earlier profiled run, labelled as such in the line (traffic_source)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     with open(p) as f:
         e = json.load(f).get(cfg_key)
-    return None if e is None else e.get("hbm_bytes_per_step")
+    if e is None:
+        return None, None
+    src = ("profiles/pmc_traffic.json (static, from an earlier rocprofv3 --pmc run of this kernel; "
+           "L2<->fabric bytes, Infinity-Cache hits included)")
+    return e.get("hbm_bytes_per_step"), src
 
 
 def main():
@@ -106,6 +121,9 @@ def main():
     ap.add_argument("--python-orchestration", action="store_true",
                     help="sharded: per-step Python orchestration over torch.distributed instead of "
                          "the library's runner")
+    ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild"],
+                    help="exact: the reference's batch-synchronous step (default, the headline); "
+                         "hogwild: opt-in relaxed synchronisation (a separate, labelled line)")
     ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend (gloo: rehearse several ranks on one GPU, IPC "
                          "transport; RCCL refuses two ranks on one device)")
@@ -123,6 +141,9 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     sharded = world > 1 or a.sharded
+    hog = a.semantics == "hogwild"
+    if hog and sharded:
+        raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
     if sharded:
         import torch.distributed as dist
         if "RANK" not in os.environ:  # --sharded without a launcher: a one-rank group
@@ -136,7 +157,8 @@ def main():
     U, I, d, B = a.users, a.items, a.factor, a.batch_size
     pos = syn.make_positives(U, I, a.positives, a.seed)
     if not sharded:
-        m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed, device=local)
+        m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed, device=local,
+                     semantics=a.semantics)
         m.set_train(pos)
         n_steps = m.epoch_size()[1]
 
@@ -201,21 +223,27 @@ def main():
             if "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
+            elif "step_graph" in us and hog:  # one k_hogwild launch per chunk
+                step_us, what = us["step_graph"], ("k_hogwild (in-kernel sampling + gather + dots + "
+                                                   "sigmoid + SGD scatter, one launch per chunk)")
             elif "step_graph" in us:  # events around each chunk's step launches (GPU-bound)
                 step_us, what = us["step_graph"], ("fused step launches (K2 of step t + K1 of step "
                                                    "t+1 per launch; a chunk is K1, n-1 fused, K2)")
             else:  # eager (sharded): events around the two kernels of sampled steps
                 step_us, what = us["user_step"] + us["item_step"], "user_step + item_step"
             ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9
+            tkey = f"ml20m_d{d}_B{B}" + ("_hogwild" if hog else "")
+            traffic, tsrc = load_traffic(tkey) if (U, I) == (U_ML20M, I_ML20M) else (None, None)
             roof = dict(bound="hbm", kernel=what, achieved=round(ach, 1), peak=HBM_PEAK_GBS,
                         unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                        traffic=load_traffic(f"ml20m_d{d}_B{B}"),
+                        traffic=traffic, traffic_source=tsrc,
                         algorithmic_bytes_per_launch=B * bytes_per_triplet(d),
                         avg_us_per_step=round(step_us, 3),
                         avg_launch_us={k: round(v, 3) for k, v in us.items()})
         cpu = None
         if not a.no_cpu_baseline and world == 1 and not sharded:
             cpu = cpu_baseline(pos, U, I, d, B)
+            cpu["reference_cpu_quoted"] = REFERENCE_CPU_QUOTED
         out = {"metric": "BPR triplets/sec ml-20m d=128 (HR@10 parity vs ref: tests/test_gpu_parity.py)",
                "value": round(value, 1), "unit": "triplets/s", "n_gpus": world, "steps": a.steps,
                "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 5),
@@ -228,7 +256,10 @@ def main():
                           "parallelism": (f"users+items row-sharded x{world}, "
                                           f"{'python/torch.distributed' if a.python_orchestration else m.runner} exchange"
                                           if sharded else "single GPU"),
-                          "semantics": "exact batch-synchronous SGD (reference step), lazy weight decay"},
+                          "semantics": ("relaxed (hogwild: per-triplet lock-free updates, weight decay "
+                                        "once per row per step, staleness bounded by the launch's "
+                                        "in-flight window; NOT the reference step)" if hog else
+                                        "exact batch-synchronous SGD (reference step), lazy weight decay")},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if dist:

@@ -36,6 +36,13 @@ typedef enum {
   BPRMF_E_UNSUPPORTED = -6
 } bprmf_status;
 
+/* Step semantics.  EXACT: every step reads the tables as the previous step left them, duplicate
+ * rows' gradients are summed (BPRMFRecommender.py:172-176), bitwise reproducible.  HOGWILD:
+ * each triplet is applied on its own as soon as its rows arrive, lock-free (concurrent updates
+ * of a row may overwrite each other), weight decay still once per row per step; staleness is
+ * bounded by the launch's in-flight window.  Single-GPU handles only. */
+enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1 };
+
 typedef struct {
   int64_t user_num;     /* rows of embed_user  (BPRMFRecommender.py:36) — global count */
   int64_t item_num;     /* rows of embed_item  (BPRMFRecommender.py:37) — global count */
@@ -49,7 +56,9 @@ typedef struct {
   int32_t device;       /* HIP device ordinal */
   int32_t rank;         /* shard of this handle: owns users u%world==rank, items i%world==rank */
   int32_t world;        /* 1 for a single GPU */
-  int32_t reserved[4];
+  int32_t semantics;    /* BPRMF_SEM_EXACT (0, default): the reference's batch-synchronous step;
+                           BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
+  int32_t reserved[3];
 } bprmf_config;
 
 typedef struct {

@@ -74,6 +74,55 @@ def train_replay(P, Q, triplets, bounds, lr, wd):
     return np.array(losses)
 
 
+def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
+    """The opt-in relaxed mode (semantics "hogwild", csrc/hogwild.hip) run serially: the spec its
+    SERIAL test build (BPRMF_HOGWILD_SERIAL=1: one lane group, slot order) must reproduce.
+    NOT the reference step (BPRMFRecommender.py:172-176 sums a batch's gradients before one
+    update); this applies each triplet on its own, keeping the reference's per-step weight decay:
+      slot s belongs to step t = t0 + 1 + s // B; a row with stamp st < t is first brought to step
+      t - 1 (x (1 - lr wd)^(t-1-st)) and takes the wd term, its stamp becomes t; a row with
+      st >= t (already updated in step t) takes neither;
+      x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x); g_u = -c (Q_i - Q_j), g_i = -c P_u, g_j = c P_u,
+      all from the values read before the triplet's stores; stores in the order P_u, Q_i, Q_j (so
+      Q_j's wins when i == j).
+    In place on float32 P, Q; stamps sP, sQ (int arrays, default all t0) are updated too.
+    Returns the loss sum of -log sigmoid(x) (float64)."""
+    P_, Q_ = P, Q
+    sP = np.full(P.shape[0], t0, np.int64) if sP is None else sP
+    sQ = np.full(Q.shape[0], t0, np.int64) if sQ is None else sQ
+    log2a = math.log2(1.0 - float(lr) * float(wd))
+    lr32, wd32 = np.float32(lr), np.float32(wd)
+    loss = 0.0
+
+    def bring(W, st, r, t):
+        if st[r] < t:
+            f = np.float32(2.0 ** np.float32((t - 1 - st[r]) * log2a)) if t - 1 - st[r] > 0 else np.float32(1)
+            return (W[r] * f).astype(np.float32), True
+        return W[r].copy(), False
+
+    for s in range(len(u)):
+        t = t0 + 1 + s // B
+        uu, ii, jj = int(u[s]), int(i[s]), int(j[s])
+        pu, fu = bring(P_, sP, uu, t)
+        vi, fi = bring(Q_, sQ, ii, t)
+        vj, fj = bring(Q_, sQ, jj, t)
+        x = np.float32(np.dot(pu.astype(np.float64), vi.astype(np.float64)) -
+                       np.dot(pu.astype(np.float64), vj.astype(np.float64)))
+        c = np.float32(1.0) / (np.float32(1.0) + np.float32(np.exp(np.float64(x))))
+        loss += float(np.logaddexp(0.0, -float(x)))
+        gu, gi, gj = -c * (vi - vj), -c * pu, c * pu
+        P_[uu] = pu - lr32 * (gu + (wd32 if fu else np.float32(0)) * pu)
+        Q_[ii] = vi - lr32 * (gi + (wd32 if fi else np.float32(0)) * vi)
+        Q_[jj] = vj - lr32 * (gj + (wd32 if fj else np.float32(0)) * vj)
+        if fu:
+            sP[uu] = t
+        if fi:
+            sQ[ii] = t
+        if fj:
+            sQ[jj] = t
+    return loss, sP, sQ
+
+
 # ----------------------------------------------------------------------------------------------
 # 2. sampler specification (bit-exact target for the HIP sampler)
 # ----------------------------------------------------------------------------------------------

@@ -25,7 +25,8 @@ class Config(ctypes.Structure):
                 ("weight_decay", ctypes.c_float), ("batch_size", ctypes.c_int32),
                 ("num_ng", ctypes.c_int32), ("init_std", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("device", ctypes.c_int32), ("rank", ctypes.c_int32),
-                ("world", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("world", ctypes.c_int32), ("semantics", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 3)]
 
 
 class NcfConfig(ctypes.Structure):  # ncf_config, include/ncf.h

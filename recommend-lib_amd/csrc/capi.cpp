@@ -92,8 +92,13 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_INVALID, "lr, weight_decay and init_std must be >= 0");
   Geom g;
   if (!make_geom(cfg->factor_num, &g)) return fail(BPRMF_E_UNSUPPORTED, "factor_num must be in [1, 1024]");
+  if (cfg->semantics != BPRMF_SEM_EXACT && cfg->semantics != BPRMF_SEM_HOGWILD)
+    return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0) or BPRMF_SEM_HOGWILD (1)");
+  if (cfg->semantics == BPRMF_SEM_HOGWILD && cfg->world != 1)
+    return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
   auto* h = new bprmf_handle();
   h->cfg = *cfg;
+  h->semantics = cfg->semantics;
   h->geom = g;
   h->hp.lr = cfg->lr;
   h->hp.wd = cfg->weight_decay;
@@ -622,6 +627,29 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   const int64_t B = h->cfg.batch_size;
   const int64_t nb = (n + B - 1) / B;
   if ((int64_t)h->t + nb >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  if (h->semantics == BPRMF_SEM_HOGWILD) {
+    // one launch for the chunk: triplets sampled in the kernel (or replayed), each applied on its
+    // own (hogwild.hip); the loss goes to the segmented path's kSegLossSlots slots
+    if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
+    const SamplerArgs sa = sampler_args(h);
+    {
+      hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
+      if (ea) HIPCHK(hipEventRecord(ea, h->stream));
+      HIPCHK(hogwild(h->geom, ru ? nullptr : &sa, epoch, first_slot, ru, ri, rj, n, h->P, h->Q, h->hp,
+                     h->t, (int)B, h->d_loss, h->d_err, h->stream));
+      if (ea) {
+        hipEvent_t eb = prof_event(h);
+        if (eb) {
+          HIPCHK(hipEventRecord(eb, h->stream));
+          h->prof_rec[BPRMF_KPROF_STEPS].push_back({ea, eb});
+          h->prof_weight[BPRMF_KPROF_STEPS] += nb - 1;  // one pair covers nb steps
+        }
+      }
+    }
+    h->t += (int32_t)nb;
+    *steps_done += nb;
+    return 0;
+  }
   if (!seg_mode(h)) {
     if (!ru) {
       if (int r = ensure_trip(h, n)) return r;

@@ -217,4 +217,20 @@ static inline unsigned grid_flat(int64_t n) {
     default: return hipErrorInvalidValue;                           \
   }
 
+// Expand BODY for every instantiated float4 geometry (G4_, S_).
+#define BPRMF_DISPATCH4(geom, BODY)                                \
+  switch ((geom).G4 * 10 + (geom).S) {                             \
+    case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
+    case 21: { constexpr int G4_ = 2, S_ = 1; BODY; } break;       \
+    case 41: { constexpr int G4_ = 4, S_ = 1; BODY; } break;       \
+    case 81: { constexpr int G4_ = 8, S_ = 1; BODY; } break;       \
+    case 161: { constexpr int G4_ = 16, S_ = 1; BODY; } break;     \
+    case 321: { constexpr int G4_ = 32, S_ = 1; BODY; } break;     \
+    case 641: { constexpr int G4_ = 64, S_ = 1; BODY; } break;     \
+    case 642: { constexpr int G4_ = 64, S_ = 2; BODY; } break;     \
+    case 643: { constexpr int G4_ = 64, S_ = 3; BODY; } break;     \
+    case 644: { constexpr int G4_ = 64, S_ = 4; BODY; } break;     \
+    default: return hipErrorInvalidValue;                          \
+  }
+
 }  // namespace bprmf

@@ -62,6 +62,7 @@ struct bprmf_handle {
   float* d_xloss = nullptr;    // [2][B] x per triplet (K1 -> K2's loss workgroups)
   int32_t* d_pend_q = nullptr;  // [2][I] step that last marked an item row (fused step)
   int32_t* d_pend_p = nullptr;  // [2][U] the same for user rows K2 finishes
+  int32_t semantics = BPRMF_SEM_EXACT;  // cfg.semantics (BPRMF_SEM_HOGWILD: hogwild.hip)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan

@@ -217,6 +217,13 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
                       const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
                       double* loss, int32_t* err, hipStream_t s);
 int item_long_blocks(int B);
+// relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
+// sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s
+// belongs to step t0 + 1 + s / B; loss into kSegLossSlots slots
+hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
+                   const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
+                   Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
+                   hipStream_t s);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

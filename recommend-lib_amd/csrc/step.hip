@@ -622,22 +622,6 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
                                       hp, ld, t + 1, sb, nullptr, B, err);
 }
 
-// Expand BODY for every instantiated float4 geometry (G4_, S_).
-#define BPRMF_DISPATCH4(geom, BODY)                                \
-  switch ((geom).G4 * 10 + (geom).S) {                             \
-    case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
-    case 21: { constexpr int G4_ = 2, S_ = 1; BODY; } break;       \
-    case 41: { constexpr int G4_ = 4, S_ = 1; BODY; } break;       \
-    case 81: { constexpr int G4_ = 8, S_ = 1; BODY; } break;       \
-    case 161: { constexpr int G4_ = 16, S_ = 1; BODY; } break;     \
-    case 321: { constexpr int G4_ = 32, S_ = 1; BODY; } break;     \
-    case 641: { constexpr int G4_ = 64, S_ = 1; BODY; } break;     \
-    case 642: { constexpr int G4_ = 64, S_ = 2; BODY; } break;     \
-    case 643: { constexpr int G4_ = 64, S_ = 3; BODY; } break;     \
-    case 644: { constexpr int G4_ = 64, S_ = 4; BODY; } break;     \
-    default: return hipErrorInvalidValue;                          \
-  }
-
 // BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread
 // item-step workgroups (A/B of the two choices; read at launch / capture time)
 static bool use_wt() {

@@ -35,18 +35,25 @@ def _as_pairs(train_set):
     return np.ascontiguousarray(a[:, 0], dtype=np.int32), np.ascontiguousarray(a[:, 1], dtype=np.int32)
 
 
+# step semantics (include/bprmf.h BPRMF_SEM_*): "exact" is the reference's batch-synchronous SGD
+# (the default); "hogwild" is the opt-in relaxed mode (lock-free per-triplet updates, weight decay
+# still once per row per step; single GPU)
+SEMANTICS = {"exact": 0, "hogwild": 1}
+
+
 class BPRMF:
     """BPR matrix factorisation trained on one MI355X (or one shard of a multi-GPU run).
 
     Parameters follow the reference CLI (BPRMFRecommender.py:53-116): lr=0.01, wd=0.001,
     batch_size=4096, epochs=20, factor_num=32, num_ng=4; init N(0, 0.01^2) (:39-40).
     `seed` makes init, negative sampling and the epoch shuffle reproducible (the reference is
-    unseeded).
+    unseeded).  `semantics="hogwild"` opts into relaxed synchronisation (not the reference's
+    step; faster, nondeterministic; see DESIGN.md §5b for its HR@10 / NDCG@10 against exact).
     """
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, epochs=20, init_std=0.01, seed=0, device=0, rank=0, world=1,
-                 verbose=False):
+                 verbose=False, semantics="exact"):
         self.user_num, self.item_num = int(user_num), int(item_num)
         self.factor_num = int(factor_num)
         self.lr, self.wd = float(lr), float(wd)
@@ -54,6 +61,9 @@ class BPRMF:
         self.seed, self.device = int(seed), int(device)
         self.rank, self.world = int(rank), int(world)
         self.verbose = verbose
+        if semantics not in SEMANTICS:
+            raise ValueError(f"semantics must be one of {sorted(SEMANTICS)}")
+        self.semantics = semantics
         self.epoch = 0
         self.history = []
         L = _lib.load()
@@ -61,7 +71,7 @@ class BPRMF:
                           factor_num=self.factor_num, lr=self.lr, weight_decay=self.wd,
                           batch_size=self.batch_size, num_ng=self.num_ng, init_std=float(init_std),
                           seed=self.seed & (2**64 - 1), device=self.device, rank=self.rank,
-                          world=self.world)
+                          world=self.world, semantics=SEMANTICS[semantics])
         h = ctypes.c_void_p()
         _lib.check(L.bprmf_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -193,3 +193,28 @@ def test_metric_eval_ncf_ranks_each_batch(rl):
     assert ndcg == pytest.approx((1 / np.log2(3) + 1.0) / 2)
     with pytest.raises(ValueError):
         rl.metrics.metric_eval(Stub(), batches, 2, algo="nfm")
+
+
+def test_hogwild_spec_equals_reference_step_at_batch_one():
+    """The relaxed mode's serial spec (oracle hogwild_serial) is per-triplet SGD with the reference's
+    per-step weight decay, so with one triplet per step (B = 1, i != j) it IS the reference step
+    (BPRMFRecommender.py:172-176, here oracle bpr_step_dense) applied triplet by triplet, once every
+    row is brought to the last step."""
+    g = np.random.default_rng(5)
+    U, I, d, n, lr, wd = 7, 9, 6, 80, 0.05, 0.02
+    P0 = (0.3 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.3 * g.standard_normal((I, d))).astype(np.float32)
+    u, i = g.integers(0, U, n), g.integers(0, I, n)
+    j = (i + 1 + g.integers(0, I - 1, n)) % I
+    P, Q = P0.copy(), Q0.copy()
+    loss, sP, sQ = O.hogwild_serial(P, Q, u, i, j, lr, wd, 1)
+    a = 1.0 - lr * wd
+    P = P * np.power(a, n - sP)[:, None]
+    Q = Q * np.power(a, n - sQ)[:, None]
+    Pr, Qr = P0.copy(), Q0.copy()
+    lr_ = 0.0
+    for s in range(n):
+        lr_ += O.bpr_step_dense(Pr, Qr, u[s:s + 1], i[s:s + 1], j[s:s + 1], lr, wd)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+    assert loss == pytest.approx(lr_, rel=1e-5)

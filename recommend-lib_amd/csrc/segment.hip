@@ -162,7 +162,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
     int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int slot_stride,
-    int user_bits, int item_bits, int tpb, BatchBuf bb, int32_t* __restrict__ err, CursorInit ci) {
+    int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb, int32_t* __restrict__ err,
+    CursorInit ci) {
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -359,25 +360,39 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) s_key[tid * IPT2 + k] = ik[k];
   __syncthreads();
-  int iheads = 0;
+  // k1_items (single GPU): an item with ONE reference in the batch is updated by K1 from that
+  // triplet (its gradient is that one term; the same arithmetic K2 would do): no contribution row,
+  // no K2 record.  Item segments K2 serves are the others, numbered compactly (`mseg`).
+  const int nref = 2 * nvalid;
+  auto is_head = [&](int r, uint32_t key) { return r == 0 || s_key[r - 1] != key; };
+  auto is_sole = [&](int r, uint32_t key) {
+    return k1_items && is_head(r, key) && (r + 1 >= nref || s_key[r + 1] != key);
+  };
+  int iheads = 0, mheads = 0;
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) {
     const int r = tid * IPT2 + k;
     if (ik[k] != kNone) {
-      iheads += (r == 0 || s_key[r - 1] != ik[k]);
+      const bool h = is_head(r, ik[k]);
+      iheads += h;
+      mheads += h && !is_sole(r, ik[k]);
       v.refs[r] = (int32_t)iv[k];
       if (BUCKET) s_refs[r] = (int32_t)iv[k];
     }
   }
-  int iseg0 = 0, n_iseg = 0;
-  Scan().exclusive_scan(iheads, iseg0, 0, n_iseg, sscan, rocprim::plus<int>());
+  // one scan for both counts (each <= 2B <= 16384): all heads high, K2-served heads low
+  int ipre = 0, itot = 0;
+  Scan().exclusive_scan((iheads << 16) | mheads, ipre, 0, itot, sscan, rocprim::plus<int>());
+  const int iseg0 = ipre >> 16, n_iseg = itot >> 16;
+  const int mseg0 = ipre & 0xFFFF, n_mseg = itot & 0xFFFF;
   {
     int s = iseg0 - 1;  // segment of this thread's first ref if it is not a head
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] == kNone) continue;
-      const bool head = r == 0 || s_key[r - 1] != ik[k];
+      const bool head = is_head(r, ik[k]);
+      const bool sole = is_sole(r, ik[k]);
       if (head) {
         ++s;
         if (BUCKET)
@@ -391,13 +406,14 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       }
       // triplet side -> its item slot (sharded); bit 31: this reference is its item's first in
       // the batch (K1 marks the item for the next step's fused K1 from that triplet only: one
-      // mark per distinct item instead of one per reference on hot addresses).  Each (triplet,
-      // side) belongs to exactly one reference, so the writes need no atomics.
+      // mark per distinct item instead of one per reference on hot addresses); bit 30: it is the
+      // item's only reference (K1 updates the item).  Each (triplet, side) belongs to exactly one
+      // reference, so the writes need no atomics.
       int32_t& side = (iv[k] & 1 ? s_j : s_i)[iv[k] >> 1];
       if (slots)
         side = s | (head ? (int32_t)0x80000000 : 0);
       else if (head)
-        side |= (int32_t)0x80000000;
+        side |= (int32_t)0x80000000 | (sole ? (int32_t)0x40000000 : 0);
     }
   }
   if (tid == 0) (BUCKET ? s_ioff : v.ioff)[n_iseg] = 2 * nvalid;
@@ -429,11 +445,15 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   };
   int nlong_mine = 0;
   {
-    int s = iseg0;
+    int s = iseg0, ms = mseg0;  // segment index, K2 record index
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
-      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
+      if (ik[k] != kNone && is_head(r, ik[k])) {
+        if (is_sole(r, ik[k])) {  // K1's: no record
+          ++s;
+          continue;
+        }
         const int end = ioff_at(s + 1);
         const int len = end - r;
         const int lng = len > kLongSeg;
@@ -445,9 +465,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
           const int b = 2 * m + 1 < len ? ref_at(r + 2 * m + 1) : 0;
           pk[m] = a | (b << 16);
         }
-        store_rec(v.irec + (int64_t)s * kRec, slots ? slot_of(s) : (int)ik[k],
+        store_rec(v.irec + (int64_t)ms * kRec, slots ? slot_of(s) : (int)ik[k],
                   r | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
         ++s;
+        ++ms;
       }
     }
   }
@@ -456,20 +477,25 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   BSTAMP(6);
   Scan().exclusive_scan(nlong_mine, lpre, 0, n_long, sscan, rocprim::plus<int>());
   if (nlong_mine) {
-    int s = iseg0;
+    int s = iseg0, ms = mseg0;
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
-      if (ik[k] != kNone && (r == 0 || s_key[r - 1] != ik[k])) {
+      if (ik[k] != kNone && is_head(r, ik[k])) {
+        if (is_sole(r, ik[k])) {
+          ++s;
+          continue;
+        }
         const int end = ioff_at(s + 1);
         if (end - r > kLongSeg) {
           if (lpre < kMaxLongItems)
             store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
           else
-            v.irec[(int64_t)s * kRec + 1] = r | ((end - r) << 15);  // over the cap: short path
+            v.irec[(int64_t)ms * kRec + 1] = r | ((end - r) << 15);  // over the cap: short path
           ++lpre;
         }
         ++s;
+        ++ms;
       }
     }
   }
@@ -500,7 +526,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   if (tid == 0) {
     v.meta[0] = nvalid;
     v.meta[1] = n_useg;
-    v.meta[2] = n_iseg;
+    v.meta[2] = n_mseg;  // item segments K2 serves (= all of them unless k1_items)
     v.meta[3] = min(n_long, kMaxLongItems);
     v.meta[4] = n_multi;
   }
@@ -533,18 +559,22 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // the sorts see only these low bits of it
   const int ub = bits_for(u_rows + 1), ib = bits_for(iloc * world + 1);
   const bool radix = getenv("BPRMF_RADIX_BUILD") != nullptr;  // A/B of the two sorts (tests)
+  // single GPU: items with one reference in a batch are K1's (BPRMF_K1_ITEMS=0: all K2's, A/B);
+  // the trec flag bits 30-31 need item ids below 2^30
+  const char* k1e = getenv("BPRMF_K1_ITEMS");
+  const int k1_items = (!slots && i_rows < (1LL << 30) && !(k1e && k1e[0] == '0')) ? 1 : 0;
   if (B <= kBuildThreads * 4 && !radix)
     k_build_batches<4, true><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
+        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
   else if (B <= kBuildThreads * 4)
     k_build_batches<4, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
+        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
   else
     k_build_batches<8, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
         a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, bb, err, ci);
+        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
   return hipGetLastError();
 }
 

@@ -189,17 +189,21 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
   int32_t u = 0;
   __shared__ float4 s_g[S * kBlock];  // per-triplet user gradients of in-workgroup segments
   if (p < n) {
-    const int32_t i = r.x & 0x7FFFFFFF, j = r.y & 0x7FFFFFFF;  // bit 31: the item's first ref
+    // bit 31: the item's first reference in the batch; bit 30 (single GPU): its ONLY reference,
+    // so this triplet finishes the item (no contribution row, no K2 record)
+    const int32_t i = r.x & 0x3FFFFFFF, j = r.y & 0x3FFFFFFF;
+    const bool soli = !SH && (r.x & 0x40000000), solj = !SH && (r.y & 0x40000000);
     u = r.z;
     w = r.w;
     prow = P.W + (int64_t)u * ld + 4 * sub;
     if (sb.pend_q && sub == 0) {  // this step's rows, for the next step's fused K1
-      // one mark per distinct item (from the triplet holding its first reference) and per user
-      // K2 finishes; write-through (sc1), so no dirty partial lines wait for the kernel boundary
+      // one mark per distinct item K2 updates (from the triplet holding its first reference) and
+      // per user K2 finishes; write-through (sc1), so no dirty partial lines wait for the kernel
+      // boundary.  Rows K1 finishes itself are final before the next launch: no mark.
       const int64_t o = (int64_t)(t & 1);
-      if (r.x < 0)
+      if (r.x < 0 && !soli)
         __hip_atomic_store(sb.pend_q + o * sb.qrows + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (r.y < 0)
+      if (r.y < 0 && !solj)
         __hip_atomic_store(sb.pend_q + o * sb.qrows + j, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w == 0)
         __hip_atomic_store(sb.pend_p + o * sb.prows + u, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -274,9 +278,25 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     SSTAMP(0, 2);
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
     if (sub == 0 && xloss) st_word<WT>(reinterpret_cast<int32_t*>(xloss) + p, __float_as_int(x));  // K2 sums the loss terms
-    float* cb = contrib + (int64_t)p * ld + 4 * sub;
+    if (!(soli && solj)) {  // K2 reads c*P_u for the side(s) it serves
+      float* cb = contrib + (int64_t)p * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) st4o<WT>(cb + 4 * G4 * k, scale4(pu[k], c));
+      for (int k = 0; k < S; ++k) st4o<WT>(cb + 4 * G4 * k, scale4(pu[k], c));
+    }
+    // an item with this one reference: W = V - lr (g + wd V), g = -c P_u (i) / +c P_u (j), the
+    // exact arithmetic of K2's one-term sum (fmaf(-/+1, c P_u, 0) is -/+ c P_u exactly)
+    if (soli) {
+      float* qw = Q.W + (int64_t)i * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) st4o<WT>(qw + 4 * G4 * k, sgd4(vi[k], scale4(scale4(pu[k], c), -1.f), hp.lr, hp.wd));
+      if (sub == 0) st_word<WT>(Q.stamp + i, t);
+    }
+    if (solj) {
+      float* qw = Q.W + (int64_t)j * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) st4o<WT>(qw + 4 * G4 * k, sgd4(vj[k], scale4(pu[k], c), hp.lr, hp.wd));
+      if (sub == 0) st_word<WT>(Q.stamp + j, t);
+    }
     if (w == 1) {  // the user's only triplet: W = V - lr (g + wd V) with g = -c (Q_i - Q_j)
 #pragma unroll
       for (int k = 0; k < S; ++k)

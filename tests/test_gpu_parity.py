@@ -335,6 +335,28 @@ def test_fused_step_equals_separate_kernels_bitwise(rl, golden, monkeypatch, d, 
     assert l0 == l1
 
 
+@pytest.mark.parametrize("d,B,fused", [(32, 4096, "1"), (128, 1000, "1"), (384, 256, "1"),
+                                       (128, 4096, "0"), (8, 64, "1")])
+def test_k1_sole_items_equal_k2_items_bitwise(rl, golden, monkeypatch, d, B, fused):
+    """Items with one reference in a batch finished by K1 from that triplet (default) give the
+    result of K2 finishing every item (BPRMF_K1_ITEMS=0) bit for bit: a one-term sum is that term."""
+    pos, U, I = _ml100k_pos(golden)
+    outs = []
+    monkeypatch.setenv("BPRMF_FUSED", fused)
+    for k1 in ("1", "0"):
+        monkeypatch.setenv("BPRMF_K1_ITEMS", k1)
+        m = _model(rl, U, I, d, B, seed=21)
+        m.set_train(pos)
+        n = m.epoch_size()[1]
+        m.train_steps(0, 0, min(n, 40))
+        st = m.train_steps(1, 3, min(n - 3, 9))
+        outs.append((m.get_weights(), st["loss"]))
+    (P0, Q0), l0 = outs[0]
+    (P1, Q1), l1 = outs[1]
+    assert np.array_equal(P0, P1) and np.array_equal(Q0, Q1)
+    assert l0 == l1
+
+
 def test_step_graphs_equal_eager_launches(rl, golden, monkeypatch):
     """Position-independent step graphs (sizes 64/16 replayed from the device cursor; chunks of
     64 units or more) give the same result as eager launches for chunks of any length at any

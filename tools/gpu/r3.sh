@@ -12,4 +12,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-me
 tail -2 "$out/gpu_tests.log"
 timeout -k 10 240 python bench.py --steps 20 --warmup 5 > "$out/bench20.log" 2>&1 || { tail -5 "$out/bench20.log"; exit 1; }
 grep '^{' "$out/bench20.log"
+timeout -k 10 240 python bench.py --steps 20 --warmup 5 --semantics hogwild --no-cpu-baseline > "$out/bench20_hog.log" 2>&1 || { tail -5 "$out/bench20_hog.log"; exit 1; }
+grep '^{' "$out/bench20_hog.log"
 exit $rc

@@ -37,7 +37,19 @@
 
 namespace bprmf {
 
-static __device__ __forceinline__ float4 hw_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// 16-byte row load past this CU's L1: a non-temporal load (global_load_dwordx4 ... nt) is served
+// by the XCD's L2 (MI355X_MICROARCH.md: sc1 / nt loads bypass L1 only), and the L2 drops every
+// line the XCD stores sc1.  A plain load may hit a line this CU cached long ago: a hot row's, or
+// its stamp's, and a stale stamp then decays the row again on every touch.  (A compiler builtin,
+// so the loads stay visible to its wait counting.)
+static __device__ __forceinline__ float4 hw_ld4(const float* p) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  return make_float4(x[0], x[1], x[2], x[3]);
+}
+static __device__ __forceinline__ int32_t hw_ld_word(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 dword load
+}
 
 // write-through (sc1) 16-byte store: the line leaves and is dropped from the XCD's L2
 static __device__ __forceinline__ void hw_st4(float* p, float4 v) {
@@ -146,9 +158,9 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
             vi[r][k] = hw_ld4(qi + 4 * G4 * k);
             vj[r][k] = hw_ld4(qj + 4 * G4 * k);
           }
-          su[r] = P.stamp[uu[r]];
-          si[r] = Q.stamp[ii[r]];
-          sj[r] = Q.stamp[jj[r]];
+          su[r] = hw_ld_word(P.stamp + uu[r]);
+          si[r] = hw_ld_word(Q.stamp + ii[r]);
+          sj[r] = hw_ld_word(Q.stamp + jj[r]);
         } else {
           su[r] = si[r] = sj[r] = 0;
 #pragma unroll
@@ -243,6 +255,10 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   const int wpb = kBlock / 64;
   int64_t blocks = serial ? 1 : (waves + wpb - 1) / wpb;
   if (blocks > kMaxGridBlocks) blocks = kMaxGridBlocks;  // grid-stride beyond
+  if (const char* e = getenv("BPRMF_HOGWILD_BLOCKS")) {  // A/B: cap the grid (smaller window)
+    const int64_t cap = atoll(e);
+    if (cap > 0 && blocks > cap) blocks = cap;
+  }
   const unsigned threads = serial ? 64 : kBlock;
   SamplerArgs a{};
   if (sa) a = *sa;

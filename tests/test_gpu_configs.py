@@ -9,7 +9,7 @@
       single-GPU run of the global batches (each step's union of the shards' batches, B=8192),
       whose sampled triplets are the shard samplers' (bit-exact to the oracle's, tested here).
   C4  NCF at ml-20m shape, d=64, 3 layers (NCFRecommender.py:27-124,255-260), full-size tables:
-      two batches of forward + gradients + Adam against oracle/ncf_oracle.py, and the NCF
+      one batch of forward + gradients + Adam against oracle/ncf_oracle.py, and the NCF
       sampler (NCFData.ng_sample, util/data_loader.py:931-972) bit-exact on slices.
   C5  10M users x 100M items, d=256, one GPU (tables 112.6 GB in HBM; row offsets past 2^32
       floats): sampler slices bit-exact at both ends of the epoch; 3 device-sampled steps
@@ -157,30 +157,41 @@ def test_c3_per_rank_shape_sharded_equals_single_gpu_global_batch(rl):
 
 
 # ---- C4: NCF at ml-20m shape, d=64, 3 layers ---------------------------------------------------
-def test_c4_ncf_ml20m_shape_steps_vs_oracle(rl):
+def test_c4_ncf_ml20m_shape_step_vs_oracle(rl):
+    """One NeuMF-end Adam step on the full-size tables against the float64 oracle.
+    Forward and loss: to f32 rounding.  Parameters: Adam's first step moves every element with a
+    nonzero gradient by ~lr * sign(g) (NCFRecommender.py:259-260, torch Adam), so an element whose
+    gradient is within f32 noise of zero can move the other way: the GPU result (measured: 665 of
+    the 131,072 layer-1 weights, 0.5 %) may differ there by up to 2 lr.  Bounded: at most 1 % of a
+    parameter's elements beyond 5e-5, none beyond 2 lr (+ rounding).  Later steps compound those
+    flips through the forward (Adam is scale-free), so one step is what is compared."""
     _free()
-    U, I, d, L, B = 138493, 26744, 64, 3, 256
+    U, I, d, L, B, lr = 138493, 26744, 64, 3, 256, 0.001
     g = np.random.default_rng(44)
-    m = rl.NCF(U, I, d, L, batch_size=B, seed=9)
+    m = rl.NCF(U, I, d, L, batch_size=B, seed=9, lr=lr)
     params = m.state_dict()
     assert params["embed_user_MLP.weight"].shape == (U, d * 2 ** (L - 1))
-    opt = N.Adam(params)
-    for k in range(2):
-        u = g.integers(0, U, B)
-        i = g.integers(0, I, B)
-        u[:20] = 5  # a repeated user and item (summed gradients)
-        i[10:40] = 11
-        y = (g.random(B) < 0.2).astype(np.float32)
-        z = m.predict_logits(u, i)
-        z_ref, _ = N.forward(params, "NeuMF-end", L, u, i)
-        np.testing.assert_allclose(z, z_ref, rtol=1e-4, atol=2e-6)
-        grads, loss = N.grads(params, "NeuMF-end", L, u, i, y)
-        params = opt.step(params, grads)
-        st = m.train_samples(u, i, y)
-        assert abs(st["loss"] - loss) < 1e-5
+    opt = N.Adam(params, lr=lr)
+    u = g.integers(0, U, B)
+    i = g.integers(0, I, B)
+    u[:20] = 5  # a repeated user and item (summed gradients)
+    i[10:40] = 11
+    y = (g.random(B) < 0.2).astype(np.float32)
+    z = m.predict_logits(u, i)
+    z_ref, _ = N.forward(params, "NeuMF-end", L, u, i)
+    np.testing.assert_allclose(z, z_ref, rtol=1e-5, atol=1e-7)
+    grads, loss = N.grads(params, "NeuMF-end", L, u, i, y)
+    params = opt.step(params, grads)
+    st = m.train_samples(u, i, y)
+    assert abs(st["loss"] - loss) < 1e-6
     got = m.state_dict()
     for n in m.names:
-        np.testing.assert_allclose(got[n], params[n], rtol=0, atol=5e-5, err_msg=n)
+        dd = np.abs(got[n].astype(np.float64) - params[n])
+        assert dd.max() <= 2 * lr * 1.001 + 1e-7, (n, dd.max())
+        assert np.mean(dd > 5e-5) <= 0.01, (n, np.mean(dd > 5e-5))
+    z1 = m.predict_logits(u, i)
+    z1_ref, _ = N.forward(params, "NeuMF-end", L, u, i)
+    assert np.abs(z1 - z1_ref).max() < 5e-4
     m.close()
 
 

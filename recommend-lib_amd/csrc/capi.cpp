@@ -632,6 +632,16 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     // own (hogwild.hip); the loss goes to the segmented path's kSegLossSlots slots
     if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
     const SamplerArgs sa = sampler_args(h);
+    const char* pre = getenv("BPRMF_HOGWILD_PRESAMPLE");  // A/B: k_sample first, then replay
+    if (!ru && pre && pre[0] == '1') {
+      if (int r = ensure_trip(h, n)) return r;
+      int32_t* tu = h->d_trip;
+      HIPCHK(sample(sa, epoch, first_slot, n, tu, tu + h->trip_cap, tu + 2 * h->trip_cap, h->d_err,
+                    h->stream));
+      ru = tu;
+      ri = tu + h->trip_cap;
+      rj = tu + 2 * h->trip_cap;
+    }
     {
       hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
       if (ea) HIPCHK(hipEventRecord(ea, h->stream));

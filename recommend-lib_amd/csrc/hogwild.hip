@@ -15,9 +15,9 @@
 //     only on the row's first touch in step t (s < t), so every row decays once per step as torch's
 //     SGD does; a row already at a later step (s >= t, touched by a later batch in flight) is
 //     neither decayed nor re-stamped (stamps only move forward);
-//   - staleness is bounded by the launch's in-flight window: a wave takes `tpw` consecutive slots,
-//     all waves of the grid start together, so a triplet may run beside any triplet up to
-//     grid_waves * tpw slots away (DESIGN.md §5b gives the window per shape).
+//   - staleness is bounded by the launch's in-flight window: at most ~min(U, I) triplets are in
+//     flight at once (the grid is capped to that), so a row sees about one other update in flight
+//     whatever the table size; a wave takes `tpw` consecutive slots.
 // Coherence: row and stamp stores are write-through (sc1) — the line leaves the XCD's L2 and is
 // dropped there — so no XCD keeps a dirty or long-lived stale copy of a row another XCD updates;
 // a reader sees another XCD's update at most one read-modify-write window late (MI355X_MICROARCH.md
@@ -26,8 +26,11 @@
 // Work layout: lane l of a wave samples slot base + l itself (the device sampler's spec,
 // device_common.h: Philox + Feistel shuffle + k-th non-member; bit-exact to k_sample), so no
 // triplet array makes a round trip through HBM; the wave then walks its tpw triplets G4 lanes per
-// triplet (one float4 per lane and stripe), kUnroll * (64 / G4) triplets' rows in flight at once.
+// triplet (one float4 per lane and stripe), two rounds of kHwUnroll * (64 / G4) triplets' rows in
+// flight at once (double-buffered: the next round's loads go out before this round's stores).
 #include <stdlib.h>
+
+#include <algorithm>
 
 #include "device_common.h"
 
@@ -96,26 +99,151 @@ static __device__ __forceinline__ void hw_sample(const SamplerArgs& a, uint32_t 
   }
 }
 
-constexpr int kHwUnroll = 4;  // rounds of (64 / G4) triplets whose rows are in flight together
+constexpr int kHwUnroll = 2;  // triplets per lane group per round (rows in flight per buffer)
+
+// One round of a wave: kHwUnroll triplets per lane group, their ids, stamps and rows.
+template <int S, int UNR>
+struct HwRound {
+  float4 pu[UNR][S], vi[UNR][S], vj[UNR][S];
+  int32_t su[UNR], si[UNR], sj[UNR], uu[UNR], ii[UNR], jj[UNR];
+  bool ok[UNR];
+};
+
+// issue the round starting at slot k0 of the wave's chunk (ids from the lanes that sampled them)
+template <int G4, int S, int UNR, int GPW, bool SERIAL>
+static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
+                                               int32_t mi, int32_t mj, const Table& P,
+                                               const Table& Q, int ld, int sub, int gw, int fl) {
+  const bool nt = fl & 1, noload = fl & 2;
+#pragma unroll
+  for (int r = 0; r < UNR; ++r) {
+    const int src = k0 + r * GPW + gw;
+    R.uu[r] = __shfl(mu, src & 63);
+    R.ii[r] = __shfl(mi, src & 63);
+    R.jj[r] = __shfl(mj, src & 63);
+    R.ok[r] = (SERIAL ? gw == 0 : true) && src < cnt && R.uu[r] >= 0;
+    if (R.ok[r] && !noload) {
+      const float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
+      const float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
+      const float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        if (nt) {
+          R.pu[r][k] = hw_ld4(pr + 4 * G4 * k);
+          R.vi[r][k] = hw_ld4(qi + 4 * G4 * k);
+          R.vj[r][k] = hw_ld4(qj + 4 * G4 * k);
+        } else {
+          R.pu[r][k] = *reinterpret_cast<const float4*>(pr + 4 * G4 * k);
+          R.vi[r][k] = *reinterpret_cast<const float4*>(qi + 4 * G4 * k);
+          R.vj[r][k] = *reinterpret_cast<const float4*>(qj + 4 * G4 * k);
+        }
+      }
+      R.su[r] = hw_ld_word(P.stamp + R.uu[r]);
+      R.si[r] = hw_ld_word(Q.stamp + R.ii[r]);
+      R.sj[r] = hw_ld_word(Q.stamp + R.jj[r]);
+    } else {
+      R.su[r] = R.si[r] = R.sj[r] = 0;
+#pragma unroll
+      for (int k = 0; k < S; ++k) R.pu[r][k] = R.vi[r][k] = R.vj[r][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// compute and store the round at slot k0 (slot base + k0 + ... of step t0 + 1 + slot / B)
+template <int G4, int S, int UNR, int GPW, bool SERIAL>
+static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base, int k0,
+                                                const Table& P, const Table& Q, const Hyper& hp,
+                                                int ld, int32_t t0, int B, int sub, int gw,
+                                                float& lacc, int fl) {
+  const float lr = hp.lr, wd = hp.wd;
+  const bool nostore = fl & 4;
+  const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
+#pragma unroll
+  for (int r = 0; r < UNR; ++r) {
+    const int src = k0 + r * GPW + gw;
+    const int32_t t = t0 + 1 + (int32_t)((uint32_t)(base + src) / (uint32_t)B);  // chunks < 2^31 slots
+    // first touch of the row in step t: decay to t - 1 and take the wd term; else neither
+    const bool fu1 = R.su[r] < t, fi1 = R.si[r] < t, fj1 = R.sj[r] < t;
+    const float fu = fu1 ? decay_pow(hp.log2a, t - 1 - R.su[r]) : 1.f;
+    const float fi = fi1 ? decay_pow(hp.log2a, t - 1 - R.si[r]) : 1.f;
+    const float fj = fj1 ? decay_pow(hp.log2a, t - 1 - R.sj[r]) : 1.f;
+    float di = 0.f, dj = 0.f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      float4& pu = R.pu[r][k];
+      float4& vi = R.vi[r][k];
+      float4& vj = R.vj[r][k];
+      pu = make_float4(pu.x * fu, pu.y * fu, pu.z * fu, pu.w * fu);
+      vi = make_float4(vi.x * fi, vi.y * fi, vi.z * fi, vi.w * fi);
+      vj = make_float4(vj.x * fj, vj.y * fj, vj.z * fj, vj.w * fj);
+      di = hw_dot4(pu, vi, di);
+      dj = hw_dot4(pu, vj, dj);
+    }
+    // the group's lanes are in one wave: the butterfly needs every lane of the wave, so it runs
+    // whatever ok[] says (inactive groups carry zeros)
+    di = group_sum<G4>(R.ok[r] ? di : 0.f);
+    dj = group_sum<G4>(R.ok[r] ? dj : 0.f);
+    if (!R.ok[r] || nostore) continue;
+    const float x = di - dj;
+    const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
+    if (sub == 0) lacc += softplus(-x);       // -log sigmoid(x)
+    float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
+    float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
+    float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const float4 pu = R.pu[r][k], vi = R.vi[r][k], vj = R.vj[r][k];
+      const float4 gu = make_float4(-c * (vi.x - vj.x), -c * (vi.y - vj.y), -c * (vi.z - vj.z),
+                                    -c * (vi.w - vj.w));
+      const float4 gi = make_float4(-c * pu.x, -c * pu.y, -c * pu.z, -c * pu.w);
+      const float4 gj = make_float4(c * pu.x, c * pu.y, c * pu.z, c * pu.w);
+      if (plainst) {
+        if (!nousers) *reinterpret_cast<float4*>(pr + 4 * G4 * k) = hw_sgd(pu, gu, lr, fu1 ? wd : 0.f);
+        if (!noitems) {
+          *reinterpret_cast<float4*>(qi + 4 * G4 * k) = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f);
+          *reinterpret_cast<float4*>(qj + 4 * G4 * k) = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
+        }
+        continue;
+      }
+      if (!nousers) hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
+      if (!noitems) {
+        hw_st4(qi + 4 * G4 * k, hw_sgd(vi, gi, lr, fi1 ? wd : 0.f));
+        hw_st4(qj + 4 * G4 * k, hw_sgd(vj, gj, lr, fj1 ? wd : 0.f));
+      }
+    }
+    if (sub == 0) {
+      if (fu1) hw_st_word(P.stamp + R.uu[r], t);
+      if (fi1) hw_st_word(Q.stamp + R.ii[r], t);
+      if (fj1) hw_st_word(Q.stamp + R.jj[r], t);
+    }
+    if (SERIAL) {  // the next triplet reads these rows: stores done, this CU's L1 dropped
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+}
 
 // SAMPLE: slots come from the device sampler (a, epoch, slot0 + s); else replayed ids tu/ti/tj[s].
 // SERIAL (tests): one lane group, one triplet at a time, in slot order (launched as one wave).
+// Rounds are double-buffered: round k+1's loads are issued BEFORE round k's stores, so waiting
+// for them does not wait for round k's write-through acknowledgements (gfx9 counts stores in
+// vmcnt, in order with the loads).
 template <int G4, int S, bool SAMPLE, bool SERIAL>
 __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoch, int64_t slot0,
                                                     const int32_t* __restrict__ tu,
                                                     const int32_t* __restrict__ ti,
                                                     const int32_t* __restrict__ tj, int64_t n,
                                                     Table P, Table Q, Hyper hp, int ld, int32_t t0,
-                                                    int B, int tpw, double* __restrict__ loss,
+                                                    int B, int tpw, int fl, double* __restrict__ loss,
                                                     int32_t* __restrict__ err) {
-  constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round
+  constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round and unroll step
   constexpr int UNR = SERIAL ? 1 : kHwUnroll;
+  constexpr int STEP = GPW * UNR;
   const int lane = threadIdx.x & 63;
   const int sub = lane & (G4 - 1);
   const int gw = lane / G4;
   const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
-  const float lr = hp.lr, wd = hp.wd;
   float lacc = 0.f;
   for (int64_t base = wave * tpw; base < n; base += nwaves * tpw) {
     const int cnt = (int)min<int64_t>(tpw, n - base);
@@ -136,86 +264,22 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
         mu = -1;
       }
     }
-    for (int k0 = 0; k0 < cnt; k0 += GPW * UNR) {
-      float4 pu[UNR][S], vi[UNR][S], vj[UNR][S];
-      int32_t su[UNR], si[UNR], sj[UNR], uu[UNR], ii[UNR], jj[UNR];
-      bool ok[UNR];
-      // every round's ids, rows and stamps requested before any is used
-#pragma unroll
-      for (int r = 0; r < UNR; ++r) {
-        const int src = k0 + r * GPW + gw;
-        uu[r] = __shfl(mu, src & 63);
-        ii[r] = __shfl(mi, src & 63);
-        jj[r] = __shfl(mj, src & 63);
-        ok[r] = (SERIAL ? gw == 0 : true) && src < cnt && uu[r] >= 0;
-        if (ok[r]) {
-          const float* pr = P.W + (int64_t)uu[r] * ld + 4 * sub;
-          const float* qi = Q.W + (int64_t)ii[r] * ld + 4 * sub;
-          const float* qj = Q.W + (int64_t)jj[r] * ld + 4 * sub;
-#pragma unroll
-          for (int k = 0; k < S; ++k) {
-            pu[r][k] = hw_ld4(pr + 4 * G4 * k);
-            vi[r][k] = hw_ld4(qi + 4 * G4 * k);
-            vj[r][k] = hw_ld4(qj + 4 * G4 * k);
-          }
-          su[r] = hw_ld_word(P.stamp + uu[r]);
-          si[r] = hw_ld_word(Q.stamp + ii[r]);
-          sj[r] = hw_ld_word(Q.stamp + jj[r]);
-        } else {
-          su[r] = si[r] = sj[r] = 0;
-#pragma unroll
-          for (int k = 0; k < S; ++k) pu[r][k] = vi[r][k] = vj[r][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+    HwRound<S, UNR> A, Bf;
+    if (SERIAL) {  // each triplet reads what the one before it stored: no prefetch
+      for (int k0 = 0; k0 < cnt; k0 += STEP) {
+        hw_load<G4, S, UNR, GPW, SERIAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+        hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
       }
-#pragma unroll
-      for (int r = 0; r < UNR; ++r) {
-        const int src = k0 + r * GPW + gw;
-        const int32_t t = t0 + 1 + (int32_t)((base + src) / B);
-        // first touch of the row in step t: decay to t - 1 and take the wd term; else neither
-        const bool fu1 = su[r] < t, fi1 = si[r] < t, fj1 = sj[r] < t;
-        const float fu = fu1 ? decay_pow(hp.log2a, t - 1 - su[r]) : 1.f;
-        const float fi = fi1 ? decay_pow(hp.log2a, t - 1 - si[r]) : 1.f;
-        const float fj = fj1 ? decay_pow(hp.log2a, t - 1 - sj[r]) : 1.f;
-        float di = 0.f, dj = 0.f;
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-          pu[r][k] = make_float4(pu[r][k].x * fu, pu[r][k].y * fu, pu[r][k].z * fu, pu[r][k].w * fu);
-          vi[r][k] = make_float4(vi[r][k].x * fi, vi[r][k].y * fi, vi[r][k].z * fi, vi[r][k].w * fi);
-          vj[r][k] = make_float4(vj[r][k].x * fj, vj[r][k].y * fj, vj[r][k].z * fj, vj[r][k].w * fj);
-          di = hw_dot4(pu[r][k], vi[r][k], di);
-          dj = hw_dot4(pu[r][k], vj[r][k], dj);
-        }
-        // the group's lanes are in one wave: the butterfly needs every lane of the wave, so it
-        // runs whatever ok[] says (inactive groups carry zeros)
-        di = group_sum<G4>(ok[r] ? di : 0.f);
-        dj = group_sum<G4>(ok[r] ? dj : 0.f);
-        if (!ok[r]) continue;
-        const float x = di - dj;
-        const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
-        if (sub == 0) lacc += softplus(-x);       // -log sigmoid(x)
-        float* pr = P.W + (int64_t)uu[r] * ld + 4 * sub;
-        float* qi = Q.W + (int64_t)ii[r] * ld + 4 * sub;
-        float* qj = Q.W + (int64_t)jj[r] * ld + 4 * sub;
-#pragma unroll
-        for (int k = 0; k < S; ++k) {
-          const float4 gu = make_float4(-c * (vi[r][k].x - vj[r][k].x), -c * (vi[r][k].y - vj[r][k].y),
-                                        -c * (vi[r][k].z - vj[r][k].z), -c * (vi[r][k].w - vj[r][k].w));
-          const float4 gi = make_float4(-c * pu[r][k].x, -c * pu[r][k].y, -c * pu[r][k].z, -c * pu[r][k].w);
-          const float4 gj = make_float4(c * pu[r][k].x, c * pu[r][k].y, c * pu[r][k].z, c * pu[r][k].w);
-          hw_st4(pr + 4 * G4 * k, hw_sgd(pu[r][k], gu, lr, fu1 ? wd : 0.f));
-          hw_st4(qi + 4 * G4 * k, hw_sgd(vi[r][k], gi, lr, fi1 ? wd : 0.f));
-          hw_st4(qj + 4 * G4 * k, hw_sgd(vj[r][k], gj, lr, fj1 ? wd : 0.f));
-        }
-        if (sub == 0) {
-          if (fu1) hw_st_word(P.stamp + uu[r], t);
-          if (fi1) hw_st_word(Q.stamp + ii[r], t);
-          if (fj1) hw_st_word(Q.stamp + jj[r], t);
-        }
-        if (SERIAL) {  // the next triplet reads these rows: stores done, this CU's L1 dropped
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-      }
+      continue;
+    }
+    hw_load<G4, S, UNR, GPW, SERIAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+    for (int k0 = 0; k0 < cnt; k0 += 2 * STEP) {
+      const bool more1 = k0 + STEP < cnt, more2 = k0 + 2 * STEP < cnt;
+      if (more1) hw_load<G4, S, UNR, GPW, SERIAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+      hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
+      if (!more1) break;
+      if (more2) hw_load<G4, S, UNR, GPW, SERIAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+      hw_apply<G4, S, UNR, GPW, SERIAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
     }
   }
   // the wave's loss into one of kSegLossSlots f64 slots (no-return atomics; order is not fixed,
@@ -255,26 +319,45 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   const int wpb = kBlock / 64;
   int64_t blocks = serial ? 1 : (waves + wpb - 1) / wpb;
   if (blocks > kMaxGridBlocks) blocks = kMaxGridBlocks;  // grid-stride beyond
-  if (const char* e = getenv("BPRMF_HOGWILD_BLOCKS")) {  // A/B: cap the grid (smaller window)
+  // Staleness window: at most ~min(U, I) triplets in flight (each wave holds 64/G4 * kHwUnroll),
+  // so a row sees about one other update in flight at a time whatever the table size.  Measured
+  // (ml-100k, d=32: 943 x 1,682 rows): ~1k in flight trains like the exact step, ~8k (64
+  // workgroups) barely trains (lost updates on every row); ml-20m (26,744 items) at the full grid
+  // (~24k resident) matches the exact step's HR@10.  BPRMF_HOGWILD_WINDOW overrides (triplets),
+  // BPRMF_HOGWILD_BLOCKS caps the grid directly (A/B).
+  {
+    int64_t window = std::min<int64_t>(P.rows, Q.rows);
+    if (const char* e = getenv("BPRMF_HOGWILD_WINDOW")) window = std::max<int64_t>(1, atoll(e));
+    const int64_t per_block = (int64_t)wpb * (64 / g.G4) * 2 * kHwUnroll;  // two rounds in flight
+    const int64_t cap = std::max<int64_t>(1, (window + per_block - 1) / per_block);
+    if (blocks > cap) blocks = cap;
+  }
+  if (const char* e = getenv("BPRMF_HOGWILD_BLOCKS")) {
     const int64_t cap = atoll(e);
     if (cap > 0 && blocks > cap) blocks = cap;
   }
   const unsigned threads = serial ? 64 : kBlock;
+  // row loads past L1 (nt) by default; BPRMF_HOGWILD_PLAIN=1: plain loads (A/B)
+  const char* pl = getenv("BPRMF_HOGWILD_PLAIN");
+  int fl = (pl && pl[0] == '1') ? 0 : 1;
+  // diagnostic timing only (wrong results): bit 1 = no row loads, bit 2 = no row stores, bit 3 =
+  // plain (write-back) row stores, bit 4 = no item row stores, bit 5 = no user row stores
+  if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 62);
   SamplerArgs a{};
   if (sa) a = *sa;
   BPRMF_DISPATCH4(g, ({
     if (serial && sa)
       k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                          g.ld, t0, B, tpw, loss, err);
+                                                          g.ld, t0, B, tpw, fl, loss, err);
     else if (serial)
       k_hogwild<G4_, S_, false, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                           g.ld, t0, B, tpw, loss, err);
+                                                           g.ld, t0, B, tpw, fl, loss, err);
     else if (sa)
       k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
     else
       k_hogwild<G4_, S_, false, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
   }));
   return hipGetLastError();
 }

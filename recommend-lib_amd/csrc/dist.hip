@@ -16,6 +16,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "dist_body.h"
 
 namespace bprmf {
 
@@ -98,46 +99,14 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
   }
 }
 
-// owner: rows requested by every peer for step k, brought to step t-1: the row of position
-// (p, idx) goes to dst.to[p] + idx * ld (packed send blocks, this rank's own slots, or -- IPC
-// transport -- straight into peer p's landing buffer).  With dst.done set (IPC), the grid is a
-// bounded grid-stride loop and the last workgroup to finish raises each peer's row flag to the
-// step number once every workgroup's stores are acknowledged.
 template <int G4, int S>
 __global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t* __restrict__ ids_recv,
                                                         int64_t n, int world, int cap, int k,
                                                         Hyper hp, int ld,
                                                         const int32_t* __restrict__ tbase,
                                                         PushArgs dst, uint32_t* __restrict__ done) {
-  constexpr int NG = kBlock / G4;
-  const int sub = threadIdx.x & (G4 - 1);
-  const int32_t t = *tbase + k + 1;
-  for (int64_t x = blockIdx.x * (int64_t)NG + threadIdx.x / G4; x < (int64_t)world * cap;
-       x += (int64_t)gridDim.x * NG) {
-    const int p = (int)(x / cap), idx = (int)(x % cap);
-    const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
-    if ((uint32_t)row >= (uint32_t)Q.rows) continue;
-    const float* w = Q.W + (int64_t)row * ld + 4 * sub;
-    float4 v[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
-    const float f = decay_pow(hp.log2a, t - 1 - Q.stamp[row]);
-    float* o = static_cast<float*>(dst.dst[p]) + (int64_t)idx * ld + 4 * sub;
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
-  }
-  if (!done) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int p = 0; p < world; ++p)
-        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  owner_gather_body<G4, S>(blockIdx.x, gridDim.x, Q, ids_recv, n, world, cap, k, hp, ld, tbase, dst,
+                           done);
 }
 
 // owner: for each distinct row of step k (its leader position) sum the peers' gradients in peer
@@ -203,12 +172,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_apply(Table Q, const int32_t* 
   if (sub == 0) Q.stamp[row] = t;
 }
 
-// Fused owner step: apply step k (as k_owner_apply) and gather step k+1 (as k_owner_gather) in one
-// launch.  A row step k applies is served to step k+1's requesters by its leader, from the value
-// it just stored (gdep); rows step k does not apply are gathered by their own groups (gfree).  No
-// row is both read by a free gather and written by an apply, so the groups are independent.
-// With done set (IPC), a bounded grid-stride grid and the last workgroup raises the peers' row
-// flags to step k+1.
+// Fused owner step (dist_body.h owner_step_body): apply step k and gather step k+1 in one launch.
 template <int G4, int S>
 __global__ __launch_bounds__(kBlock) void k_owner_step(Table Q, const int32_t* __restrict__ ids_recv,
                                                       const int32_t* __restrict__ aplan,
@@ -221,94 +185,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_step(Table Q, const int32_t* _
                                                       const int32_t* __restrict__ wait_flags,
                                                       int32_t* __restrict__ err, PushArgs dst,
                                                       uint32_t* __restrict__ done) {
-  constexpr int NG = kBlock / G4;
-  const int sub = threadIdx.x & (G4 - 1);
-  const int32_t t = *tbase + k + 1;
-  wait_peer_flags(wait_flags, world, self, t, err);  // IPC: the peers' gradients of step k
-  const int64_t WC = (int64_t)world * cap;
-  const float lr = hp.lr, wd = hp.wd;
-  for (int64_t x = blockIdx.x * (int64_t)NG + threadIdx.x / G4; x < 2 * WC; x += (int64_t)gridDim.x * NG) {
-    if (x < WC) {  // apply: the leader position of a row of step k
-      const int32_t* rec = aplan + ((int64_t)k * WC + x) * world;
-      const int32_t r0 = rec[0];
-      if (r0 == -2) continue;
-      const int p = (int)(x / cap), idx = (int)(x % cap);
-      const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
-      float* w = Q.W + (int64_t)row * ld + 4 * sub;
-      float4 cur[S], g[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        cur[s] = ld4(w + 4 * G4 * s);
-        g[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      const int32_t stamp = Q.stamp[row];
-      for (int q0 = 0; q0 < world; q0 += 8) {  // peers' rows in flight, summed in peer order
-        int32_t pos[8];
-        float4 gr[8][S];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          pos[m] = q0 + m < world ? (q0 + m == 0 ? r0 : rec[q0 + m]) : -1;
-          if (pos[m] >= 0) {
-            const int q = pos[m] / cap, i = pos[m] - q * cap;
-            const float* gp = (q == self ? self_grads + (int64_t)i * ld : grads_recv + (int64_t)pos[m] * ld) + 4 * sub;
-#pragma unroll
-            for (int s = 0; s < S; ++s) gr[m][s] = ld4(gp + 4 * G4 * s);
-          }
-        }
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-          if (pos[m] >= 0) {
-#pragma unroll
-            for (int s = 0; s < S; ++s)
-              g[s] = make_float4(g[s].x + gr[m][s].x, g[s].y + gr[m][s].y, g[s].z + gr[m][s].z,
-                                 g[s].w + gr[m][s].w);
-          }
-      }
-      const float f = decay_pow(hp.log2a, t - 1 - stamp);
-      float4 nv[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const float4 v = make_float4(cur[s].x * f, cur[s].y * f, cur[s].z * f, cur[s].w * f);
-        nv[s] = make_float4(fmaf(-lr, fmaf(wd, v.x, g[s].x), v.x), fmaf(-lr, fmaf(wd, v.y, g[s].y), v.y),
-                            fmaf(-lr, fmaf(wd, v.z, g[s].z), v.z), fmaf(-lr, fmaf(wd, v.w, g[s].w), v.w));
-        st4(w + 4 * G4 * s, nv[s]);
-      }
-      if (sub == 0) Q.stamp[row] = t;
-      const int32_t* dep = gdep + ((int64_t)k * WC + x) * world;
-      for (int q = 0; q < world; ++q) {  // step k+1's requests of this row: the new value
-        const int32_t i2 = dep[q];
-        if (i2 < 0) continue;
-        float* o = static_cast<float*>(dst.dst[q]) + (int64_t)i2 * ld + 4 * sub;
-#pragma unroll
-        for (int s = 0; s < S; ++s) st4(o + 4 * G4 * s, nv[s]);
-      }
-    } else {  // gather: a position of step k+1 whose row step k does not apply
-      const int64_t y = x - WC;
-      if (!gfree[(int64_t)(k + 1) * WC + y]) continue;
-      const int q = (int)(y / cap), idx = (int)(y % cap);
-      const int32_t row = ids_recv[((int64_t)q * n + k + 1) * cap + idx];
-      const float* w = Q.W + (int64_t)row * ld + 4 * sub;
-      float4 v[S];
-#pragma unroll
-      for (int s = 0; s < S; ++s) v[s] = ld4(w + 4 * G4 * s);
-      const float f = decay_pow(hp.log2a, t - Q.stamp[row]);  // brought to step (t + 1) - 1
-      float* o = static_cast<float*>(dst.dst[q]) + (int64_t)idx * ld + 4 * sub;
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
-    }
-  }
-  if (!done) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int p = 0; p < world; ++p)
-        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  owner_step_body<G4, S>(blockIdx.x, gridDim.x, Q, ids_recv, aplan, gdep, gfree, n, world, cap, k, hp,
+                         ld, tbase, grads_recv, self, self_grads, wait_flags, err, dst, done);
 }
 
 // ---- IPC transport: blocks pushed straight into the peers' buffers over xGMI ----------------

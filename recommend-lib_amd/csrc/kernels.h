@@ -266,6 +266,38 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
                          hipStream_t s);
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
                            int32_t* gdep, int32_t* gfree, hipStream_t s);
+// ---- the fused sharded step over the IPC transport (step.hip; two launches per step) ----
+// K2 whose per-slot gradients go straight to the owners: slot s of owner p = s / S lands at
+// dst[p] + (s % S) * ld; once every workgroup's stores are acknowledged the launch's last
+// workgroup raises flag[p] (non-null) to the step number; done: [9] counters, zero between launches
+struct GradRoute {
+  float* dst[kMaxWorld];
+  int32_t* flag[kMaxWorld];
+  int S = 0, world = 1;
+  uint32_t* done = nullptr;
+};
+hipError_t item_step_push(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                          const int32_t* tbase, int step, float* contrib, float* ugrad, float* xloss,
+                          double* loss, const GradRoute& gr, hipStream_t s);
+// the owner phase's arguments (dist.hip k_owner_gather / k_owner_step)
+struct OwnerArgs {
+  const int32_t* ids_recv = nullptr;
+  const int32_t* aplan = nullptr;
+  const int32_t* gdep = nullptr;
+  const int32_t* gfree = nullptr;
+  int64_t n = 0;
+  int world = 1, cap = 0, self = 0;
+  const float* grads_recv = nullptr;
+  const float* self_grads = nullptr;
+  const int32_t* wait_flags = nullptr;
+  PushArgs dst;
+  uint32_t* done = nullptr;
+};
+// owner phase of step `step` of the chunk (0: gather step 0; else apply step-1 and gather step)
+// in the first workgroups, K1 of `step` (sharded, waiting for every rank's row flags) in the rest
+hipError_t dist_front(const Geom& g, const OwnerArgs& o, BatchView bv, int B, Table P, Table Q,
+                      const Hyper& hp, const int32_t* tbase, int step, float* contrib, float* ugrad,
+                      float* xloss, const float* item_rows, const PeerWait& pw, hipStream_t s);
 // apply step k and gather step k+1 in one launch (dist.hip k_owner_step)
 hipError_t dist_owner_step(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                            const int32_t* gdep, const int32_t* gfree, int64_t n, int world, int cap,

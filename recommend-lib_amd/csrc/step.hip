@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "dist_body.h"
 
 // The in-launch hand-off below uses gfx94x/gfx950 cache-policy bits (sc1 stores and loads) and
 // the CDNA3/4 L2-per-XCD coherence model; no other target is built or supported.
@@ -380,9 +381,18 @@ template <int G4, int S, bool SH, bool WT, bool PUB>
 static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int slot,
                                                    const float4 (&g)[S], const ItemRow<G4, S, SH>& row,
                                                    const Hyper& hp, int ld, int32_t t, int sub,
-                                                   float* __restrict__ grads) {
+                                                   float* __restrict__ grads,
+                                                   const GradRoute* gr = nullptr) {
   if (SH) {
-    float* o = grads + (int64_t)slot * ld + 4 * sub;
+    // per-slot gradient: the exchange's send buffer, or (gr: fused IPC step) straight into its
+    // owner's landing buffer
+    float* o;
+    if (gr) {
+      const int p = slot / gr->S;
+      o = gr->dst[p] + (int64_t)(slot - p * gr->S) * ld + 4 * sub;
+    } else {
+      o = grads + (int64_t)slot * ld + 4 * sub;
+    }
 #pragma unroll
     for (int k = 0; k < S; ++k) st4o<WT>(o + 4 * G4 * k, g[k]);
   } else {
@@ -429,7 +439,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, int long_blocks, int item_blocks,
                                                float* __restrict__ grads, double* __restrict__ loss,
-                                               int B) {
+                                               int B, const GradRoute* gr = nullptr) {
   constexpr int NG = KB / G4;
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = PUB || !kFusedStampsOnly;
@@ -541,7 +551,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
 #pragma unroll
       for (int k = 0; k < S; ++k) g[k] = part[0][sub + G4 * k];
       SSTAMP(1, 2);
-      finish_item<G4, S, SH, WT, PUB>(Q, item, r0.w, g, row, hp, ld, t, sub, grads);
+      finish_item<G4, S, SH, WT, PUB>(Q, item, r0.w, g, row, hp, ld, t, sub, grads, gr);
     }
     SSTAMP(1, 3);
     return;
@@ -600,7 +610,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     }
   }
   SSTAMP(1, 2);
-  finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads);  // SH: item field = slot
+  finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads, gr);  // SH: item field = slot
   SSTAMP(1, 3);
 }
 
@@ -640,6 +650,65 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
   else
     k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
                                       hp, ld, t + 1, sb, nullptr, B, err);
+}
+
+// ---- the fused sharded step over the IPC transport (dist.cpp enqueue_steps, two launches/step) ----
+// Back: K2 of step t (sharded: per-slot gradients) written straight into the owners' landing
+// buffers (GradRoute), then a two-level completion count (per XCD-parity group of workgroups, then
+// the groups) so the launch's last workgroup, once every workgroup's stores are acknowledged,
+// raises each peer's gradient flag to t (the pattern of dist.hip k_ipc_push, with the push kernel
+// gone).
+template <int G4, int S, int KB>
+__global__ __launch_bounds__(KB) void k_item_step_push(BatchView bv, Table P, Table Q, Hyper hp,
+                                                       int ld, const int32_t* __restrict__ tbase,
+                                                       int step, StepBufs sb, int long_blocks,
+                                                       int item_blocks, double* __restrict__ loss,
+                                                       int B, GradRoute gr) {
+  const int32_t t = *tbase + step + 1;
+  k2_body<G4, S, true, KB, true, false>(blockIdx.x, bv, P, Q, hp, ld, t, sb, long_blocks,
+                                        item_blocks, nullptr, loss, B, &gr);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned grp = blockIdx.x & 7u, ngrp = min(gridDim.x, 8u);
+    const unsigned in_grp = (gridDim.x - grp + 7u) / 8u;  // workgroups b with b % 8 == grp
+    const uint32_t prev = __hip_atomic_fetch_add(gr.done + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == in_grp - 1) {
+      __hip_atomic_store(gr.done + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t top = __hip_atomic_fetch_add(gr.done + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (top == ngrp - 1) {
+        __hip_atomic_store(gr.done + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int p = 0; p < gr.world; ++p)
+          if (gr.flag[p]) __hip_atomic_store(gr.flag[p], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+// Front: the owner phase of step t (k == 0 of a chunk: gather step 0's rows; else apply step k-1
+// and gather step k, dist_body.h) in the first `ob` workgroups, K1 of step t in the others.  The
+// owner workgroups come first in the grid (dispatched before any K1 workgroup that waits on them);
+// every K1 workgroup waits for the row flags of EVERY rank, this one's own included (its own
+// owner workgroups raise that flag once their stores into its landing slots are acknowledged).
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_dist_front(OwnerArgs o, BatchView bv, Table P, Table Q,
+                                                       Hyper hp, int ld, const int32_t* __restrict__ tbase,
+                                                       int step, StepBufs sb,
+                                                       const float* __restrict__ item_rows,
+                                                       PeerWait pw, int ob, int B) {
+  if ((int)blockIdx.x < ob) {
+    if (step == 0)
+      owner_gather_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.n, o.world, o.cap, 0, hp, ld, tbase,
+                               o.dst, o.done);
+    else
+      owner_step_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.aplan, o.gdep, o.gfree, o.n, o.world,
+                             o.cap, step - 1, hp, ld, tbase, o.grads_recv, o.self, o.self_grads,
+                             o.wait_flags, pw.err, o.dst, o.done);
+    return;
+  }
+  wait_peer_flags(pw.flags, pw.world, -1, *tbase + step + 1, pw.err);
+  k1_body<G4, S, true, true, false>(blockIdx.x - ob, bv, P, Q, hp, ld, *tbase + step + 1, sb, item_rows,
+                                    B, nullptr);
 }
 
 // BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread
@@ -759,6 +828,37 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
     k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
         bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,
         bstride, B, err);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t item_step_push(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
+                          const int32_t* tbase, int step, float* contrib, float* ugrad, float* xloss,
+                          double* loss, const GradRoute& gr, hipStream_t s) {
+  const StepBufs sb = plain_bufs(contrib, ugrad, xloss, nullptr);
+  if (!xloss) loss = nullptr;
+  if (!gr.done || gr.S <= 0) return hipErrorInvalidValue;
+  BPRMF_DISPATCH4(g, ({
+    const K2Grid k = k2_grid<G4_, 256>(B, loss != nullptr);
+    k_item_step_push<G4_, S_, 256><<<(unsigned)k.total(), 256, 0, s>>>(
+        bv, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, loss, B, gr);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t dist_front(const Geom& g, const OwnerArgs& o, BatchView bv, int B, Table P, Table Q,
+                      const Hyper& hp, const int32_t* tbase, int step, float* contrib, float* ugrad,
+                      float* xloss, const float* item_rows, const PeerWait& pw, hipStream_t s) {
+  const StepBufs sb = plain_bufs(contrib, ugrad, xloss, nullptr);
+  if (!o.done || o.cap <= 0) return hipErrorInvalidValue;
+  BPRMF_DISPATCH4(g, ({
+    // the owner grid of dist.hip's launches: one lane group per position (two per position for
+    // the fused apply + gather), at most 160 workgroups (one `done` increment each)
+    const int64_t units = (step == 0 ? 1 : 2) * (int64_t)o.world * o.cap * G4_;
+    const int ob = (int)std::max<int64_t>(1, std::min<int64_t>(160, (units + kBlock - 1) / kBlock));
+    const int k1b = (B + kBlock / G4_ - 1) / (kBlock / G4_);
+    k_dist_front<G4_, S_><<<(unsigned)(ob + k1b), kBlock, 0, s>>>(o, bv, P, Q, hp, g.ld, tbase, step, sb,
+                                                                 item_rows, pw, ob, B);
   }));
   return hipGetLastError();
 }

@@ -6,7 +6,9 @@
 //             hipIpc; xGMI peer writes) and raise a per-source flag.  Per step, the owners'
 //             gather writes the rows into the requesters' landing buffers itself and K1 waits on
 //             its row flags; K2's gradients go out with one push kernel and the owners' apply
-//             waits on its gradient flags: 5 kernels per step, no host in the loop.
+//             waits on its gradient flags, no host in the loop.  Default (fused2): two launches
+//             per step, the owner phase beside K1 (step.hip k_dist_front) and K2 writing its
+//             gradients straight into the owners' landing buffers (k_item_step_push).
 //   rccl      an RCCL communicator owned by the handle (ncclCommInitRank from a unique id the
 //             caller broadcasts); per-peer blocks move with grouped ncclSend/ncclRecv over xGMI.
 //   loopback  handles of one process exchanging through a shared table + device copies (the
@@ -126,7 +128,8 @@ struct IpcTransport final : Transport {
   void* recv_base[X_KINDS] = {};          // the buffers the runner reads (alloc_shared)
   void* local[kIpcHandles] = {};          // this rank's landing buffers (X_KINDS: flags)
   std::vector<void*> remote[kIpcHandles];  // [world] peers' mappings (self: local)
-  uint32_t* done = nullptr;                // [X_KINDS] last-block counters of the push kernels
+  uint32_t* done = nullptr;                // [X_KINDS] last-block counters of the push kernels,
+                                           // then [9] of the fused step's K2 (kDone2)
   bool opened = false;
   static bool copied(int kind) { return kind == X_ROWS || kind == X_IDS; }
   ~IpcTransport() override {
@@ -159,6 +162,14 @@ struct IpcTransport final : Transport {
   // landing buffers, K1 reads them there after waiting on its flags, and the apply waits on the
   // gradient flags itself; only the gradient push remains a separate kernel
   bool fused() const { return opened && !self_exchange && world > 1; }
+  // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
+  // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
+  // K1, K2 and the push kernel as separate launches)
+  bool fused2() const {
+    const char* e = getenv("BPRMF_DIST_FUSE2");
+    return fused() && !(e && e[0] == '0');
+  }
+  static constexpr int kDone2 = X_KINDS;  // offset of the fused K2's 9 counters in `done`
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
   void* peer_landing(int kind, int p) const { return remote[kind][p]; }
   int32_t* peer_flag(int kind, int p) const {
@@ -422,6 +433,53 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     }
   }
   const PeerWait pw{fused ? ipc->my_flags(X_ROWS) : nullptr, W, (int)R, h->d_err};
+  if (fused && ipc->fused2() && cap > 0) {
+    // two launches per step: [owner phase of step k | K1(k)], [K2(k) -> owners' landing buffers]
+    const int64_t WC0 = (int64_t)W * cap;
+    OwnerArgs oa;
+    oa.ids_recv = ids_recv;
+    oa.aplan = aplan;
+    oa.gdep = aplan + n * WC0 * W;
+    oa.gfree = oa.gdep + n * WC0 * W;
+    oa.n = n;
+    oa.world = W;
+    oa.cap = cap;
+    oa.self = (int)R;
+    oa.grads_recv = d->grads_recv;
+    oa.self_grads = d->grads_send + R * d->S * ld;
+    oa.wait_flags = ipc->my_flags(X_GRADS);
+    oa.dst = gd;
+    oa.dst.flag[R] = const_cast<int32_t*>(ipc->my_flags(X_ROWS)) + R;  // K1 waits on its own too
+    oa.done = ipc->done + X_ROWS;
+    GradRoute gr;
+    for (int p = 0; p < W; ++p) {
+      gr.dst[p] = p == R ? d->grads_send + R * d->S * ld
+                         : static_cast<float*>(ipc->peer_landing(X_GRADS, p)) + R * (int64_t)cap * ld;
+      gr.flag[p] = p == R ? nullptr : ipc->peer_flag(X_GRADS, p);
+    }
+    gr.S = d->S;
+    gr.world = W;
+    gr.done = ipc->done + IpcTransport::kDone2;
+    for (int64_t k = 0; k < n; ++k) {
+      const BatchView v = bb.view(k);
+      const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
+      {
+        ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
+        HIPCHK(dist_front(h->geom, oa, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                          h->d_ugrad, h->d_xloss, rows_in, pw, h->stream));
+      }
+      {
+        ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
+        HIPCHK(item_step_push(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                              h->d_ugrad, h->d_xloss, h->d_loss, gr, h->stream));
+      }
+    }
+    ProfScope ps(h, BPRMF_KPROF_OWNER, prof_kernels && ((h->t + n - 1) % kProfStride) == 0);
+    HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)(n - 1), h->hp, h->d_tbase,
+                            d->grads_recv, (int)R, oa.self_grads, ipc->my_flags(X_GRADS), h->d_err,
+                            h->stream));
+    return 0;
+  }
   std::vector<const void*> sp(W);
   std::vector<void*> rp(W);
   const int64_t WC = (int64_t)W * cap;
@@ -650,9 +708,9 @@ int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
   tr->rank = h->cfg.rank;
   const size_t flag_bytes = sizeof(int32_t) * X_KINDS * kMaxWorld;
   hipError_t e = hipExtMallocWithFlags(&tr->local[X_KINDS], flag_bytes, hipDeviceMallocUncached);
-  if (e == hipSuccess) e = hipMalloc((void**)&tr->done, sizeof(uint32_t) * X_KINDS);
+  if (e == hipSuccess) e = hipMalloc((void**)&tr->done, sizeof(uint32_t) * (X_KINDS + 9));
   if (e == hipSuccess) e = hipMemset(tr->local[X_KINDS], 0, flag_bytes);
-  if (e == hipSuccess) e = hipMemset(tr->done, 0, sizeof(uint32_t) * X_KINDS);
+  if (e == hipSuccess) e = hipMemset(tr->done, 0, sizeof(uint32_t) * (X_KINDS + 9));
   if (e != hipSuccess) {
     delete tr;
     return fail(BPRMF_E_HIP, "ipc transport buffers: %s", hipGetErrorString(e));

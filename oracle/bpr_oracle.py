@@ -83,8 +83,10 @@ def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
       t - 1 (x (1 - lr wd)^(t-1-st)) and takes the wd term, its stamp becomes t; a row with
       st >= t (already updated in step t) takes neither;
       x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x); g_u = -c (Q_i - Q_j), g_i = -c P_u, g_j = c P_u,
-      all from the values read before the triplet's stores; stores in the order P_u, Q_i, Q_j (so
-      Q_j's wins when i == j).
+      all from the values read before the triplet's stores; i == j: the one row takes g_i + g_j
+      (as the reference's summed dense gradient does).
+    The kernel keeps the most referenced items' rows apart (hot rows, scaled by the decay since an
+    anchor step, updates accumulated per wave); in real arithmetic that is this same sequence.
     In place on float32 P, Q; stamps sP, sQ (int arrays, default all t0) are updated too.
     Returns the loss sum of -log sigmoid(x) (float64)."""
     P_, Q_ = P, Q
@@ -112,8 +114,11 @@ def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
         loss += float(np.logaddexp(0.0, -float(x)))
         gu, gi, gj = -c * (vi - vj), -c * pu, c * pu
         P_[uu] = pu - lr32 * (gu + (wd32 if fu else np.float32(0)) * pu)
-        Q_[ii] = vi - lr32 * (gi + (wd32 if fi else np.float32(0)) * vi)
-        Q_[jj] = vj - lr32 * (gj + (wd32 if fj else np.float32(0)) * vj)
+        if ii == jj:
+            Q_[ii] = vi - lr32 * ((gi + gj) + (wd32 if fi else np.float32(0)) * vi)
+        else:
+            Q_[ii] = vi - lr32 * (gi + (wd32 if fi else np.float32(0)) * vi)
+            Q_[jj] = vj - lr32 * (gj + (wd32 if fj else np.float32(0)) * vj)
         if fu:
             sP[uu] = t
         if fi:

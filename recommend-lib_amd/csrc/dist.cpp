@@ -123,6 +123,7 @@ struct RcclTransport final : Transport {
 // are then copied by a receive kernel (which waits per peer) into ordinary cached buffers, since
 // the step kernels read them many times; gradients and capacities are read once, in place.
 constexpr int kIpcHandles = X_KINDS + 1;  // the four landing buffers + the flag array
+constexpr int kBusIdBytes = 64;          // a PCI bus id string, after the handles in the blob
 struct IpcTransport final : Transport {
   int world = 0, rank = 0;
   void* recv_base[X_KINDS] = {};          // the buffers the runner reads (alloc_shared)
@@ -131,6 +132,7 @@ struct IpcTransport final : Transport {
   uint32_t* done = nullptr;                // [X_KINDS] last-block counters of the push kernels,
                                            // then [9] of the fused step's K2 (kDone2)
   bool opened = false;
+  bool shared_device = false;  // some peer runs on this rank's GPU (rehearsals on one device)
   static bool copied(int kind) { return kind == X_ROWS || kind == X_IDS; }
   ~IpcTransport() override {
     for (int b = 0; b < kIpcHandles; ++b)
@@ -165,9 +167,14 @@ struct IpcTransport final : Transport {
   // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
   // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
   // K1, K2 and the push kernel as separate launches)
+  // Off when ranks share a device: a launch's K1 workgroups spin on every rank's row flag, and
+  // with several ranks' launches on one GPU the spinning workgroups can hold the CUs a peer's
+  // owner workgroups need (measured: 4 ranks on one MI355X time out).  One rank per GPU (the
+  // 8-GPU node) has no such coupling: each launch's owner workgroups are dispatched first.
   bool fused2() const {
     const char* e = getenv("BPRMF_DIST_FUSE2");
-    return fused() && !(e && e[0] == '0');
+    if (e && *e) return fused() && e[0] != '0';
+    return fused() && !shared_device;
   }
   static constexpr int kDone2 = X_KINDS;  // offset of the fused K2's 9 counters in `done`
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
@@ -722,6 +729,10 @@ int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
     HIPCHK(hipIpcGetMemHandle(&hd, tr->local[b]));
     memcpy(blob + b * sizeof hd, &hd, sizeof hd);
   }
+  // this rank's physical device (PCI bus id) after the handles: peers on the same GPU are seen
+  static_assert(sizeof(hipIpcMemHandle_t) * kIpcHandles + kBusIdBytes <= BPRMF_IPC_BLOB_BYTES, "blob");
+  HIPCHK(hipDeviceGetPCIBusId(reinterpret_cast<char*>(blob) + kIpcHandles * sizeof(hipIpcMemHandle_t),
+                              kBusIdBytes - 1, h->cfg.device));
   return 0;
 }
 
@@ -732,6 +743,15 @@ int bprmf_dist_init_ipc(bprmf_handle* h, const uint8_t* blobs) {
   if (tr->opened) return fail(BPRMF_E_STATE, "ipc transport already initialised");
   if (int r = set_dev(h)) return r;
   for (int b = 0; b < kIpcHandles; ++b) tr->remote[b].assign(tr->world, nullptr);
+  {
+    const size_t off = kIpcHandles * sizeof(hipIpcMemHandle_t);
+    const char* mine = reinterpret_cast<const char*>(blobs) + (size_t)tr->rank * BPRMF_IPC_BLOB_BYTES + off;
+    for (int p = 0; p < tr->world; ++p)
+      if (p != tr->rank &&
+          strncmp(mine, reinterpret_cast<const char*>(blobs) + (size_t)p * BPRMF_IPC_BLOB_BYTES + off,
+                  kBusIdBytes) == 0)
+        tr->shared_device = true;
+  }
   for (int p = 0; p < tr->world; ++p)
     for (int b = 0; b < kIpcHandles; ++b) {
       if (p == tr->rank) {

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _run_workers(tmp_path, spec, mode, world=2, timeout=300):
+def _run_workers(tmp_path, spec, mode, world=2, timeout=300, extra_env=None):
     """Start `world` worker processes, each logging to its own file; poll them together and stop
     the rest as soon as one fails, so a crash on one rank reports that rank's log instead of a
     peer's timeout (and no pipe can fill while another worker is being waited on)."""
@@ -40,7 +40,7 @@ def _run_workers(tmp_path, spec, mode, world=2, timeout=300):
         log = str(tmp_path / f"log_{mode}_{r}.txt")
         logs.append(log)
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
-                   WORLD_SIZE=str(world), LOCAL_RANK="0", IPC_SPEC=spec_path)
+                   WORLD_SIZE=str(world), LOCAL_RANK="0", IPC_SPEC=spec_path, **(extra_env or {}))
         with open(log, "w") as lf:
             procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ipc_worker.py"),
                                            out, mode], env=env, stdout=lf, stderr=subprocess.STDOUT))
@@ -107,8 +107,11 @@ def _loopback(rl, world, spec, mode, key):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world):
+@pytest.mark.parametrize("world,fuse2", [(2, "auto"), (3, "auto"), (4, "auto"), (2, "1"), (3, "1")])
+def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse2):
+    """fuse2 "1": the two-launch step (owner phase beside K1, K2 straight into the owners'
+    landing buffers) forced on although the ranks share the box's one GPU (it is off by default
+    there); "auto": the default (on one GPU: the owner step, K1, K2 and a push kernel)."""
     U, I, D, GB, steps = 301, 157, 128, 512, 6
     g = np.random.default_rng(11)
     u = g.integers(0, U, (steps, GB)).astype(np.int32)
@@ -118,7 +121,8 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world):
     spec = dict(U=U, I=I, D=D, B=GB, lr=0.05, wd=0.01, seed=3, u=u, i=i, j=j,
                 P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
                 Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
-    res = _run_workers(tmp_path, spec, "replay", world)
+    res = _run_workers(tmp_path, spec, "replay", world,
+                       extra_env=None if fuse2 == "auto" else {"BPRMF_DIST_FUSE2": fuse2})
     sh = rl.sharded
     P = sh.unshard_rows([r["P"] for r in res], U)
     Q = sh.unshard_rows([r["Q"] for r in res], I)

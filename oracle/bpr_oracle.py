@@ -85,8 +85,6 @@ def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
       x = <P_u,Q_i> - <P_u,Q_j>, c = sigmoid(-x); g_u = -c (Q_i - Q_j), g_i = -c P_u, g_j = c P_u,
       all from the values read before the triplet's stores; i == j: the one row takes g_i + g_j
       (as the reference's summed dense gradient does).
-    The kernel keeps the most referenced items' rows apart (hot rows, scaled by the decay since an
-    anchor step, updates accumulated per wave); in real arithmetic that is this same sequence.
     In place on float32 P, Q; stamps sP, sQ (int arrays, default all t0) are updated too.
     Returns the loss sum of -log sigmoid(x) (float64)."""
     P_, Q_ = P, Q

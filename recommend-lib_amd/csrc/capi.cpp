@@ -184,7 +184,7 @@ int bprmf_destroy(bprmf_handle* h) {
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p, h->d_hot_slot, h->d_hot_items, h->d_hot_rows};
+                  h->d_pend_q, h->d_pend_p};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -227,60 +227,6 @@ int bprmf_row_stride(bprmf_handle* h, int32_t* ld) {
   *ld = h->geom.ld;
   return 0;
 }
-
-}  // extern "C"
-
-// hogwild: the most referenced items (positive counts; the sampler draws each positive's item
-// num_ng times, negatives uniformly) get their rows kept apart (hogwild.hip HotArgs): at most
-// kHotMax of them, at most 16 KB of LDS accumulator per wave, and only items with at least four
-// times the mean count (uniform data has none)
-static int choose_hot(bprmf_handle* h, const std::vector<int32_t>& pi) {
-  void* olds[] = {h->d_hot_slot, h->d_hot_items, h->d_hot_rows};
-  for (void* p : olds)
-    if (p) HIPCHK(hipFree(p));
-  h->d_hot_slot = nullptr;
-  h->d_hot_items = nullptr;
-  h->d_hot_rows = nullptr;
-  h->hot_n = 0;
-  h->hot_valid = false;
-  const char* e = getenv("BPRMF_HOGWILD_HOT");
-  int cap = std::min<int64_t>(kHotMax, 4096 / h->geom.ld);
-  if (e && *e) cap = std::min(cap, std::max(0, atoi(e)));
-  if (cap <= 0 || h->I <= 0 || pi.empty()) return 0;
-  std::vector<int64_t> cnt(h->I, 0);
-  for (int32_t i : pi) ++cnt[i];
-  std::vector<int32_t> order(h->I);
-  for (int64_t i = 0; i < h->I; ++i) order[i] = (int32_t)i;
-  const int k = (int)std::min<int64_t>(cap, h->I);
-  std::partial_sort(order.begin(), order.begin() + k, order.end(), [&](int32_t a, int32_t b) {
-    return cnt[a] != cnt[b] ? cnt[a] > cnt[b] : a < b;
-  });
-  const double mean = (double)pi.size() / (double)h->I;
-  std::vector<int32_t> hot;
-  for (int s = 0; s < k; ++s)
-    if ((double)cnt[order[s]] >= 4.0 * mean) hot.push_back(order[s]);
-  if (hot.empty()) return 0;
-  std::vector<int8_t> slot(h->I, -1);
-  for (size_t s = 0; s < hot.size(); ++s) slot[hot[s]] = (int8_t)s;
-  if (int r = dalloc(&h->d_hot_slot, h->I)) return r;
-  if (int r = dalloc(&h->d_hot_items, (int64_t)hot.size())) return r;
-  HIPCHK(hipExtMallocWithFlags((void**)&h->d_hot_rows, sizeof(float) * hot.size() * h->geom.ld,
-                               hipDeviceMallocUncached));
-  HIPCHK(hipMemcpy(h->d_hot_slot, slot.data(), h->I, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_hot_items, hot.data(), 4 * hot.size(), hipMemcpyHostToDevice));
-  h->hot_n = (int)hot.size();
-  return 0;
-}
-
-int bprmf::hogwild_end(bprmf_handle* h) {
-  if (h->semantics != BPRMF_SEM_HOGWILD || !h->hot_n || !h->hot_valid) return 0;
-  HotArgs hot{h->d_hot_slot, h->d_hot_rows, h->hot_n, h->hot_anchor};
-  HIPCHK(hot_sync(h->geom, hot, h->d_hot_items, h->Q, h->hp, h->t, true, h->stream));
-  h->hot_anchor = h->t;
-  return 0;
-}
-
-extern "C" {
 
 int bprmf_set_train(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz) {
   return bprmf_set_train_ex(h, users, items, nnz, nullptr, nullptr, 0);
@@ -353,8 +299,6 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
     if (h->cfg.world == 1 && h->use_graphs)
       if (int r = ensure_step_graphs(h)) return r;
   }
-  if (h->semantics == BPRMF_SEM_HOGWILD)
-    if (int r = choose_hot(h, pi)) return r;
   return 0;
 }
 
@@ -701,18 +645,8 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     {
       hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
       if (ea) HIPCHK(hipEventRecord(ea, h->stream));
-      HotArgs hot;
-      if (h->hot_n) {
-        if (!h->hot_valid) {  // the hot rows from the table, brought to this step
-          hot = HotArgs{h->d_hot_slot, h->d_hot_rows, h->hot_n, h->t};
-          HIPCHK(hot_sync(h->geom, hot, h->d_hot_items, h->Q, h->hp, h->t, false, h->stream));
-          h->hot_anchor = h->t;
-          h->hot_valid = true;
-        }
-        hot = HotArgs{h->d_hot_slot, h->d_hot_rows, h->hot_n, h->hot_anchor};
-      }
       HIPCHK(hogwild(h->geom, ru ? nullptr : &sa, epoch, first_slot, ru, ri, rj, n, h->P, h->Q, h->hp,
-                     hot, h->t, (int)B, h->d_loss, h->d_err, h->stream));
+                     h->t, (int)B, h->d_loss, h->d_err, h->stream));
       if (ea) {
         hipEvent_t eb = prof_event(h);
         if (eb) {
@@ -839,7 +773,6 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps))
       return r;
   trace_mark();
-  if (int r = hogwild_end(h)) return r;
   const int rc_end = end_call(h, st, end - beg, steps);
   trace_mark();
   trace_flush();
@@ -864,7 +797,6 @@ int bprmf_train_triplets_dev(bprmf_handle* h, const int32_t* u, const int32_t* i
     const int64_t m = std::min(chunk, n - off);
     if (int r = run_chunk(h, 0, 0, m, u + off, i + off, j + off, &steps)) return r;
   }
-  if (int r = hogwild_end(h)) return r;
   return end_call(h, st, n, steps);
 }
 
@@ -896,7 +828,6 @@ int bprmf_train_triplets(bprmf_handle* h, const int32_t* u, const int32_t* i, co
     if (int r = run_chunk(h, 0, 0, m, tu, ti, tj, &steps)) return r;
     HIPCHK(hipStreamSynchronize(h->stream));  // host buffers reused by the next chunk's copies
   }
-  if (int r = hogwild_end(h)) return r;
   return end_call(h, st, n, steps);
 }
 
@@ -940,7 +871,6 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   if (int r = set_dev(h)) return r;
   const size_t D = h->geom.D, ld = h->geom.ld;
   HIPCHK(hipStreamSynchronize(h->stream));
-  h->hot_valid = false;  // hogwild: the hot rows are reloaded from the new table
   HIPCHK(hipMemset(h->P.W, 0, sizeof(float) * h->U * ld));
   HIPCHK(hipMemset(h->Q.W, 0, sizeof(float) * h->I * ld));
   if (h->U) HIPCHK(hipMemcpy2D(h->P.W, ld * 4, P, D * 4, D * 4, h->U, hipMemcpyHostToDevice));

@@ -63,13 +63,6 @@ struct bprmf_handle {
   int32_t* d_pend_q = nullptr;  // [2][I] step that last marked an item row (fused step)
   int32_t* d_pend_p = nullptr;  // [2][U] the same for user rows K2 finishes
   int32_t semantics = BPRMF_SEM_EXACT;  // cfg.semantics (BPRMF_SEM_HOGWILD: hogwild.hip)
-  // hogwild: the hot items' rows kept apart (kernels.h HotArgs), chosen at set_train
-  int hot_n = 0;
-  int8_t* d_hot_slot = nullptr;   // [I] slot of a hot item, -1 otherwise
-  int32_t* d_hot_items = nullptr; // [hot_n]
-  float* d_hot_rows = nullptr;    // [hot_n][ld], uncached
-  int32_t hot_anchor = 0;
-  bool hot_valid = false;         // the hot rows hold the current values (else: load them first)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan
@@ -144,8 +137,6 @@ int read_loss(bprmf_handle* h, double* loss);
 int loss_zero_slots(bprmf_handle* h);
 int begin_call(bprmf_handle* h);
 int end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps);
-// hogwild: the hot rows back into the item table at the call's end (no-op otherwise)
-int hogwild_end(bprmf_handle* h);
 // mapped status block: byte offsets of the two call sequence words (end_call, the sharded
 // runner's capacity read-back)
 constexpr size_t kSeqEndOff = 16 + sizeof(double) * kLossSlots;

@@ -101,34 +101,31 @@ static __device__ __forceinline__ void hw_sample(const SamplerArgs& a, uint32_t 
 
 constexpr int kHwUnroll = 2;  // triplets per lane group per round (rows in flight per buffer)
 
-// One round of a wave: kHwUnroll triplets per lane group, their ids, hot slots, stamps and rows.
+// One round of a wave: kHwUnroll triplets per lane group, their ids, stamps and rows.
 template <int S, int UNR>
 struct HwRound {
   float4 pu[UNR][S], vi[UNR][S], vj[UNR][S];
-  int32_t su[UNR], si[UNR], sj[UNR], uu[UNR], ii[UNR], jj[UNR], hi[UNR], hj[UNR];
+  int32_t su[UNR], si[UNR], sj[UNR], uu[UNR], ii[UNR], jj[UNR];
   bool ok[UNR];
 };
 
-// issue the round starting at slot k0 of the wave's chunk (ids and hot slots from the lanes that
-// sampled them).  A hot item's row comes from the hot rows (scaled; no stamp).
+// issue the round starting at slot k0 of the wave's chunk (ids from the lanes that sampled them)
 template <int G4, int S, int UNR, int GPW, bool SERIAL>
 static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
-                                               int32_t mi, int32_t mj, int32_t mhi, int32_t mhj,
-                                               const Table& P, const Table& Q, const HotArgs& hot,
-                                               int ld, int sub, int gw, bool nt) {
+                                               int32_t mi, int32_t mj, const Table& P,
+                                               const Table& Q, int ld, int sub, int gw, int fl) {
+  const bool nt = fl & 1, noload = fl & 2;
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
     R.uu[r] = __shfl(mu, src & 63);
     R.ii[r] = __shfl(mi, src & 63);
     R.jj[r] = __shfl(mj, src & 63);
-    R.hi[r] = __shfl(mhi, src & 63);
-    R.hj[r] = __shfl(mhj, src & 63);
     R.ok[r] = (SERIAL ? gw == 0 : true) && src < cnt && R.uu[r] >= 0;
-    if (R.ok[r]) {
+    if (R.ok[r] && !noload) {
       const float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
-      const float* qi = (R.hi[r] >= 0 ? hot.rows + (int64_t)R.hi[r] * ld : Q.W + (int64_t)R.ii[r] * ld) + 4 * sub;
-      const float* qj = (R.hj[r] >= 0 ? hot.rows + (int64_t)R.hj[r] * ld : Q.W + (int64_t)R.jj[r] * ld) + 4 * sub;
+      const float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
+      const float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         if (nt) {
@@ -142,8 +139,8 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
         }
       }
       R.su[r] = hw_ld_word(P.stamp + R.uu[r]);
-      R.si[r] = R.hi[r] >= 0 ? 0 : hw_ld_word(Q.stamp + R.ii[r]);
-      R.sj[r] = R.hj[r] >= 0 ? 0 : hw_ld_word(Q.stamp + R.jj[r]);
+      R.si[r] = hw_ld_word(Q.stamp + R.ii[r]);
+      R.sj[r] = hw_ld_word(Q.stamp + R.jj[r]);
     } else {
       R.su[r] = R.si[r] = R.sj[r] = 0;
 #pragma unroll
@@ -152,69 +149,24 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
   }
 }
 
-// a hot item's update, -lr g in the scaled coordinates (x alpha^-(t - anchor)), added into this
-// wave's LDS accumulator row of the item (LDS atomics: the wave's lane groups may share a row)
-template <int G4, int S>
-static __device__ __forceinline__ void hw_hot_acc(float* acc, int slot, const float4 (&g)[S],
-                                                  float scale, int ld, int sub) {
-  float* a = acc + (int64_t)slot * ld + 4 * sub;
-#pragma unroll
-  for (int k = 0; k < S; ++k) {
-    atomicAdd(a + 4 * G4 * k + 0, g[k].x * scale);
-    atomicAdd(a + 4 * G4 * k + 1, g[k].y * scale);
-    atomicAdd(a + 4 * G4 * k + 2, g[k].z * scale);
-    atomicAdd(a + 4 * G4 * k + 3, g[k].w * scale);
-  }
-}
-
-// this wave's accumulated hot-row updates into the hot rows (no-return f32 atomics at the memory
-// side: the rows are uncached, every reader sees them), and the accumulators zeroed.  hmask: the
-// slots this lane's groups touched; the wave's union is walked, one slot per lane group at a time.
-template <int G4, int S, int GPW>
-static __device__ __forceinline__ void hw_flush(float* acc, uint32_t& hmask, const HotArgs& hot,
-                                                int ld, int sub, int gw) {
-  uint32_t m = hmask;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off);
-  hmask = 0;
-  for (int idx = 0; m; ++idx) {
-    const int s = __ffs(m) - 1;
-    m &= m - 1;
-    if (idx % GPW != gw) continue;
-    float* a = acc + (int64_t)s * ld + 4 * sub;
-    float* h = hot.rows + (int64_t)s * ld + 4 * sub;
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const float4 v = *reinterpret_cast<const float4*>(a + 4 * G4 * k);
-      unsafeAtomicAdd(h + 4 * G4 * k + 0, v.x);
-      unsafeAtomicAdd(h + 4 * G4 * k + 1, v.y);
-      unsafeAtomicAdd(h + 4 * G4 * k + 2, v.z);
-      unsafeAtomicAdd(h + 4 * G4 * k + 3, v.w);
-      *reinterpret_cast<float4*>(a + 4 * G4 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-}
-
 // compute and store the round at slot k0 (slot base + k0 + ... of step t0 + 1 + slot / B)
 template <int G4, int S, int UNR, int GPW, bool SERIAL>
 static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base, int k0,
                                                 const Table& P, const Table& Q, const Hyper& hp,
-                                                const HotArgs& hot, float* acc, uint32_t& hmask,
                                                 int ld, int32_t t0, int B, int sub, int gw,
-                                                float& lacc) {
+                                                float& lacc, int fl) {
   const float lr = hp.lr, wd = hp.wd;
+  const bool nostore = fl & 4;
+  const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
     const int32_t t = t0 + 1 + (int32_t)((uint32_t)(base + src) / (uint32_t)B);  // chunks < 2^31 slots
-    const bool hot_i = R.hi[r] >= 0, hot_j = R.hj[r] >= 0;
-    // first touch of the row in step t: decay to t - 1 and take the wd term; else neither.  A hot
-    // row is stored scaled: its value at step t - 1 is alpha^(t-1-anchor) * the stored row, and the
-    // decay is in that scale (every step exactly once, however many touches)
-    const bool fu1 = R.su[r] < t, fi1 = !hot_i && R.si[r] < t, fj1 = !hot_j && R.sj[r] < t;
+    // first touch of the row in step t: decay to t - 1 and take the wd term; else neither
+    const bool fu1 = R.su[r] < t, fi1 = R.si[r] < t, fj1 = R.sj[r] < t;
     const float fu = fu1 ? decay_pow(hp.log2a, t - 1 - R.su[r]) : 1.f;
-    const float fi = hot_i ? decay_pow(hp.log2a, t - 1 - hot.anchor) : fi1 ? decay_pow(hp.log2a, t - 1 - R.si[r]) : 1.f;
-    const float fj = hot_j ? decay_pow(hp.log2a, t - 1 - hot.anchor) : fj1 ? decay_pow(hp.log2a, t - 1 - R.sj[r]) : 1.f;
+    const float fi = fi1 ? decay_pow(hp.log2a, t - 1 - R.si[r]) : 1.f;
+    const float fj = fj1 ? decay_pow(hp.log2a, t - 1 - R.sj[r]) : 1.f;
     float di = 0.f, dj = 0.f;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -231,43 +183,35 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
     // whatever ok[] says (inactive groups carry zeros)
     di = group_sum<G4>(R.ok[r] ? di : 0.f);
     dj = group_sum<G4>(R.ok[r] ? dj : 0.f);
-    if (!R.ok[r]) continue;
+    if (!R.ok[r] || nostore) continue;
     const float x = di - dj;
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
     if (sub == 0) lacc += softplus(-x);       // -log sigmoid(x)
-    const bool same = R.ii[r] == R.jj[r];     // i == j: one row, the two gradients summed
-    float4 gu[S], gi[S], gj[S];
+    float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
+    float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
+    float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
+    const bool same = R.ii[r] == R.jj[r];  // i == j: one row, both gradients (stored once, as i)
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const float4 pu = R.pu[r][k], vi = R.vi[r][k], vj = R.vj[r][k];
-      gu[k] = make_float4(-c * (vi.x - vj.x), -c * (vi.y - vj.y), -c * (vi.z - vj.z), -c * (vi.w - vj.w));
-      gi[k] = make_float4(-c * pu.x, -c * pu.y, -c * pu.z, -c * pu.w);
-      gj[k] = make_float4(c * pu.x, c * pu.y, c * pu.z, c * pu.w);
-      if (same) gi[k] = make_float4(gi[k].x + gj[k].x, gi[k].y + gj[k].y, gi[k].z + gj[k].z, gi[k].w + gj[k].w);
-    }
-    float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
-#pragma unroll
-    for (int k = 0; k < S; ++k) hw_st4(pr + 4 * G4 * k, hw_sgd(R.pu[r][k], gu[k], lr, fu1 ? wd : 0.f));
-    if (hot_i || hot_j) {
-      const float inv = exp2f((float)(-(double)(t - hot.anchor) * hp.log2a));  // alpha^-(t-anchor)
-      if (hot_i) {
-        hw_hot_acc<G4, S>(acc, R.hi[r], gi, -lr * inv, ld, sub);
-        hmask |= 1u << R.hi[r];
+      const float4 gu = make_float4(-c * (vi.x - vj.x), -c * (vi.y - vj.y), -c * (vi.z - vj.z),
+                                    -c * (vi.w - vj.w));
+      const float4 gj = make_float4(c * pu.x, c * pu.y, c * pu.z, c * pu.w);
+      float4 gi = make_float4(-c * pu.x, -c * pu.y, -c * pu.z, -c * pu.w);
+      if (same) gi = make_float4(gi.x + gj.x, gi.y + gj.y, gi.z + gj.z, gi.w + gj.w);
+      if (plainst) {
+        if (!nousers) *reinterpret_cast<float4*>(pr + 4 * G4 * k) = hw_sgd(pu, gu, lr, fu1 ? wd : 0.f);
+        if (!noitems) {
+          *reinterpret_cast<float4*>(qi + 4 * G4 * k) = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f);
+          if (!same) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
+        }
+        continue;
       }
-      if (hot_j && !same) {
-        hw_hot_acc<G4, S>(acc, R.hj[r], gj, -lr * inv, ld, sub);
-        hmask |= 1u << R.hj[r];
+      if (!nousers) hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
+      if (!noitems) {
+        hw_st4(qi + 4 * G4 * k, hw_sgd(vi, gi, lr, fi1 ? wd : 0.f));
+        if (!same) hw_st4(qj + 4 * G4 * k, hw_sgd(vj, gj, lr, fj1 ? wd : 0.f));
       }
-    }
-    if (!hot_i) {
-      float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
-#pragma unroll
-      for (int k = 0; k < S; ++k) hw_st4(qi + 4 * G4 * k, hw_sgd(R.vi[r][k], gi[k], lr, fi1 ? wd : 0.f));
-    }
-    if (!hot_j && !same) {
-      float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
-#pragma unroll
-      for (int k = 0; k < S; ++k) hw_st4(qj + 4 * G4 * k, hw_sgd(R.vj[r][k], gj[k], lr, fj1 ? wd : 0.f));
     }
     if (sub == 0) {
       if (fu1) hw_st_word(P.stamp + R.uu[r], t);
@@ -275,7 +219,6 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
       if (fj1 && !same) hw_st_word(Q.stamp + R.jj[r], t);
     }
     if (SERIAL) {  // the next triplet reads these rows: stores done, this CU's L1 dropped
-      hw_flush<G4, S, GPW>(acc, hmask, hot, ld, sub, gw);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
@@ -292,9 +235,9 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
                                                     const int32_t* __restrict__ tu,
                                                     const int32_t* __restrict__ ti,
                                                     const int32_t* __restrict__ tj, int64_t n,
-                                                    Table P, Table Q, Hyper hp, HotArgs hot, int ld,
-                                                    int32_t t0, int B, int tpw, int nt,
-                                                    double* __restrict__ loss, int32_t* __restrict__ err) {
+                                                    Table P, Table Q, Hyper hp, int ld, int32_t t0,
+                                                    int B, int tpw, int fl, double* __restrict__ loss,
+                                                    int32_t* __restrict__ err) {
   constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round and unroll step
   constexpr int UNR = SERIAL ? 1 : kHwUnroll;
   constexpr int STEP = GPW * UNR;
@@ -304,11 +247,6 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
   const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
   float lacc = 0.f;
-  // this wave's accumulators of hot-row updates: [hot.n][ld] floats of dynamic LDS per wave
-  extern __shared__ float hw_lds[];
-  float* acc = hw_lds + (int64_t)(threadIdx.x / 64) * hot.n * ld;
-  uint32_t hmask = 0;
-  for (int e = lane; e < hot.n * ld; e += 64) acc[e] = 0.f;
   for (int64_t base = wave * tpw; base < n; base += nwaves * tpw) {
     const int cnt = (int)min<int64_t>(tpw, n - base);
     int32_t mu = 0, mi = 0, mj = 0;
@@ -328,30 +266,23 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
         mu = -1;
       }
     }
-    // hot slots of the two items, looked up once per slot here (beside the sampler's loads)
-    int32_t mhi = -1, mhj = -1;
-    if (hot.n && lane < cnt && mu >= 0) {
-      mhi = hot.slot[mi];
-      mhj = hot.slot[mj];
-    }
     HwRound<S, UNR> A, Bf;
     if (SERIAL) {  // each triplet reads what the one before it stored: no prefetch
       for (int k0 = 0; k0 < cnt; k0 += STEP) {
-        hw_load<G4, S, UNR, GPW, SERIAL>(A, k0, cnt, mu, mi, mj, mhi, mhj, P, Q, hot, ld, sub, gw, nt);
-        hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, hot, acc, hmask, ld, t0, B, sub, gw, lacc);
+        hw_load<G4, S, UNR, GPW, SERIAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+        hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
       }
       continue;
     }
-    hw_load<G4, S, UNR, GPW, SERIAL>(A, 0, cnt, mu, mi, mj, mhi, mhj, P, Q, hot, ld, sub, gw, nt);
+    hw_load<G4, S, UNR, GPW, SERIAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
     for (int k0 = 0; k0 < cnt; k0 += 2 * STEP) {
       const bool more1 = k0 + STEP < cnt, more2 = k0 + 2 * STEP < cnt;
-      if (more1) hw_load<G4, S, UNR, GPW, SERIAL>(Bf, k0 + STEP, cnt, mu, mi, mj, mhi, mhj, P, Q, hot, ld, sub, gw, nt);
-      hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, hot, acc, hmask, ld, t0, B, sub, gw, lacc);
+      if (more1) hw_load<G4, S, UNR, GPW, SERIAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+      hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
       if (!more1) break;
-      if (more2) hw_load<G4, S, UNR, GPW, SERIAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, mhi, mhj, P, Q, hot, ld, sub, gw, nt);
-      hw_apply<G4, S, UNR, GPW, SERIAL>(Bf, base, k0 + STEP, P, Q, hp, hot, acc, hmask, ld, t0, B, sub, gw, lacc);
+      if (more2) hw_load<G4, S, UNR, GPW, SERIAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+      hw_apply<G4, S, UNR, GPW, SERIAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
     }
-    if (hot.n) hw_flush<G4, S, GPW>(acc, hmask, hot, ld, sub, gw);  // once per chunk of tpw slots
   }
   // the wave's loss into one of kSegLossSlots f64 slots (no-return atomics; order is not fixed,
   // like the updates themselves)
@@ -381,10 +312,9 @@ static int hw_tpw(int64_t n) {
 
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
-                   Table Q, const Hyper& hp, const HotArgs& hot, int32_t t0, int B, double* loss,
-                   int32_t* err, hipStream_t s) {
+                   Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
+                   hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (hot.n < 0 || hot.n > kHotMax || (hot.n && (!hot.slot || !hot.rows))) return hipErrorInvalidValue;
   const bool serial = hw_serial();
   const int tpw = serial ? 64 : hw_tpw(n);
   const int64_t waves = (n + tpw - 1) / tpw;
@@ -411,58 +341,25 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   const unsigned threads = serial ? 64 : kBlock;
   // row loads past L1 (nt) by default; BPRMF_HOGWILD_PLAIN=1: plain loads (A/B)
   const char* pl = getenv("BPRMF_HOGWILD_PLAIN");
-  const int nt = (pl && pl[0] == '1') ? 0 : 1;
-  // LDS: one [hot.n][ld] accumulator per wave
-  const size_t lds = sizeof(float) * (size_t)(threads / 64) * hot.n * g.ld;
+  int fl = (pl && pl[0] == '1') ? 0 : 1;
+  // diagnostic timing only (wrong results): bit 1 = no row loads, bit 2 = no row stores, bit 3 =
+  // plain (write-back) row stores, bit 4 = no item row stores, bit 5 = no user row stores
+  if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 62);
   SamplerArgs a{};
   if (sa) a = *sa;
   BPRMF_DISPATCH4(g, ({
     if (serial && sa)
-      k_hogwild<G4_, S_, true, true><<<1, threads, lds, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                            hot, g.ld, t0, B, tpw, nt, loss, err);
+      k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
+                                                          g.ld, t0, B, tpw, fl, loss, err);
     else if (serial)
-      k_hogwild<G4_, S_, false, true><<<1, threads, lds, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                             hot, g.ld, t0, B, tpw, nt, loss, err);
+      k_hogwild<G4_, S_, false, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
+                                                           g.ld, t0, B, tpw, fl, loss, err);
     else if (sa)
-      k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, lds, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, hot, g.ld, t0, B, tpw, nt, loss, err);
+      k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, 0, s>>>(
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
     else
-      k_hogwild<G4_, S_, false, false><<<(unsigned)blocks, threads, lds, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, hot, g.ld, t0, B, tpw, nt, loss, err);
-  }));
-  return hipGetLastError();
-}
-
-// hot rows <-> the item table.  load: row s = item hot.items[s] brought to step t (its stamp's
-// pending decay applied), anchor t.  store: the item row = alpha^(t - anchor) * row s, stamp t, and
-// row s re-anchored at t (the same value in the new scale).
-template <int G4, int S>
-__global__ __launch_bounds__(kBlock) void k_hot_sync(HotArgs hot, const int32_t* __restrict__ items,
-                                                     Table Q, Hyper hp, int ld, int32_t t, int store) {
-  const int sub = threadIdx.x & (G4 - 1);
-  const int s = blockIdx.x * (kBlock / G4) + threadIdx.x / G4;
-  if (s >= hot.n) return;
-  const int32_t item = items[s];
-  float* w = Q.W + (int64_t)item * ld + 4 * sub;
-  float* h = hot.rows + (int64_t)s * ld + 4 * sub;
-  const float f = store ? decay_pow(hp.log2a, t - hot.anchor) : decay_pow(hp.log2a, t - Q.stamp[item]);
-#pragma unroll
-  for (int k = 0; k < S; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>((store ? h : w) + 4 * G4 * k);
-    const float4 o = make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
-    *reinterpret_cast<float4*>(w + 4 * G4 * k) = o;
-    *reinterpret_cast<float4*>(h + 4 * G4 * k) = o;
-  }
-  if (sub == 0) Q.stamp[item] = t;
-}
-
-hipError_t hot_sync(const Geom& g, const HotArgs& hot, const int32_t* items, Table Q, const Hyper& hp,
-                    int32_t t, bool store, hipStream_t s) {
-  if (hot.n <= 0) return hipSuccess;
-  BPRMF_DISPATCH4(g, ({
-    const int per = kBlock / G4_;
-    k_hot_sync<G4_, S_><<<(unsigned)((hot.n + per - 1) / per), kBlock, 0, s>>>(hot, items, Q, hp, g.ld, t,
-                                                                             store ? 1 : 0);
+      k_hogwild<G4_, S_, false, false><<<(unsigned)blocks, threads, 0, s>>>(
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
   }));
   return hipGetLastError();
 }

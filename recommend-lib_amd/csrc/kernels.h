@@ -220,25 +220,10 @@ int item_long_blocks(int B);
 // relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
 // sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s
 // belongs to step t0 + 1 + s / B; loss into kSegLossSlots slots
-// hot items (the most referenced, by positive count; at most kHotMax): their rows live apart in
-// `rows` (uncached: every reader sees the memory-side atomic adds) in a scaled form, value at step
-// t = alpha^(t - anchor) * row; the kernel accumulates their updates per wave in LDS and adds them
-// with f32 atomics once per chunk of slots, instead of racing whole-row stores on them
-constexpr int kHotMax = 32;
-struct HotArgs {
-  const int8_t* slot = nullptr;  // [item rows] hot slot of an item, -1 if not hot
-  float* rows = nullptr;         // [n][ld]
-  int n = 0;
-  int32_t anchor = 0;
-};
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
-                   Table Q, const Hyper& hp, const HotArgs& hot, int32_t t0, int B, double* loss,
-                   int32_t* err, hipStream_t s);
-// hot rows from the item table (store = false: brought to step t, anchor t) or back into it
-// (store = true: the rows as of step t, stamped t; the hot rows re-anchored at t)
-hipError_t hot_sync(const Geom& g, const HotArgs& hot, const int32_t* items, Table Q, const Hyper& hp,
-                    int32_t t, bool store, hipStream_t s);
+                   Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
+                   hipStream_t s);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

@@ -58,38 +58,6 @@ def test_serial_replay_matches_oracle(rl, monkeypatch, d, B):
     assert st["loss"] == pytest.approx(loss, rel=1e-5)
 
 
-@pytest.mark.parametrize("d", [32, 128])
-def test_serial_replay_with_hot_rows_matches_oracle(rl, golden, monkeypatch, d):
-    """Hot items (chosen from the positives at set_train) live apart in scaled form and take their
-    updates through per-wave accumulators: serially that is the oracle's sequence again."""
-    monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
-    pos, U, I = _ml100k(golden)
-    g = np.random.default_rng(d + 1)
-    B, n = 64, 400
-    m = _hog(rl, U, I, d, B)
-    m.set_train(pos)
-    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
-    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
-    m.set_weights(P0, Q0)
-    # triplets over the most popular items, so hot rows are hit often (and i == j on a hot item)
-    top = np.argsort(-np.bincount(pos[:, 1], minlength=I), kind="stable")[:12]
-    u = g.integers(0, U, n)
-    i = np.where(g.random(n) < 0.7, top[g.integers(0, 12, n)], g.integers(0, I, n))
-    j = np.where(g.random(n) < 0.5, top[g.integers(0, 12, n)], g.integers(0, I, n))
-    j[:5] = i[:5]
-    st = m.train_triplets(u, i, j)
-    P, Q = P0.copy(), Q0.copy()
-    loss, sP, sQ = O.hogwild_serial(P, Q, u, i, j, 0.05, 0.01, B)
-    T = st["steps"]
-    a = np.float32(1 - 0.05 * 0.01)
-    Pg, Qg = m.get_weights()
-    Pw = P * np.power(np.float64(a), (T - sP))[:, None].astype(np.float32)
-    Qw = Q * np.power(np.float64(a), (T - sQ))[:, None].astype(np.float32)
-    np.testing.assert_allclose(Pg, Pw, rtol=1e-5, atol=HOG_ATOL)
-    np.testing.assert_allclose(Qg, Qw, rtol=1e-5, atol=HOG_ATOL)
-    assert st["loss"] == pytest.approx(loss, rel=1e-5)
-
-
 def _ml100k(golden):
     f = golden("bpr_ml100k_replay.npz")
     return f["positives"].astype(np.int64), int(f["U"]), int(f["I"])
@@ -102,7 +70,6 @@ def test_serial_device_sampled_equals_replay_of_oracle_triplets(rl, golden, monk
     a = _hog(rl, U, I, 16, B, seed=seed)
     a.set_train(pos)
     b = _hog(rl, U, I, 16, B, seed=seed)
-    b.set_train(pos)  # the same hot items (chosen from the positives)
     P0, Q0 = a.get_weights()
     b.set_weights(P0, Q0)
     sa = a.train_steps(2, 5, steps)  # slots at an offset inside epoch 2

@@ -124,17 +124,38 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
   }
   __syncthreads();
   BSTAMP_SORT(2);
-  for (int x = tid; x < total; x += T) {
-    const uint64_t me = sc.bk[x];
-    const int b = (int)((uint32_t)(me >> 32) >> shift);
-    const int bs = sc.start[b], be = sc.start[b + 1];
-    int rank = 0, y = bs;
-    for (; y + 4 <= be; y += 4) {  // four reads in flight (a hot item's bucket holds ~80)
-      const uint64_t a0 = sc.bk[y], a1 = sc.bk[y + 1], a2 = sc.bk[y + 2], a3 = sc.bk[y + 3];
-      rank += (int)(a0 < me) + (int)(a1 < me) + (int)(a2 < me) + (int)(a3 < me);
+  // every element's loads issued together (E chains in flight, not one after the other): its
+  // entry, its bucket's bounds, then the bucket's first two entries (nearly every bucket holds
+  // at most two); only the lanes of a larger bucket loop over the rest
+  {
+    uint64_t me[E];
+    int bs[E], be[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) me[k] = tid + k * T < total ? sc.bk[tid + k * T] : ~0ull;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int b = min((int)((uint32_t)(me[k] >> 32) >> shift), kBuckets - 1);
+      bs[k] = sc.start[b];
+      be[k] = sc.start[b + 1];
     }
-    for (; y < be; ++y) rank += sc.bk[y] < me;
-    sc.srt[bs + rank] = (int32_t)(uint32_t)me;
+    int rank[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int last = max(total - 1, 0);
+      const uint64_t a0 = sc.bk[min(bs[k], last)], a1 = sc.bk[min(bs[k] + 1, last)];
+      rank[k] = (int)(be[k] > bs[k] && a0 < me[k]) + (int)(be[k] > bs[k] + 1 && a1 < me[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      if (tid + k * T >= total) continue;
+      int y = bs[k] + 2;
+      for (; y + 4 <= be[k]; y += 4) {  // four reads in flight (a hot item's bucket holds ~60)
+        const uint64_t a0 = sc.bk[y], a1 = sc.bk[y + 1], a2 = sc.bk[y + 2], a3 = sc.bk[y + 3];
+        rank[k] += (int)(a0 < me[k]) + (int)(a1 < me[k]) + (int)(a2 < me[k]) + (int)(a3 < me[k]);
+      }
+      for (; y < be[k]; ++y) rank[k] += sc.bk[y] < me[k];
+      sc.srt[bs[k] + rank[k]] = (int32_t)(uint32_t)me[k];
+    }
   }
   __syncthreads();
   BSTAMP_SORT(3);
@@ -169,6 +190,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
   using SortI = rocprim::block_radix_sort<uint32_t, T, IPT2, uint32_t>;
   using Scan = rocprim::block_scan<int, T>;
+  using ScanL = rocprim::block_scan<uint64_t, T>;
   union RadixSmem {  // the sorted keys alias the sort storage (barrier after every sort)
     typename SortU::storage_type su;
     typename SortI::storage_type si;
@@ -180,6 +202,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   constexpr size_t kSortBytes = BUCKET ? kBucketBytes : sizeof(RadixSmem);
   __shared__ __attribute__((aligned(16))) unsigned char s_sort[kSortBytes];
   __shared__ typename Scan::storage_type sscan;
+  __shared__ typename ScanL::storage_type sscan64;
   __shared__ int32_t s_i[T * IPT];  // per sorted position: item row (world 1) or item slot
   __shared__ int32_t s_j[T * IPT];
   __shared__ int s_own[kMaxWorld];
@@ -276,13 +299,17 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     s_key[tid * IPT + k] = key[k];
   }
   __syncthreads();  // slot-order reads of s_i/s_j done; s_key complete
+  // segment heads from the neighbouring key: in this thread's registers but for its first position
+  const uint32_t uprev = tid ? s_key[tid * IPT - 1] : kNone;
+  bool uhead[IPT];
   int heads = 0;
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     const int p = tid * IPT + k;
     s_i[p] = my_i[k];  // sorted order from here on
     s_j[p] = my_j[k];
-    if (key[k] != kNone) heads += (p == 0 || s_key[p - 1] != key[k]);
+    uhead[k] = key[k] != kNone && (k ? key[k - 1] : uprev) != key[k];
+    heads += uhead[k];
   }
   // one scan for both counts: segment heads in the high half, valid triplets in the low
   int pre = 0, tot = 0;
@@ -294,13 +321,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   {
     int s = seg0;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int p = tid * IPT + k;
-      if (key[k] != kNone && (p == 0 || s_key[p - 1] != key[k])) s_seg[s++] = p;
-    }
+    for (int k = 0; k < IPT; ++k)
+      if (uhead[k]) s_seg[s++] = tid * IPT + k;
   }
   __syncthreads();
-  bool uhead[IPT];
   int uend[IPT];  // a head's segment end
   // trec.w: 1 = the user's only triplet; >= 2 = head of a segment of that length that lies in one
   // K1 workgroup (tpb consecutive positions: K1 sums it in LDS and updates the user); -1 = another
@@ -311,12 +335,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int p = tid * IPT + k;
-      uhead[k] = key[k] != kNone && (p == 0 || s_key[p - 1] != key[k]);
       uend[k] = p + 1;
       uw[k] = 0;
       if (key[k] != kNone) {
         if (uhead[k]) ++s;
-        const int b = s_seg[s], e = s + 1 < n_useg ? s_seg[s + 1] : nvalid;
+        const int b = s_seg[max(s, 0)], e = s + 1 < n_useg ? s_seg[s + 1] : nvalid;
         uend[k] = e;
         const int len = e - b;
         if (len == 1)
@@ -363,36 +386,53 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   // k1_items (single GPU): an item with ONE reference in the batch is updated by K1 from that
   // triplet (its gradient is that one term; the same arithmetic K2 would do): no contribution row,
   // no K2 record.  Item segments K2 serves are the others, numbered compactly (`mseg`).
+  // Per reference: head (first of its item), sole (only one), long (more than kLongSeg: position
+  // r + kLongSeg still holds the key), from the neighbouring keys (registers but at this thread's
+  // ends).  Invalid keys (kNone) sit after every valid one, so an item's last reference is
+  // followed by a different key.
   const int nref = 2 * nvalid;
-  auto is_head = [&](int r, uint32_t key) { return r == 0 || s_key[r - 1] != key; };
-  auto is_sole = [&](int r, uint32_t key) {
-    return k1_items && is_head(r, key) && (r + 1 >= nref || s_key[r + 1] != key);
-  };
-  int iheads = 0, mheads = 0;
+  const uint32_t iprev = tid ? s_key[tid * IPT2 - 1] : kNone;
+  const uint32_t inext = tid + 1 < T ? s_key[(tid + 1) * IPT2] : kNone;
+  uint32_t hm = 0, sm = 0, lm = 0;  // bit k: reference k of this thread is a head / sole / long
+  int iheads = 0, mheads = 0, nlong = 0;
 #pragma unroll
   for (int k = 0; k < IPT2; ++k) {
     const int r = tid * IPT2 + k;
-    if (ik[k] != kNone) {
-      const bool h = is_head(r, ik[k]);
-      iheads += h;
-      mheads += h && !is_sole(r, ik[k]);
-      v.refs[r] = (int32_t)iv[k];
-      if (BUCKET) s_refs[r] = (int32_t)iv[k];
-    }
+    if (ik[k] == kNone) continue;
+    const bool h = (k ? ik[k - 1] : iprev) != ik[k];
+    const bool so = k1_items && h && (k + 1 < IPT2 ? ik[k + 1] : inext) != ik[k];
+    const bool lg = h && !so && r + kLongSeg < T * IPT2 && s_key[r + kLongSeg] == ik[k];
+    hm |= (uint32_t)h << k;
+    sm |= (uint32_t)so << k;
+    lm |= (uint32_t)lg << k;
+    iheads += h;
+    mheads += h && !so;
+    nlong += lg;
+    v.refs[r] = (int32_t)iv[k];
+    if (BUCKET) s_refs[r] = (int32_t)iv[k];
   }
-  // one scan for both counts (each <= 2B <= 16384): all heads high, K2-served heads low
-  int ipre = 0, itot = 0;
-  Scan().exclusive_scan((iheads << 16) | mheads, ipre, 0, itot, sscan, rocprim::plus<int>());
-  const int iseg0 = ipre >> 16, n_iseg = itot >> 16;
-  const int mseg0 = ipre & 0xFFFF, n_mseg = itot & 0xFFFF;
+  // ONE scan for four counts (each <= 2B <= 16384, 16 bits apiece): item segments, K2-served item
+  // segments, long item segments, and the user segments K2 finishes (w = 0 heads)
+  int nmulti = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) nmulti += uhead[k] && uw[k] == 0;
+  uint64_t cpre = 0, ctot = 0;
+  ScanL().exclusive_scan((uint64_t)iheads | (uint64_t)mheads << 16 | (uint64_t)nlong << 32 |
+                             (uint64_t)nmulti << 48,
+                         cpre, 0ull, ctot, sscan64, rocprim::plus<uint64_t>());
+  auto field = [](uint64_t x, int f) { return (int)((x >> (16 * f)) & 0xFFFF); };
+  const int iseg0 = field(cpre, 0), n_iseg = field(ctot, 0);
+  const int mseg0 = field(cpre, 1), n_mseg = field(ctot, 1);
+  const int n_long = field(ctot, 2), n_multi = field(ctot, 3);
+  int lpre = field(cpre, 2), mpre = field(cpre, 3);
   {
     int s = iseg0 - 1;  // segment of this thread's first ref if it is not a head
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
       if (ik[k] == kNone) continue;
-      const bool head = is_head(r, ik[k]);
-      const bool sole = is_sole(r, ik[k]);
+      const bool head = (hm >> k) & 1;
+      const bool sole = (sm >> k) & 1;
       if (head) {
         ++s;
         if (BUCKET)
@@ -443,72 +483,40 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     }
     return lo * slot_stride + (s - s_opre[lo]);
   };
-  int nlong_mine = 0;
+  BSTAMP(6);
+  // item records of the K2-served segments, and the long ones' copies (the first kMaxLongItems;
+  // past the cap a long segment's record drops its long bit and K2 takes the short path)
   {
     int s = iseg0, ms = mseg0;  // segment index, K2 record index
 #pragma unroll
     for (int k = 0; k < IPT2; ++k) {
       const int r = tid * IPT2 + k;
-      if (ik[k] != kNone && is_head(r, ik[k])) {
-        if (is_sole(r, ik[k])) {  // K1's: no record
-          ++s;
-          continue;
-        }
-        const int end = ioff_at(s + 1);
-        const int len = end - r;
-        const int lng = len > kLongSeg;
-        nlong_mine += lng;
-        int pk[kInlineRefs / 2];
-#pragma unroll
-        for (int m = 0; m < kInlineRefs / 2; ++m) {
-          const int a = 2 * m < len ? ref_at(r + 2 * m) : 0;
-          const int b = 2 * m + 1 < len ? ref_at(r + 2 * m + 1) : 0;
-          pk[m] = a | (b << 16);
-        }
-        store_rec(v.irec + (int64_t)ms * kRec, slots ? slot_of(s) : (int)ik[k],
-                  r | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
+      if (!((hm >> k) & 1)) continue;
+      if ((sm >> k) & 1) {  // K1's: no record
         ++s;
-        ++ms;
+        continue;
       }
+      const int end = ioff_at(s + 1);
+      const int len = end - r;
+      const int lng = ((lm >> k) & 1) && lpre < kMaxLongItems;
+      int pk[kInlineRefs / 2];
+#pragma unroll
+      for (int m = 0; m < kInlineRefs / 2; ++m) {
+        const int a = ref_at(min(r + 2 * m, nref - 1)), b = ref_at(min(r + 2 * m + 1, nref - 1));
+        pk[m] = (2 * m < len ? a : 0) | ((2 * m + 1 < len ? b : 0) << 16);
+      }
+      store_rec(v.irec + (int64_t)ms * kRec, slots ? slot_of(s) : (int)ik[k],
+                r | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
+      if (lng) store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
+      lpre += (lm >> k) & 1;
+      ++s;
+      ++ms;
     }
   }
-  __syncthreads();
-  int lpre = 0, n_long = 0;
-  BSTAMP(6);
-  Scan().exclusive_scan(nlong_mine, lpre, 0, n_long, sscan, rocprim::plus<int>());
-  if (nlong_mine) {
-    int s = iseg0, ms = mseg0;
-#pragma unroll
-    for (int k = 0; k < IPT2; ++k) {
-      const int r = tid * IPT2 + k;
-      if (ik[k] != kNone && is_head(r, ik[k])) {
-        if (is_sole(r, ik[k])) {
-          ++s;
-          continue;
-        }
-        const int end = ioff_at(s + 1);
-        if (end - r > kLongSeg) {
-          if (lpre < kMaxLongItems)
-            store_rec(v.lrec + (int64_t)lpre * kRec, (int)ik[k], r, end, slot_of(s), 0, 0, 0, 1);
-          else
-            v.irec[(int64_t)ms * kRec + 1] = r | ((end - r) << 15);  // over the cap: short path
-          ++lpre;
-        }
-        ++s;
-        ++ms;
-      }
-    }
-  }
+  BSTAMP(7);
 
   // 3. triplet records, now that s_i/s_j hold the final item rows (world 1) or slots, and the
   //    records of user segments with more than one triplet (K2 finishes those users)
-  int nmulti_mine = 0;
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) nmulti_mine += uhead[k] && uw[k] == 0;
-  __syncthreads();  // sscan reuse
-  int mpre = 0, n_multi = 0;
-  BSTAMP(7);
-  Scan().exclusive_scan(nmulti_mine, mpre, 0, n_multi, sscan, rocprim::plus<int>());
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     const int p = tid * IPT + k;

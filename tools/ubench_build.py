@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 LIB = os.environ.get("UB_LIB", os.path.join(ROOT, "tools", "libbprmf_stamps.so"))
 PHASES = ["loads", "user sort", "user segments", "item keys+sort", "item heads/refs",
-          "item records", "long items", "triplet records"]
+          "slot prefix", "item records", "triplet records"]
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     b = importlib.import_module("recommend-lib_amd.build")

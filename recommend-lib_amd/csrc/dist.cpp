@@ -163,7 +163,11 @@ struct IpcTransport final : Transport {
   // per-step fusion (enqueue_steps): the owners' gather writes rows straight into the peers' row
   // landing buffers, K1 reads them there after waiting on its flags, and the apply waits on the
   // gradient flags itself; only the gradient push remains a separate kernel
-  bool fused() const { return opened && !self_exchange && world > 1; }
+  // BPRMF_DIST_FUSE=0: every exchange as push + receive copy into cached buffers (A/B)
+  bool fused() const {
+    const char* e = getenv("BPRMF_DIST_FUSE");
+    return opened && !self_exchange && world > 1 && !(e && e[0] == '0');
+  }
   // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
   // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
   // K1, K2 and the push kernel as separate launches)

@@ -25,7 +25,7 @@ constexpr int kBuildThreads = 1024;
 // diagnostic build only (-DBPRMF_BUILD_STAMPS, tools/ubench_build.py): s_memrealtime at the
 // builder's phase boundaries, first workgroup, first thread
 #ifdef BPRMF_BUILD_STAMPS
-__device__ uint64_t g_build_stamps[16];
+__device__ uint64_t g_build_stamps[32];
 #define BSTAMP(k)                                                                          \
   do {                                                                                     \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_build_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   BSTAMP(1);
   if constexpr (BUCKET) {
     bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
-                        [](int q) { return (uint32_t)q; });
+                        [](int q) { return (uint32_t)q; }, 16);
   } else {
     SortU().sort(key, val, reinterpret_cast<RadixSmem*>(s_sort)->su, 0, user_bits);
     __syncthreads();
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
 
 #ifdef BPRMF_BUILD_STAMPS
 extern "C" int bprmf_debug_build_stamps(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), sizeof(uint64_t) * 16) == hipSuccess ? 0 : -3;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), sizeof(uint64_t) * 32) == hipSuccess ? 0 : -3;
 }
 #endif
 

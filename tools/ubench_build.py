@@ -22,6 +22,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
     sys.exit(0)
 
 os.environ["BPRMF_DIAG_LIB"] = LIB
+# the step kernels never run on a diagnostic build's batches (some are wrong on purpose)
+os.environ["BPRMF_DIAG_BUILD_ONLY"] = "1"
 import ctypes  # noqa: E402
 
 import numpy as np  # noqa: E402
@@ -47,18 +49,21 @@ for radix in ("0",) if "--quick" in sys.argv else ("0", "1"):
                 m.train_steps(0, 20 * rep, 20)
             except rl.BprmfError:  # diagnostic builds that break the batches: stamps still valid
                 pass
-            st = np.zeros(16, np.uint64)
+            st = np.zeros(32, np.uint64)
             assert L.bprmf_debug_build_stamps(st.ctypes.data) == 0
             d = np.diff(st[:9].astype(np.int64)) * 0.01  # 100 MHz -> us
             x = st.astype(np.int64)
             sub = np.diff(np.concatenate([x[3:4], x[9:14]])) * 0.01 if radix == "0" else np.zeros(5)
-            rows.append(np.concatenate([d, sub]))
+            usub = np.diff(np.concatenate([x[1:2], x[16:21]])) * 0.01 if radix == "0" else np.zeros(5)
+            rows.append(np.concatenate([d, sub, usub]))
         med = np.median(np.array(rows[1:]), axis=0)
         key = f"radix={radix} split={split}"
         res[key] = {p: round(float(v), 2) for p, v in zip(PHASES, med[:8])}
         res[key]["total"] = round(float(med[:8].sum()), 2)
         if radix == "0":  # the item bucket sort's own phases
             res[key]["item sort phases"] = {p: round(float(v), 2) for p, v in zip(
-                ("keys+count", "scan", "scatter", "rank", "gather"), med[8:])}
+                ("keys+count", "scan", "scatter", "rank", "gather"), med[8:13])}
+            res[key]["user sort phases"] = {p: round(float(v), 2) for p, v in zip(
+                ("count", "scan", "scatter", "rank", "gather"), med[13:18])}
         m.close()
 print(json.dumps(res, indent=1))

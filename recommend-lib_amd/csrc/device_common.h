@@ -168,6 +168,41 @@ static __device__ __forceinline__ bool ipc_spin(const int32_t* flag, int32_t seq
   return true;
 }
 
+// Completion board: each producing workgroup of a grid marks its own word once its stores are
+// acknowledged (sc1 store, MI355X_MICROARCH.md valid forms, table row 1); ONE finisher workgroup,
+// dispatched after every producer (the grid's last block), polls all the marks with sc1 loads and
+// then signals.  It replaces a same-address atomic count (memory-side and serialised, ~80 ns per
+// add: a 1,168-workgroup K2 grid spent ~11 us of every step in its count).
+static __device__ __forceinline__ void board_mark(int32_t* mark, int i, int32_t seq) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's (remote) stores landed
+  __syncthreads();                                    // ... and every wave's of the workgroup
+  if (threadIdx.x == 0) __hip_atomic_store(mark + i, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the whole workgroup: true once marks[0, n) all reached seq (false after ~10 s: err bit 4)
+static __device__ __forceinline__ bool board_wait(const int32_t* mark, int n, int32_t seq,
+                                                  int32_t* err) {
+  for (int64_t spins = 0;; ++spins) {
+    int mine = 1;
+    for (int b = threadIdx.x; b < n; b += blockDim.x)
+      mine &= __hip_atomic_load(mark + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= seq;
+    if (__syncthreads_and(mine)) return true;
+    __builtin_amdgcn_s_sleep(2);
+    if (spins > 10000000) {
+      if (threadIdx.x == 0) atomicOr(err, 4);
+      return false;
+    }
+  }
+}
+// the finisher: every producer's mark, then each non-null flag[p] raised to seq (system scope)
+static __device__ __forceinline__ void board_finish(const int32_t* mark, int n, int32_t seq,
+                                                    int32_t* const* flag, int nflags,
+                                                    int32_t* err) {
+  if (!board_wait(mark, n, seq, err)) return;
+  if (threadIdx.x == 0)
+    for (int p = 0; p < nflags; ++p)
+      if (flag[p]) __hip_atomic_store(flag[p], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Sharded steps over the IPC transport: the first thread of every workgroup waits until each
 // peer's flag (this rank's flag array for one exchange kind, written remotely by the peers' push
 // kernels) reaches the step's sequence number, then the workgroup proceeds.

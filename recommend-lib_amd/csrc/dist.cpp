@@ -129,10 +129,17 @@ struct IpcTransport final : Transport {
   void* recv_base[X_KINDS] = {};          // the buffers the runner reads (alloc_shared)
   void* local[kIpcHandles] = {};          // this rank's landing buffers (X_KINDS: flags)
   std::vector<void*> remote[kIpcHandles];  // [world] peers' mappings (self: local)
-  uint32_t* done = nullptr;                // [X_KINDS] last-block counters of the push kernels,
-                                           // then [9] of the fused step's K2 (kDone2)
+  // completion boards (device_common.h board_mark / board_finish), kBoardMax words each: the
+  // push kernels' by exchange kind, then the owner phase's, then the fused step's K2
+  int32_t* boards = nullptr;
+  static constexpr int kBoardOwner = X_KINDS, kBoardK2 = X_KINDS + 1, kBoards = X_KINDS + 2;
+  int32_t* board(int b) const { return boards + (size_t)b * kBoardMax; }
   bool opened = false;
   bool shared_device = false;  // some peer runs on this rank's GPU (rehearsals on one device)
+  // owner workgroups per launch: they spin on the peers' gradient flags before applying, so with
+  // ranks sharing one GPU a full grid of them could hold every CU a peer needs to produce those
+  // gradients (measured: 2 ranks, ~1,500 owner workgroups, timed out); one rank per GPU: no cap
+  int owner_blocks() const { return shared_device ? 160 : kBoardMax; }
   static bool copied(int kind) { return kind == X_ROWS || kind == X_IDS; }
   ~IpcTransport() override {
     for (int b = 0; b < kIpcHandles; ++b)
@@ -142,14 +149,19 @@ struct IpcTransport final : Transport {
       if (b < X_KINDS && copied(b) && recv_base[b]) (void)!hipFree(recv_base[b]);
       if (local[b]) (void)!hipFree(local[b]);
     }
-    if (done) (void)!hipFree(done);
+    if (boards) (void)!hipFree(boards);
   }
   bool capturable() const override { return true; }
   bool ready() const override { return opened; }
   int alloc_shared(bprmf_handle* h, int kind, size_t bytes, void** p) override {
     (void)h;
     *p = nullptr;
-    HIPCHK(hipExtMallocWithFlags(&local[kind], std::max<size_t>(bytes, 256), hipDeviceMallocUncached));
+    // landing memory (BPRMF_DIST_LANDING, A/B): uncached (default), fine-grained, or plain
+    const char* lm = getenv("BPRMF_DIST_LANDING");
+    const unsigned flags = !lm || !*lm ? hipDeviceMallocUncached
+                           : lm[0] == 'f' ? hipDeviceMallocFinegrained
+                           : lm[0] == 'p' ? hipDeviceMallocDefault : hipDeviceMallocUncached;
+    HIPCHK(hipExtMallocWithFlags(&local[kind], std::max<size_t>(bytes, 256), flags));
     if (copied(kind)) {
       HIPCHK(hipMalloc(&recv_base[kind], std::max<size_t>(bytes, 256)));
     } else {
@@ -163,10 +175,12 @@ struct IpcTransport final : Transport {
   // per-step fusion (enqueue_steps): the owners' gather writes rows straight into the peers' row
   // landing buffers, K1 reads them there after waiting on its flags, and the apply waits on the
   // gradient flags itself; only the gradient push remains a separate kernel
-  // BPRMF_DIST_FUSE=0: every exchange as push + receive copy into cached buffers (A/B)
+  // BPRMF_DIST_FUSE=0: every exchange as push + receive copy into cached buffers; =1: the fused
+  // forms at world 1 too (A/B of what they cost on one device)
   bool fused() const {
     const char* e = getenv("BPRMF_DIST_FUSE");
-    return opened && !self_exchange && world > 1 && !(e && e[0] == '0');
+    if (e && *e) return opened && !self_exchange && e[0] != '0';
+    return opened && !self_exchange && world > 1;
   }
   // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
   // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
@@ -180,7 +194,6 @@ struct IpcTransport final : Transport {
     if (e && *e) return fused() && e[0] != '0';
     return fused() && !shared_device;
   }
-  static constexpr int kDone2 = X_KINDS;  // offset of the fused K2's 9 counters in `done`
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
   void* peer_landing(int kind, int p) const { return remote[kind][p]; }
   int32_t* peer_flag(int kind, int p) const {
@@ -201,7 +214,7 @@ struct IpcTransport final : Transport {
         a.flag[p] = peer_flag(x.kind, p);
       }
     }
-    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, done + x.kind, h->stream));
+    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, board(x.kind), h->d_err, h->stream));
     return 0;
   }
   int exchange(bprmf_handle* h, const Xchg& x) override {
@@ -222,7 +235,7 @@ struct IpcTransport final : Transport {
         a.flag[p] = static_cast<int32_t*>(remote[X_KINDS][p]) + x.kind * kMaxWorld + rank;
       }
     }
-    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, done + x.kind, h->stream));
+    HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, board(x.kind), h->d_err, h->stream));
     const int32_t* fl = flags() + x.kind * kMaxWorld;
     if (!copied(x.kind)) {
       HIPCHK(ipc_wait(fl, world, rank, x.tbase, x.k, x.seq, h->d_err, h->stream));
@@ -461,7 +474,8 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     oa.wait_flags = ipc->my_flags(X_GRADS);
     oa.dst = gd;
     oa.dst.flag[R] = const_cast<int32_t*>(ipc->my_flags(X_ROWS)) + R;  // K1 waits on its own too
-    oa.done = ipc->done + X_ROWS;
+    oa.mark = ipc->board(IpcTransport::kBoardOwner);
+    oa.max_blocks = ipc->owner_blocks();
     GradRoute gr;
     for (int p = 0; p < W; ++p) {
       gr.dst[p] = p == R ? d->grads_send + R * d->S * ld
@@ -470,7 +484,8 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     }
     gr.S = d->S;
     gr.world = W;
-    gr.done = ipc->done + IpcTransport::kDone2;
+    gr.mark = ipc->board(IpcTransport::kBoardK2);
+    gr.err = h->d_err;
     for (int64_t k = 0; k < n; ++k) {
       const BatchView v = bb.view(k);
       const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
@@ -499,7 +514,8 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
   {  // the chunk's first rows; later steps' rows come with the previous step's apply
     ProfScope ps(h, BPRMF_KPROF_OWNER, prof_kernels && (h->t % kProfStride) == 0);
     HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, 0, h->hp, h->d_tbase, gd,
-                             fused ? ipc->done + X_ROWS : nullptr, h->stream));
+                             fused ? ipc->board(IpcTransport::kBoardOwner) : nullptr, h->d_err,
+                             fused ? ipc->owner_blocks() : kBoardMax, h->stream));
   }
   for (int64_t k = 0; k < n; ++k) {
     const BatchView v = bb.view(k);
@@ -535,7 +551,8 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
       if (k + 1 < n)  // apply step k, gather step k+1
         HIPCHK(dist_owner_step(h->geom, h->Q, ids_recv, aplan, gdep, gfree, n, W, cap, (int)k, h->hp,
                                h->d_tbase, d->grads_recv, self, own, wf, h->d_err, gd,
-                               fused ? ipc->done + X_ROWS : nullptr, h->stream));
+                               fused ? ipc->board(IpcTransport::kBoardOwner) : nullptr,
+                               fused ? ipc->owner_blocks() : kBoardMax, h->stream));
       else
         HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
                                 d->grads_recv, self, own, wf, h->d_err, h->stream));
@@ -719,9 +736,10 @@ int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
   tr->rank = h->cfg.rank;
   const size_t flag_bytes = sizeof(int32_t) * X_KINDS * kMaxWorld;
   hipError_t e = hipExtMallocWithFlags(&tr->local[X_KINDS], flag_bytes, hipDeviceMallocUncached);
-  if (e == hipSuccess) e = hipMalloc((void**)&tr->done, sizeof(uint32_t) * (X_KINDS + 9));
+  const size_t board_bytes = sizeof(int32_t) * IpcTransport::kBoards * kBoardMax;
+  if (e == hipSuccess) e = hipMalloc((void**)&tr->boards, board_bytes);
   if (e == hipSuccess) e = hipMemset(tr->local[X_KINDS], 0, flag_bytes);
-  if (e == hipSuccess) e = hipMemset(tr->done, 0, sizeof(uint32_t) * (X_KINDS + 9));
+  if (e == hipSuccess) e = hipMemset(tr->boards, 0, board_bytes);
   if (e != hipSuccess) {
     delete tr;
     return fail(BPRMF_E_HIP, "ipc transport buffers: %s", hipGetErrorString(e));

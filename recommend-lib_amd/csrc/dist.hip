@@ -104,9 +104,16 @@ __global__ __launch_bounds__(kBlock) void k_owner_gather(Table Q, const int32_t*
                                                         int64_t n, int world, int cap, int k,
                                                         Hyper hp, int ld,
                                                         const int32_t* __restrict__ tbase,
-                                                        PushArgs dst, uint32_t* __restrict__ done) {
-  owner_gather_body<G4, S>(blockIdx.x, gridDim.x, Q, ids_recv, n, world, cap, k, hp, ld, tbase, dst,
-                           done);
+                                                        PushArgs dst, int32_t* __restrict__ mark,
+                                                        int32_t* __restrict__ err) {
+  // mark set (IPC): the grid's last workgroup is the finisher
+  const int nprod = mark ? (int)gridDim.x - 1 : (int)gridDim.x;
+  if ((int)blockIdx.x < nprod) {
+    owner_gather_body<G4, S>(blockIdx.x, nprod, Q, ids_recv, n, world, cap, k, hp, ld, tbase, dst,
+                             mark);
+  } else {
+    board_finish(mark, nprod, *tbase + k + 1, dst.flag, world, err);
+  }
 }
 
 // owner: for each distinct row of step k (its leader position) sum the peers' gradients in peer
@@ -184,21 +191,33 @@ __global__ __launch_bounds__(kBlock) void k_owner_step(Table Q, const int32_t* _
                                                       const float* __restrict__ self_grads,
                                                       const int32_t* __restrict__ wait_flags,
                                                       int32_t* __restrict__ err, PushArgs dst,
-                                                      uint32_t* __restrict__ done) {
-  owner_step_body<G4, S>(blockIdx.x, gridDim.x, Q, ids_recv, aplan, gdep, gfree, n, world, cap, k, hp,
-                         ld, tbase, grads_recv, self, self_grads, wait_flags, err, dst, done);
+                                                      int32_t* __restrict__ mark) {
+  const int nprod = mark ? (int)gridDim.x - 1 : (int)gridDim.x;  // IPC: the last is the finisher
+  if ((int)blockIdx.x < nprod) {
+    owner_step_body<G4, S>(blockIdx.x, nprod, Q, ids_recv, aplan, gdep, gfree, n, world, cap, k, hp,
+                           ld, tbase, grads_recv, self, self_grads, wait_flags, err, dst, mark);
+  } else {
+    board_finish(mark, nprod, *tbase + k + 2, dst.flag, world, err);
+  }
 }
 
 // ---- IPC transport: blocks pushed straight into the peers' buffers over xGMI ----------------
 // Per-peer blocks of `bytes` (a multiple of 4) are copied into a.dst[p] (a peer's buffer mapped
 // through hipIpc, or this rank's own buffer for the self block); every block fences at system
-// scope (waits for its stores' acknowledgements), and the last block to finish stores the
-// exchange's sequence number into each peer's flag for this rank.  seq = *tbase + k + 1 (per-step exchanges: graph-safe) or `seq`.
+// scope (waits for its stores' acknowledgements) and marks the completion board; the grid's last
+// block (the finisher) then stores the exchange's sequence number into each peer's flag for this
+// rank.  seq = *tbase + k + 1 (per-step exchanges: graph-safe) or `seq`.
 __global__ void k_ipc_push(PushArgs a, int world, int64_t bytes, const int32_t* __restrict__ tbase,
-                           int k, int32_t seq, uint32_t* __restrict__ done) {
+                           int k, int32_t seq, int32_t* __restrict__ mark, int32_t* __restrict__ err) {
+  const int32_t s = tbase ? *tbase + k + 1 : seq;
+  const int nprod = (int)gridDim.x - 1;
+  if ((int)blockIdx.x == nprod) {
+    board_finish(mark, nprod, s, a.flag, world, err);
+    return;
+  }
   const int64_t n16 = bytes / 16, per = n16 + (bytes % 16) / 4, total = per * world;
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-       x += (int64_t)gridDim.x * blockDim.x) {
+       x += (int64_t)nprod * blockDim.x) {
     const int p = (int)(x / per);
     const int64_t u = x - p * per;
     if (!a.src[p]) continue;
@@ -212,17 +231,7 @@ __global__ void k_ipc_push(PushArgs a, int world, int64_t bytes, const int32_t* 
   // block, which the next kernel reads after the kernel boundary): waiting for the stores'
   // acknowledgements makes them visible; a system-scope fence would also write back the whole
   // L2 of this XCD, once per block.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {  // every block's stores are acknowledged
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int32_t s = tbase ? *tbase + k + 1 : seq;
-      for (int p = 0; p < world; ++p)
-        if (a.flag[p]) __hip_atomic_store(a.flag[p], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  board_mark(mark, blockIdx.x, s);
 }
 
 // wait until every peer's flag for this exchange reached its sequence number (ipc_spin: a dead
@@ -279,12 +288,13 @@ __global__ void k_max_vals(const int32_t* __restrict__ vals, int world, int32_t*
 }
 
 hipError_t ipc_push(const PushArgs& a, int world, int64_t bytes, const int32_t* tbase, int k,
-                    int32_t seq, uint32_t* done, hipStream_t s) {
-  // at most 160 blocks: each block ends with one increment of the shared `done` counter, and
-  // same-address atomics serialise (~13 ns each); 160 x 256 lanes x 16 B keeps the links busy
+                    int32_t seq, int32_t* mark, int32_t* err, hipStream_t s) {
+  // up to 256 copying blocks (grid-stride: 256 x 256 lanes x 16 B keep the links busy) and the
+  // finisher
+  if (!mark) return hipErrorInvalidValue;
   const int64_t units = (bytes / 16 + (bytes % 16) / 4) * world;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(160, (units + kBlock - 1) / kBlock));
-  k_ipc_push<<<blocks, kBlock, 0, s>>>(a, world, bytes, tbase, k, seq, done);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (units + kBlock - 1) / kBlock));
+  k_ipc_push<<<blocks + 1, kBlock, 0, s>>>(a, world, bytes, tbase, k, seq, mark, err);
   return hipGetLastError();
 }
 
@@ -341,27 +351,29 @@ hipError_t dist_owner_step(const Geom& g, Table Q, const int32_t* ids_recv, cons
                            const int32_t* gdep, const int32_t* gfree, int64_t n, int world, int cap,
                            int k, const Hyper& hp, const int32_t* tbase, const float* grads_recv,
                            int self, const float* self_grads, const int32_t* wait_flags,
-                           int32_t* err, const PushArgs& dst, uint32_t* done, hipStream_t s) {
+                           int32_t* err, const PushArgs& dst, int32_t* mark, int max_blocks,
+                           hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
     unsigned blocks = blocks_for(2LL * world * cap * G4_);
-    if (done) blocks = std::min(blocks, 160u);  // one `done` increment per workgroup
+    if (mark) blocks = std::min<unsigned>(blocks, std::min(max_blocks, kBoardMax)) + 1;  // + finisher
     k_owner_step<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, aplan, gdep, gfree, n, world, cap,
                                                     k, hp, g.ld, tbase, grads_recv, self,
-                                                    self_grads, wait_flags, err, dst, done);
+                                                    self_grads, wait_flags, err, dst, mark);
   }));
   return hipGetLastError();
 }
 
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
                              int cap, int k, const Hyper& hp, const int32_t* tbase,
-                             const PushArgs& dst, uint32_t* done, hipStream_t s) {
+                             const PushArgs& dst, int32_t* mark, int32_t* err, int max_blocks,
+                             hipStream_t s) {
   if (cap <= 0) return hipSuccess;
   BPRMF_DISPATCH4D(g, ({
     unsigned blocks = blocks_for((int64_t)world * cap * G4_);
-    if (done) blocks = std::min(blocks, 160u);  // one `done` increment per workgroup
+    if (mark) blocks = std::min<unsigned>(blocks, std::min(max_blocks, kBoardMax)) + 1;  // + finisher
     k_owner_gather<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, ids_recv, n, world, cap, k, hp, g.ld,
-                                                      tbase, dst, done);
+                                                      tbase, dst, mark, err);
   }));
   return hipGetLastError();
 }

@@ -11,9 +11,9 @@ static __device__ __forceinline__ void dist_st4(float* p, float4 v) { *reinterpr
 
 // owner: rows requested by every peer for step k, brought to step t-1: the row of position
 // (p, idx) goes to dst.to[p] + idx * ld (packed send blocks, this rank's own slots, or -- IPC
-// transport -- straight into peer p's landing buffer).  With dst.done set (IPC), the grid is a
-// bounded grid-stride loop and the last workgroup to finish raises each peer's row flag to the
-// step number once every workgroup's stores are acknowledged.
+// transport -- straight into peer p's landing buffer).  With mark set (IPC), each workgroup marks
+// its completion board entry once its stores are acknowledged (a finisher workgroup then raises
+// the peers' row flags, device_common.h board_finish).
 // (blk, nblk: this workgroup and the owner workgroups of the launch; the body is shared by
 // k_owner_gather and the fused front launch of the sharded step, step.hip k_dist_front)
 template <int G4, int S>
@@ -23,7 +23,7 @@ static __device__ __forceinline__ void owner_gather_body(int blk, int nblk, cons
                                                          const Hyper& hp, int ld,
                                                          const int32_t* __restrict__ tbase,
                                                          const PushArgs& dst,
-                                                         uint32_t* __restrict__ done) {
+                                                         int32_t* __restrict__ mark) {
   constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int32_t t = *tbase + k + 1;
@@ -42,25 +42,15 @@ static __device__ __forceinline__ void owner_gather_body(int blk, int nblk, cons
     for (int s = 0; s < S; ++s)
       dist_st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
   }
-  if (!done) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (uint32_t)nblk - 1) {
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int p = 0; p < world; ++p)
-        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (mark) board_mark(mark, blk, t);
 }
 
 // Fused owner step: apply step k (as k_owner_apply) and gather step k+1 (as k_owner_gather) in one
 // launch.  A row step k applies is served to step k+1's requesters by its leader, from the value
 // it just stored (gdep); rows step k does not apply are gathered by their own groups (gfree).  No
 // row is both read by a free gather and written by an apply, so the groups are independent.
-// With done set (IPC), a bounded grid-stride grid and the last workgroup raises the peers' row
-// flags to step k+1.
+// With mark set (IPC), each workgroup marks its completion board entry (step k+1) once its stores
+// are acknowledged; a finisher workgroup raises the peers' row flags.
 template <int G4, int S>
 static __device__ __forceinline__ void owner_step_body(
     int blk, int nblk, const Table& Q, const int32_t* __restrict__ ids_recv,
@@ -68,7 +58,7 @@ static __device__ __forceinline__ void owner_step_body(
     const int32_t* __restrict__ gfree, int64_t n, int world, int cap, int k, const Hyper& hp, int ld,
     const int32_t* __restrict__ tbase, const float* __restrict__ grads_recv, int self,
     const float* __restrict__ self_grads, const int32_t* __restrict__ wait_flags,
-    int32_t* __restrict__ err, const PushArgs& dst, uint32_t* __restrict__ done) {
+    int32_t* __restrict__ err, const PushArgs& dst, int32_t* __restrict__ mark) {
   constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int32_t t = *tbase + k + 1;
@@ -146,17 +136,7 @@ static __device__ __forceinline__ void owner_step_body(
         dist_st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
     }
   }
-  if (!done) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (uint32_t)nblk - 1) {
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int p = 0; p < world; ++p)
-        if (dst.flag[p]) __hip_atomic_store(dst.flag[p], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (mark) board_mark(mark, blk, t + 1);
 }
 
 }  // namespace bprmf

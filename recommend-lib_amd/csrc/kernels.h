@@ -59,6 +59,7 @@ constexpr int kLongSeg = 16;
 constexpr int kInlineRefs = 12;  // refs held in an item segment's record (B <= 8192: 14-bit refs)
 constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
 constexpr int kMaxWorld = 64;
+constexpr int kBoardMax = 16384;  // producing workgroups one completion board tracks
 struct BatchView {
   int32_t *trec, *mrec, *irec, *lrec, *refs, *useg, *ioff, *ukey, *meta, *own;
   __host__ __device__ BatchView shifted(int64_t off) const {
@@ -254,8 +255,10 @@ struct PushArgs {  // one IPC exchange: per peer, source block, destination, fla
   void* dst[kMaxWorld];
   int32_t* flag[kMaxWorld];
 };
+// mark: the launch's completion board (device_common.h board_mark / board_finish), >= kBoardMax
+// words, zero before first use
 hipError_t ipc_push(const PushArgs& a, int world, int64_t bytes, const int32_t* tbase, int k,
-                    int32_t seq, uint32_t* done, hipStream_t s);
+                    int32_t seq, int32_t* mark, int32_t* err, hipStream_t s);
 hipError_t ipc_wait(const int32_t* flags, int world, int self, const int32_t* tbase, int k,
                     int32_t seq, int32_t* err, hipStream_t s);
 hipError_t ipc_recv(const PushArgs& a, int world, int self, int64_t bytes, const int32_t* flags,
@@ -269,12 +272,14 @@ hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int ca
 // ---- the fused sharded step over the IPC transport (step.hip; two launches per step) ----
 // K2 whose per-slot gradients go straight to the owners: slot s of owner p = s / S lands at
 // dst[p] + (s % S) * ld; once every workgroup's stores are acknowledged the launch's last
-// workgroup raises flag[p] (non-null) to the step number; done: [9] counters, zero between launches
+// workgroup (a finisher polling the others' completion marks) raises flag[p] (non-null) to the
+// step number
 struct GradRoute {
   float* dst[kMaxWorld];
   int32_t* flag[kMaxWorld];
   int S = 0, world = 1;
-  uint32_t* done = nullptr;
+  int32_t* mark = nullptr;  // completion board, >= kBoardMax words
+  int32_t* err = nullptr;
 };
 hipError_t item_step_push(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                           const int32_t* tbase, int step, float* contrib, float* ugrad, float* xloss,
@@ -287,11 +292,12 @@ struct OwnerArgs {
   const int32_t* gfree = nullptr;
   int64_t n = 0;
   int world = 1, cap = 0, self = 0;
+  int max_blocks = kBoardMax;  // owner workgroups at most (grid-stride beyond)
   const float* grads_recv = nullptr;
   const float* self_grads = nullptr;
   const int32_t* wait_flags = nullptr;
   PushArgs dst;
-  uint32_t* done = nullptr;
+  int32_t* mark = nullptr;  // completion board of the owner workgroups, >= kBoardMax words
 };
 // owner phase of step `step` of the chunk (0: gather step 0; else apply step-1 and gather step)
 // in the first workgroups, K1 of `step` (sharded, waiting for every rank's row flags) in the rest
@@ -303,12 +309,14 @@ hipError_t dist_owner_step(const Geom& g, Table Q, const int32_t* ids_recv, cons
                            const int32_t* gdep, const int32_t* gfree, int64_t n, int world, int cap,
                            int k, const Hyper& hp, const int32_t* tbase, const float* grads_recv,
                            int self, const float* self_grads, const int32_t* wait_flags,
-                           int32_t* err, const PushArgs& dst, uint32_t* done, hipStream_t s);
-// row of position (p, idx) -> dst.dst[p] + idx * ld; done != null: bounded grid, the last
-// workgroup raises dst.flag[p] (IPC) to the step number
+                           int32_t* err, const PushArgs& dst, int32_t* mark, int max_blocks,
+                           hipStream_t s);
+// row of position (p, idx) -> dst.dst[p] + idx * ld; mark != null (IPC): a finisher workgroup
+// raises dst.flag[p] to the step number once every other workgroup's stores are acknowledged
 hipError_t dist_owner_gather(const Geom& g, Table Q, const int32_t* ids_recv, int64_t n, int world,
                              int cap, int k, const Hyper& hp, const int32_t* tbase,
-                             const PushArgs& dst, uint32_t* done, hipStream_t s);
+                             const PushArgs& dst, int32_t* mark, int32_t* err, int max_blocks,
+                             hipStream_t s);
 // wait_flags != null (IPC): every workgroup first waits for the peers' gradient flags
 hipError_t dist_owner_apply(const Geom& g, Table Q, const int32_t* ids_recv, const int32_t* aplan,
                             int64_t n, int world, int cap, int k, const Hyper& hp,

@@ -654,10 +654,9 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
 
 // ---- the fused sharded step over the IPC transport (dist.cpp enqueue_steps, two launches/step) ----
 // Back: K2 of step t (sharded: per-slot gradients) written straight into the owners' landing
-// buffers (GradRoute), then a two-level completion count (per XCD-parity group of workgroups, then
-// the groups) so the launch's last workgroup, once every workgroup's stores are acknowledged,
-// raises each peer's gradient flag to t (the pattern of dist.hip k_ipc_push, with the push kernel
-// gone).
+// buffers (GradRoute); each workgroup marks the completion board once its stores are acknowledged,
+// and the grid's last workgroup (the finisher) raises each peer's gradient flag to t once every
+// mark is in (the pattern of dist.hip k_ipc_push, with the push kernel gone).
 template <int G4, int S, int KB>
 __global__ __launch_bounds__(KB) void k_item_step_push(BatchView bv, Table P, Table Q, Hyper hp,
                                                        int ld, const int32_t* __restrict__ tbase,
@@ -665,24 +664,14 @@ __global__ __launch_bounds__(KB) void k_item_step_push(BatchView bv, Table P, Ta
                                                        int item_blocks, double* __restrict__ loss,
                                                        int B, GradRoute gr) {
   const int32_t t = *tbase + step + 1;
+  const int nprod = (int)gridDim.x - 1;
+  if ((int)blockIdx.x == nprod) {
+    board_finish(gr.mark, nprod, t, gr.flag, gr.world, gr.err);
+    return;
+  }
   k2_body<G4, S, true, KB, true, false>(blockIdx.x, bv, P, Q, hp, ld, t, sb, long_blocks,
                                         item_blocks, nullptr, loss, B, &gr);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's (remote) stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned grp = blockIdx.x & 7u, ngrp = min(gridDim.x, 8u);
-    const unsigned in_grp = (gridDim.x - grp + 7u) / 8u;  // workgroups b with b % 8 == grp
-    const uint32_t prev = __hip_atomic_fetch_add(gr.done + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == in_grp - 1) {
-      __hip_atomic_store(gr.done + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t top = __hip_atomic_fetch_add(gr.done + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (top == ngrp - 1) {
-        __hip_atomic_store(gr.done + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int p = 0; p < gr.world; ++p)
-          if (gr.flag[p]) __hip_atomic_store(gr.flag[p], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  board_mark(gr.mark, blockIdx.x, t);
 }
 
 // Front: the owner phase of step t (k == 0 of a chunk: gather step 0's rows; else apply step k-1
@@ -699,16 +688,20 @@ __global__ __launch_bounds__(kBlock) void k_dist_front(OwnerArgs o, BatchView bv
   if ((int)blockIdx.x < ob) {
     if (step == 0)
       owner_gather_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.n, o.world, o.cap, 0, hp, ld, tbase,
-                               o.dst, o.done);
+                               o.dst, o.mark);
     else
       owner_step_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.aplan, o.gdep, o.gfree, o.n, o.world,
                              o.cap, step - 1, hp, ld, tbase, o.grads_recv, o.self, o.self_grads,
-                             o.wait_flags, pw.err, o.dst, o.done);
+                             o.wait_flags, pw.err, o.dst, o.mark);
+    return;
+  }
+  if ((int)blockIdx.x == ob) {  // the owner workgroups' finisher: every rank's row flag for us
+    board_finish(o.mark, ob, *tbase + step + 1, o.dst.flag, o.world, pw.err);
     return;
   }
   wait_peer_flags(pw.flags, pw.world, -1, *tbase + step + 1, pw.err);
-  k1_body<G4, S, true, true, false>(blockIdx.x - ob, bv, P, Q, hp, ld, *tbase + step + 1, sb, item_rows,
-                                    B, nullptr);
+  k1_body<G4, S, true, true, false>(blockIdx.x - ob - 1, bv, P, Q, hp, ld, *tbase + step + 1, sb,
+                                    item_rows, B, nullptr);
 }
 
 // BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread
@@ -837,10 +830,11 @@ hipError_t item_step_push(const Geom& g, BatchView bv, int B, Table P, Table Q, 
                           double* loss, const GradRoute& gr, hipStream_t s) {
   const StepBufs sb = plain_bufs(contrib, ugrad, xloss, nullptr);
   if (!xloss) loss = nullptr;
-  if (!gr.done || gr.S <= 0) return hipErrorInvalidValue;
+  if (!gr.mark || gr.S <= 0) return hipErrorInvalidValue;
   BPRMF_DISPATCH4(g, ({
     const K2Grid k = k2_grid<G4_, 256>(B, loss != nullptr);
-    k_item_step_push<G4_, S_, 256><<<(unsigned)k.total(), 256, 0, s>>>(
+    if (k.total() > kBoardMax) return hipErrorInvalidValue;
+    k_item_step_push<G4_, S_, 256><<<(unsigned)k.total() + 1, 256, 0, s>>>(
         bv, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, loss, B, gr);
   }));
   return hipGetLastError();
@@ -850,15 +844,16 @@ hipError_t dist_front(const Geom& g, const OwnerArgs& o, BatchView bv, int B, Ta
                       const Hyper& hp, const int32_t* tbase, int step, float* contrib, float* ugrad,
                       float* xloss, const float* item_rows, const PeerWait& pw, hipStream_t s) {
   const StepBufs sb = plain_bufs(contrib, ugrad, xloss, nullptr);
-  if (!o.done || o.cap <= 0) return hipErrorInvalidValue;
+  if (!o.mark || o.cap <= 0) return hipErrorInvalidValue;
   BPRMF_DISPATCH4(g, ({
     // the owner grid of dist.hip's launches: one lane group per position (two per position for
-    // the fused apply + gather), at most 160 workgroups (one `done` increment each)
+    // the fused apply + gather), then the owners' finisher, then K1
     const int64_t units = (step == 0 ? 1 : 2) * (int64_t)o.world * o.cap * G4_;
-    const int ob = (int)std::max<int64_t>(1, std::min<int64_t>(160, (units + kBlock - 1) / kBlock));
+    const int ob = (int)std::max<int64_t>(
+        1, std::min<int64_t>(std::min(o.max_blocks, kBoardMax), (units + kBlock - 1) / kBlock));
     const int k1b = (B + kBlock / G4_ - 1) / (kBlock / G4_);
-    k_dist_front<G4_, S_><<<(unsigned)(ob + k1b), kBlock, 0, s>>>(o, bv, P, Q, hp, g.ld, tbase, step, sb,
-                                                                 item_rows, pw, ob, B);
+    k_dist_front<G4_, S_><<<(unsigned)(ob + 1 + k1b), kBlock, 0, s>>>(o, bv, P, Q, hp, g.ld, tbase, step,
+                                                                     sb, item_rows, pw, ob, B);
   }));
   return hipGetLastError();
 }

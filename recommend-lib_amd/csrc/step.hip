@@ -162,12 +162,14 @@ static __device__ __forceinline__ void put_stamp(int32_t* stamp, int32_t t, bool
 // stamps).  WAIT (fused step, k_fused_step): this K1 runs beside K2 of step t-1, so a row that
 // step t-1 updates (pend[(t-1)&1][row] == t-1, written by K1 of step t-1 in the previous launch)
 // is read only after its owner publishes stamp t-1.  pend (single GPU): every triplet marks its
-// rows with t (users: only those K2 finishes), for K1 of step t+1.
+// rows with t (users: only those K2 finishes), for K1 of step t+1.  pw (sharded, fused front
+// launch): the record and the user row are loaded first, then the workgroup waits for the row
+// flags, then the item rows are read.
 template <int G4, int S, bool SH, bool WT, bool WAIT>
 static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, const float* __restrict__ item_rows,
-                                               int B, int32_t* err) {
+                                               int B, int32_t* err, const PeerWait* pw = nullptr) {
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = WAIT || !kFusedStampsOnly;
 #endif
@@ -189,6 +191,14 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
   int w = 0;
   int32_t u = 0;
   __shared__ float4 s_g[S * kBlock];  // per-triplet user gradients of in-workgroup segments
+  if (pw) {  // the user row (this rank's, final since the previous launch) while the owners work
+    if (p < n) {
+      const float* pr = P.W + (int64_t)r.z * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) pu[k] = ld4(pr + 4 * G4 * k);
+    }
+    wait_peer_flags(pw->flags, pw->world, pw->self, t, pw->err);
+  }
   if (p < n) {
     // bit 31: the item's first reference in the batch; bit 30 (single GPU): its ONLY reference,
     // so this triplet finishes the item (no contribution row, no K2 record)
@@ -253,7 +263,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     } else {
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        pu[k] = ld4(prow + 4 * G4 * k);
+        if (!pw) pu[k] = ld4(prow + 4 * G4 * k);
         vi[k] = ld4(qi + 4 * G4 * k);
         vj[k] = ld4(qj + 4 * G4 * k);
       }
@@ -699,9 +709,9 @@ __global__ __launch_bounds__(kBlock) void k_dist_front(OwnerArgs o, BatchView bv
     board_finish(o.mark, ob, *tbase + step + 1, o.dst.flag, o.world, pw.err);
     return;
   }
-  wait_peer_flags(pw.flags, pw.world, -1, *tbase + step + 1, pw.err);
+  const PeerWait all{pw.flags, pw.world, -1, pw.err};  // every rank's rows, this one's included
   k1_body<G4, S, true, true, false>(blockIdx.x - ob - 1, bv, P, Q, hp, ld, *tbase + step + 1, sb,
-                                    item_rows, B, nullptr);
+                                    item_rows, B, nullptr, &all);
 }
 
 // BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread

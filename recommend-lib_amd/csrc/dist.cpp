@@ -175,12 +175,20 @@ struct IpcTransport final : Transport {
   // per-step fusion (enqueue_steps): the owners' gather writes rows straight into the peers' row
   // landing buffers, K1 reads them there after waiting on its flags, and the apply waits on the
   // gradient flags itself; only the gradient push remains a separate kernel
-  // BPRMF_DIST_FUSE=0: every exchange as push + receive copy into cached buffers; =1: the fused
-  // forms at world 1 too (A/B of what they cost on one device)
+  // The fused forms need one rank per GPU: their consumers wait inside kernels (K1 workgroups on
+  // the row flags, owner workgroups on the gradient flags), and ranks sharing a device fill it
+  // with spinning workgroups until a peer cannot run the kernel that would release them (8
+  // ranks on one GPU timed out).  Shared device: every exchange is a push kernel plus a receive
+  // copy (or one waiting block), and no step kernel spins.  BPRMF_DIST_FUSE=0/1 forces either
+  // (1: also at world 1, to measure what the fused forms cost on one device); BPRMF_DIST_FUSE2=1
+  // forces the two-launch form.
   bool fused() const {
+    if (!opened || self_exchange) return false;
     const char* e = getenv("BPRMF_DIST_FUSE");
-    if (e && *e) return opened && !self_exchange && e[0] != '0';
-    return opened && !self_exchange && world > 1;
+    if (e && *e) return e[0] != '0';
+    const char* e2 = getenv("BPRMF_DIST_FUSE2");
+    if (e2 && *e2 && e2[0] != '0') return true;
+    return world > 1 && !shared_device;
   }
   // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
   // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
@@ -190,9 +198,10 @@ struct IpcTransport final : Transport {
   // owner workgroups need (measured: 4 ranks on one MI355X time out).  One rank per GPU (the
   // 8-GPU node) has no such coupling: each launch's owner workgroups are dispatched first.
   bool fused2() const {
+    if (!fused()) return false;
     const char* e = getenv("BPRMF_DIST_FUSE2");
-    if (e && *e) return fused() && e[0] != '0';
-    return fused() && !shared_device;
+    if (e && *e) return e[0] != '0';
+    return !shared_device;
   }
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
   void* peer_landing(int kind, int p) const { return remote[kind][p]; }

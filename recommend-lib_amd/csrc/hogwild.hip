@@ -158,6 +158,7 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
   const float lr = hp.lr, wd = hp.wd;
   const bool nostore = fl & 4;
   const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
+  const bool user_wb = fl & 64;  // A/B: user rows stored write-back (plain), item rows sc1
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
@@ -207,7 +208,10 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
         }
         continue;
       }
-      if (!nousers) hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
+      if (user_wb)
+        *reinterpret_cast<float4*>(pr + 4 * G4 * k) = hw_sgd(pu, gu, lr, fu1 ? wd : 0.f);
+      else if (!nousers)
+        hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
       if (!noitems) {
         hw_st4(qi + 4 * G4 * k, hw_sgd(vi, gi, lr, fi1 ? wd : 0.f));
         if (!same) hw_st4(qj + 4 * G4 * k, hw_sgd(vj, gj, lr, fj1 ? wd : 0.f));
@@ -344,7 +348,7 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   int fl = (pl && pl[0] == '1') ? 0 : 1;
   // diagnostic timing only (wrong results): bit 1 = no row loads, bit 2 = no row stores, bit 3 =
   // plain (write-back) row stores, bit 4 = no item row stores, bit 5 = no user row stores
-  if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 62);
+  if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 126);
   SamplerArgs a{};
   if (sa) a = *sa;
   BPRMF_DISPATCH4(g, ({

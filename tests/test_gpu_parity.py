@@ -514,6 +514,41 @@ def test_hr_ndcg_parity_ml100k(rl):
         assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)
 
 
+def test_headline_dim_training_and_hr_match_dense_oracle(rl):
+    """The headline dimension (d=128) end to end on the F5 data: 3 epochs of the device path
+    (sampler + batch build + fused steps) against the C dense oracle replaying the same triplets
+    (the sampler spec is bit-exact) from the same initial tables, then HR@10 / NDCG@10 of both
+    weight sets ranked by the same device ranker.  Tolerances: fp32 sums in a different order over
+    ~240 steps (weights); the two models' rankings may differ only by near-ties."""
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        p = json.load(fh)["protocol"]
+    U, I, d, B, seed, epochs = int(f["U"]), int(f["I"]), 128, p["batch_size"], 11, 3
+    pos = f["positives"].astype(np.int64)
+    m = rl.BPRMF(U, I, d, lr=p["lr"], wd=p["wd"], batch_size=B, num_ng=p["num_ng"], seed=seed)
+    m.set_train(pos)
+    P0, Q0 = m.get_weights()
+    ref = C.DenseTrainer(P0, Q0, p["lr"], p["wd"])
+    indptr, indices = O.build_csr(pos[:, 0], pos[:, 1], U)
+    N, S = m.epoch_size()
+    for e in range(epochs):
+        m.train_epoch(e)
+        u, i, j = C.sample(pos[:, 0], pos[:, 1], indptr, indices, I, p["num_ng"], seed, e, 0, N)
+        for s in range(S):
+            ref.step(u[s * B:(s + 1) * B], i[s * B:(s + 1) * B], j[s * B:(s + 1) * B])
+    P, Q = m.get_weights()
+    np.testing.assert_allclose(P, ref.P, rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(Q, ref.Q, rtol=1e-4, atol=2e-5)
+    gt = {int(uu): set(f["gt_items"][f["gt_ptr"][k]:f["gt_ptr"][k + 1]].tolist())
+          for k, uu in enumerate(f["gt_users"])}
+    o = rl.BPRMF(U, I, d, lr=p["lr"], wd=p["wd"], batch_size=B, num_ng=p["num_ng"], seed=seed)
+    o.set_weights(ref.P, ref.Q)
+    km = rl.metrics.evaluate_topk(m, f["test_data"], gt, p["topk"])
+    ko = rl.metrics.evaluate_topk(o, f["test_data"], gt, p["topk"])
+    print("d=128 HIP:", km, "oracle:", ko)
+    assert abs(km["hr"] - ko["hr"]) <= 1e-3 and abs(km["ndcg"] - ko["ndcg"]) <= 2e-3
+
+
 # ---------------------------------------------------------------------------------------------
 # full-size properties (ml-20m shape)
 # ---------------------------------------------------------------------------------------------

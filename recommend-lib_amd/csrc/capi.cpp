@@ -88,6 +88,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_INVALID, "batch_size and num_ng must be positive");
   if (cfg->world <= 0 || cfg->rank < 0 || cfg->rank >= cfg->world)
     return fail(BPRMF_E_INVALID, "need 0 <= rank < world");
+  if (cfg->world > kMaxWorld)
+    return fail(BPRMF_E_UNSUPPORTED, "world %d > %d ranks", cfg->world, kMaxWorld);
   if (!(cfg->lr >= 0.f) || !(cfg->weight_decay >= 0.f) || !(cfg->init_std >= 0.f))
     return fail(BPRMF_E_INVALID, "lr, weight_decay and init_std must be >= 0");
   Geom g;

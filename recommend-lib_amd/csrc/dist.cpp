@@ -54,6 +54,7 @@ struct Transport {
   // in-place max over ranks of one device int32; vals: [world] scratch peers may write into
   virtual int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) {
     const int W = h->cfg.world;
+    if (W == 1 && !self_exchange) return 0;  // the max over one rank
     std::vector<const void*> sp(W, dev);
     std::vector<void*> rp(W);
     for (int p = 0; p < W; ++p) rp[p] = vals + p;
@@ -649,7 +650,6 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     }
   }
   // exchange capacity of the chunk: the largest request count of any (rank, step, owner)
-  HIPCHK(hipMemsetAsync(d->d_cap, 0, 4, h->stream));
   HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
   if (int r = d->tr->max_i32(h, d->d_cap, d->vals + par * W, seq)) return r;
   // cap and the error word back in one wait: a tiny kernel writes them and then a sequence

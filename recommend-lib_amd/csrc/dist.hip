@@ -23,12 +23,21 @@ namespace bprmf {
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 static __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-// largest per-owner request count of the chunk (the exchange capacity), max-reduced into *cap
-__global__ void k_own_max(BatchBuf bb, int64_t n, int world, int32_t* __restrict__ cap) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= n * world) return;
-  const int32_t c = bb.view(x / world).own[x % world];
-  if (c > 0) atomicMax(cap, c);
+// largest per-owner request count of the chunk (the exchange capacity) into *cap: ONE workgroup
+// (n * world <= 256 steps x 64 owners), so no zeroing launch and no atomics
+__global__ __launch_bounds__(1024) void k_own_max(BatchBuf bb, int64_t n, int world,
+                                                  int32_t* __restrict__ cap) {
+  __shared__ int32_t part[1024 / 64];
+  int32_t m = 0;
+  for (int64_t x = threadIdx.x; x < n * world; x += blockDim.x)
+    m = max(m, bb.view(x / world).own[x % world]);
+  for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x / 64); ++w) m = max(m, part[w]);
+    *cap = m;
+  }
 }
 
 // ids_send[p][k][idx] = request idx of step k to owner p (its local row), -1 past the count
@@ -328,7 +337,7 @@ static unsigned blocks_for(int64_t threads) { return (unsigned)((threads + kBloc
 
 hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  k_own_max<<<blocks_for(n * world), kBlock, 0, s>>>(bb, n, world, cap);
+  k_own_max<<<1, 1024, 0, s>>>(bb, n, world, cap);
   return hipGetLastError();
 }
 

@@ -58,7 +58,10 @@ constexpr int kRec = 8;
 constexpr int kLongSeg = 16;
 constexpr int kInlineRefs = 12;  // refs held in an item segment's record (B <= 8192: 14-bit refs)
 constexpr int kMaxLongItems = 64;  // hot items per batch given a whole workgroup in K2
-constexpr int kMaxWorld = 64;
+// ranks of a sharded run at most: the per-peer tables (PushArgs, GradRoute) travel as kernel
+// arguments every step, and their size is what a launch costs on the host (one node's 8 GPUs,
+// with room to spare)
+constexpr int kMaxWorld = 16;
 constexpr int kBoardMax = 16384;  // producing workgroups one completion board tracks
 struct BatchView {
   int32_t *trec, *mrec, *irec, *lrec, *refs, *useg, *ioff, *ukey, *meta, *own;

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   const int nb = (int)max<int64_t>(0, min<int64_t>(B, n_slots - b0));
   const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
   const BatchView v = bb.view(batch);
-  if (tid < kMaxWorld) s_own[tid] = 0;
+  if (tid < kMaxWorld) s_opre[tid] = -1;  // sharded: first item segment of each owner, if any
   if (batch == 0 && ci.cursor) {  // set_cursor's work (kernels.hip k_set_cursor)
     if (tid == 0) {
       ci.cursor[0] = ci.t;
@@ -440,8 +440,12 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
         else
           v.ioff[s] = r;  // radix build: the segment starts go through global memory
         if (slots) {
+          // segments are owner-major: an owner's first segment is the head whose previous
+          // reference has another owner (no per-head atomics on a few shared counters)
+          const uint32_t o = ik[k] / (uint32_t)iloc;
+          const uint32_t pk = k ? ik[k - 1] : iprev;
           v.ukey[s] = (int32_t)(ik[k] % (uint32_t)iloc);
-          atomicAdd(&s_own[ik[k] / (uint32_t)iloc], 1);
+          if (pk == kNone || pk / (uint32_t)iloc != o) s_opre[o] = s;
         }
       }
       // triplet side -> its item slot (sharded); bit 31: this reference is its item's first in
@@ -461,12 +465,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   auto ref_at = [&](int r) { return BUCKET ? s_refs[r] : v.refs[r]; };
   __syncthreads();  // ioff, refs, slots, s_own visible block-wide
   BSTAMP(5);
-  if (slot_stride) {
-    if (tid == 0) {
-      int acc = 0;
-      for (int o = 0; o < world; ++o) {
-        s_opre[o] = acc;
-        acc += s_own[o];
+  if (slots) {
+    if (tid == 0) {  // owners without segments start where the next one does; counts by difference
+      int next = n_iseg;
+      for (int o = world - 1; o >= 0; --o) {
+        if (s_opre[o] < 0) s_opre[o] = next;
+        s_own[o] = next - s_opre[o];
+        next = s_opre[o];
       }
     }
     __syncthreads();

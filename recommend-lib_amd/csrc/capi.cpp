@@ -694,6 +694,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     if (!ru && split_build(nb)) {
       if (int r = ensure_trip(h, n)) return r;
       int32_t* tu = h->d_trip;
+      trace_mark();
       HIPCHK(sample(sampler_args(h), epoch, first_slot, n, tu, tu + h->trip_cap,
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
       trace_mark();

@@ -178,13 +178,16 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
 
 // BUCKET: bucket sorts (B <= kBuildThreads * 4); else rocPRIM block radix sorts.  Both give the
 // same arrangement, so the batches (and every step result) are identical either way.
-template <int IPT, bool BUCKET>
+// W1: one rank (world 1, item rows, no slots), so every owner / local-row division folds away
+template <int IPT, bool BUCKET, bool W1>
 __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
     SamplerArgs a, uint32_t epoch, int64_t first_slot, int64_t n_slots, int B,
     const int32_t* __restrict__ ru, const int32_t* __restrict__ ri, const int32_t* __restrict__ rj,
-    int64_t u_rows, int64_t i_rows, int world, int64_t iloc, int slots, int slot_stride,
+    int64_t u_rows, int64_t i_rows, int world_in, int64_t iloc, int slots_in, int slot_stride,
     int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb, int32_t* __restrict__ err,
     CursorInit ci) {
+  const int world = W1 ? 1 : world_in;
+  const int slots = W1 ? 0 : slots_in;
   constexpr int T = kBuildThreads;
   constexpr int IPT2 = 2 * IPT;
   using SortU = rocprim::block_radix_sort<uint32_t, T, IPT, uint32_t>;
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
       } else {
         const uint64_t q = permute((uint64_t)(first_slot + b0 + p), N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
         const int64_t pp = div_small(q, (uint32_t)a.num_ng);
-        const int64_t ul = a.pos_u[pp] / a.world;
+        const int64_t ul = a.pos_u[pp] / (W1 ? 1 : a.world);
         i = a.pos_i[pp];
         const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
         const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
@@ -576,18 +579,21 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // the trec flag bits 30-31 need item ids below 2^30
   const char* k1e = getenv("BPRMF_K1_ITEMS");
   const int k1_items = (!slots && i_rows < (1LL << 30) && !(k1e && k1e[0] == '0')) ? 1 : 0;
-  if (B <= kBuildThreads * 4 && !radix)
-    k_build_batches<4, true><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
-        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
-  else if (B <= kBuildThreads * 4)
-    k_build_batches<4, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
-        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
-  else
-    k_build_batches<8, false><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(
-        a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,
-        slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci);
+  const char* w1e = getenv("BPRMF_BUILD_W1");  // =0: the generic kernel at world 1 too (A/B)
+  const bool w1 = world == 1 && !slots && a.world == 1 && !(w1e && w1e[0] == '0');
+#define BPRMF_BUILD(IPT_, BUCKET_, W1_)                                                          \
+  k_build_batches<IPT_, BUCKET_, W1_><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(               \
+      a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,  \
+      slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci)
+  if (B <= kBuildThreads * 4 && !radix) {
+    if (w1) BPRMF_BUILD(4, true, true);
+    else BPRMF_BUILD(4, true, false);
+  } else if (B <= kBuildThreads * 4) {
+    BPRMF_BUILD(4, false, false);
+  } else {
+    BPRMF_BUILD(8, false, false);
+  }
+#undef BPRMF_BUILD
   return hipGetLastError();
 }
 

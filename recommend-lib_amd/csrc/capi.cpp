@@ -67,6 +67,7 @@ int bprmf::check_err_flag(bprmf_handle* h) {
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
+    if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
     return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
   }
@@ -416,6 +417,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 8) return fail(BPRMF_E_HIP, "fused step: a row's owner never published it (wait timed out)");
+    if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
     return fail(BPRMF_E_RANGE, "user/item id out of range (device check)");
   }

@@ -15,6 +15,7 @@
 
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/block/block_scan.hpp>
+#include <type_traits>
 
 #include "device_common.h"
 
@@ -70,7 +71,7 @@ struct BucketScratch {
 };
 
 template <int T, int E, class KeyOf, class ValOf>
-static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t (&val)[E], int bits,
+static __device__ __forceinline__ int bucket_sort(uint32_t (&key)[E], uint32_t (&val)[E], int bits,
                                                    const BucketScratch<T>& sc, KeyOf key_of,
                                                    ValOf val_of, int sb = -1) {
   // sb >= 0 (diagnostic build): stamps sb .. sb+4 after count, scan, scatter, rank, gather
@@ -174,6 +175,7 @@ static __device__ __forceinline__ void bucket_sort(uint32_t (&key)[E], uint32_t 
   __syncthreads();  // the caller reuses the scratch (its sorted keys alias bk)
   BSTAMP_SORT(4);
 #undef BSTAMP_SORT
+  return total;
 }
 
 // BUCKET: bucket sorts (B <= kBuildThreads * 4); else rocPRIM block radix sorts.  Both give the
@@ -549,6 +551,411 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
   BSTAMP(8);
 }
 
+// ================================================================================================
+// Split builder: one rank (item rows, no slots), triplets already in memory (the grid-wide
+// sampler's or replayed ids), B <= kBuildThreads * 4.  The single-workgroup builder above spends
+// most of its ~32 us on the 2B item references of a batch (sort, segment heads, records) while 255
+// other CUs idle.  Here each batch gets 1 + kItemParts workgroups:
+//   role 0      the user side: user sort, user segments, trec {u, w} words, mrec, meta[0,1,4];
+//   role 1 + q  the item references whose item lies in key range q (kItemParts equal ranges of
+//               the item id space): their sort, segment heads, trec {i, j} words (item | first /
+//               sole bits), refs, item and long-item records.
+// Every workgroup sorts the batch's triplets by user itself (a reference's value and its place in
+// the fixed summation order are the triplet's position in user order), so no workgroup waits for
+// another's sort.  Item segments, K2 records and long records are numbered across the parts in key
+// order, as the one-workgroup build numbers them: part q publishes its three counts (tagged with
+// the launch's tag) and waits for parts 0 .. q-1's before it writes records.  The batch buffer
+// comes out identical to k_build_batches's, bit for bit (refs, records, trec, meta).
+// ================================================================================================
+constexpr int kItemParts = 4;
+constexpr int kItemPartBits = 2;  // log2(kItemParts)
+
+// bucket_sort over the VALID elements (key != kNone) of a blocked E-per-thread input whose keys lie
+// in [lo, lo + 2^bits): the same order (stable by key, ties by input position), but absent
+// elements take no part (no count, no rank), and the sorted elements come out in a blocked
+// E2-per-thread arrangement (positions past the count: kNone).  The caller guarantees
+// count <= T * E2.  Returns the count.
+template <int T, int E, int E2, class KeyOf, class ValOf>
+static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E], uint32_t lo,
+                                                         int bits, const BucketScratch<T>& sc,
+                                                         KeyOf key_of, ValOf val_of,
+                                                         uint32_t (&okey)[E2], uint32_t (&oval)[E2]) {
+  using Scan = rocprim::block_scan<int, T>;
+  constexpr int PB = kBuckets / T;
+  const int tid = threadIdx.x;
+  const int shift = bits > kBucketBits ? bits - kBucketBits : 0;
+  for (int b = tid; b <= kBuckets; b += T) sc.start[b] = 0;
+  __syncthreads();
+  int li[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k)
+    li[k] = key[k] != kNone ? atomicAdd(&sc.start[(key[k] - lo) >> shift], 1) : -1;
+  __syncthreads();
+  int c[PB], sum = 0;
+#pragma unroll
+  for (int m = 0; m < PB; ++m) {
+    c[m] = sc.start[tid * PB + m];
+    sum += c[m];
+  }
+  int pre = 0, total = 0;
+  Scan().exclusive_scan(sum, pre, 0, total, *sc.scan, rocprim::plus<int>());
+#pragma unroll
+  for (int m = 0; m < PB; ++m) {
+    sc.start[tid * PB + m] = pre;
+    pre += c[m];
+  }
+  if (tid == 0) sc.start[kBuckets] = total;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E; ++k)
+    if (li[k] >= 0)
+      sc.bk[sc.start[(key[k] - lo) >> shift] + li[k]] = ((uint64_t)key[k] << 32) | (uint32_t)(tid * E + k);
+  __syncthreads();
+  // rank inside the bucket (bucket_sort's phase 4), over the count's elements only
+  constexpr int R = (E2 * T + T - 1) / T;  // elements per thread in the strided rank pass
+  {
+    uint64_t me[R];
+    int bs[R], be[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) me[k] = tid + k * T < total ? sc.bk[tid + k * T] : ~0ull;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int b = min((int)(((uint32_t)(me[k] >> 32) - lo) >> shift), kBuckets - 1);
+      bs[k] = sc.start[b];
+      be[k] = sc.start[b + 1];
+    }
+    int rank[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int last = max(total - 1, 0);
+      const uint64_t a0 = sc.bk[min(bs[k], last)], a1 = sc.bk[min(bs[k] + 1, last)];
+      rank[k] = (int)(be[k] > bs[k] && a0 < me[k]) + (int)(be[k] > bs[k] + 1 && a1 < me[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (tid + k * T >= total) continue;
+      int y = bs[k] + 2;
+      for (; y + 4 <= be[k]; y += 4) {
+        const uint64_t a0 = sc.bk[y], a1 = sc.bk[y + 1], a2 = sc.bk[y + 2], a3 = sc.bk[y + 3];
+        rank[k] += (int)(a0 < me[k]) + (int)(a1 < me[k]) + (int)(a2 < me[k]) + (int)(a3 < me[k]);
+      }
+      for (; y < be[k]; ++y) rank[k] += sc.bk[y] < me[k];
+      sc.srt[bs[k] + rank[k]] = (int32_t)(uint32_t)me[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E2; ++k) {
+    const int pos = tid * E2 + k;
+    if (pos < total) {
+      const int q = sc.srt[pos];
+      okey[k] = key_of(q);
+      oval[k] = val_of(q);
+    } else {
+      okey[k] = kNone;
+      oval[k] = 0;
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
+// The parts' counts for the batch, in 64-bit words {tag, payload} (one store each, write-through):
+// xch[2q] = tag << 32 | n_iseg | n_mseg << 16, xch[2q + 1] = tag << 32 | n_long.  The area is the
+// batch's ukey range (sharded mode only; 8-byte aligned).
+static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
+  return reinterpret_cast<uint64_t*>(v.ukey);
+}
+
+__global__ __launch_bounds__(kBuildThreads) void k_build_split(
+    int64_t n_slots, int B, const int32_t* __restrict__ ru, const int32_t* __restrict__ ri,
+    const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int user_bits, int item_bits,
+    int tpb, int k1_items, BatchBuf bb, int32_t* __restrict__ err, CursorInit ci, uint32_t tag) {
+  constexpr int T = kBuildThreads;
+  constexpr int IPT = 4;
+  constexpr int IPT2 = 2 * IPT;
+  using Scan = rocprim::block_scan<int, T>;
+  using ScanL = rocprim::block_scan<uint64_t, T>;
+  constexpr size_t kBucketBytes = 12 * (size_t)T * IPT2 + 4 * (kBuckets + 4);
+  __shared__ __attribute__((aligned(16))) unsigned char s_sort[kBucketBytes];
+  __shared__ typename Scan::storage_type sscan;
+  __shared__ typename ScanL::storage_type sscan64;
+  __shared__ int32_t s_i[T * IPT];  // per sorted position: item row
+  __shared__ int32_t s_j[T * IPT];
+  __shared__ int32_t s_ninv;
+  __shared__ int s_base[3];  // item parts: segments, K2 records, long records of the parts before
+  __shared__ int s_prev[kItemParts][3];
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_sort);
+  uint32_t* s_u = reinterpret_cast<uint32_t*>(s_sort) + 2 * T * IPT;
+  int32_t* s_refs = reinterpret_cast<int32_t*>(s_sort) + T * IPT2;
+  int32_t* s_ioff = reinterpret_cast<int32_t*>(s_sort + 8 * (size_t)T * IPT2);
+  BucketScratch<T> bs;
+  bs.bk = reinterpret_cast<uint64_t*>(s_sort);
+  bs.srt = reinterpret_cast<int32_t*>(s_sort + 8 * (size_t)T * IPT2);
+  bs.start = reinterpret_cast<int32_t*>(s_sort + 12 * (size_t)T * IPT2);
+  bs.ninv = &s_ninv;
+  bs.scan = &sscan;
+  const int tid = threadIdx.x;
+  const int role = (int)(blockIdx.x % (kItemParts + 1));
+  const int64_t batch = blockIdx.x / (kItemParts + 1);
+  const int64_t b0 = batch * (int64_t)B;
+  const int nb = (int)max<int64_t>(0, min<int64_t>(B, n_slots - b0));
+  const BatchView v = bb.view(batch);
+  if (batch == 0 && role == 0 && ci.cursor) {  // set_cursor's work (kernels.hip k_set_cursor)
+    if (tid == 0) {
+      ci.cursor[0] = ci.t;
+      ci.cursor[1] = ci.k;
+    }
+    if (ci.loss && tid < ci.nloss) ci.loss[tid] = 0.0;
+  }
+
+  // 1. the batch's triplets in slot order, keyed by user row (as k_build_batches)
+  uint32_t key[IPT], val[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int p = tid * IPT + k;
+    key[k] = kNone;
+    val[k] = (uint32_t)p;
+    if (p < nb && ru[b0 + p] >= 0) {  // u < 0: an empty slot
+      const int32_t u = ru[b0 + p], i = ri[b0 + p], j = rj[b0 + p];
+      if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
+          (uint64_t)j < (uint64_t)i_rows) {
+        key[k] = (uint32_t)u;
+        s_u[p] = (uint32_t)u;
+        s_i[p] = i;
+        s_j[p] = j;
+      } else if (role == 0) {
+        atomicOr(err, 1);
+      }
+    }
+  }
+  const int nvalid = bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
+                                         [](int q) { return (uint32_t)q; });
+  // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
+  int32_t my_i[IPT], my_j[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const bool ok = key[k] != kNone;
+    my_i[k] = ok ? s_i[val[k]] : 0;
+    my_j[k] = ok ? s_j[val[k]] : 0;
+    s_key[tid * IPT + k] = key[k];
+  }
+  __syncthreads();  // slot-order reads of s_i/s_j done; s_key complete
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    s_i[tid * IPT + k] = my_i[k];  // sorted order from here on
+    s_j[tid * IPT + k] = my_j[k];
+  }
+
+  if (role == 0) {
+    // ---- user side: segments, w, trec {u, w}, mrec, meta (k_build_batches lines for these) ----
+    const uint32_t uprev = tid ? s_key[tid * IPT - 1] : kNone;
+    bool uhead[IPT];
+    int heads = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      uhead[k] = key[k] != kNone && (k ? key[k - 1] : uprev) != key[k];
+      heads += uhead[k];
+    }
+    int pre = 0, tot = 0;
+    Scan().exclusive_scan(heads, pre, 0, tot, sscan, rocprim::plus<int>());
+    const int seg0 = pre, n_useg = tot;
+    int32_t* s_seg = reinterpret_cast<int32_t*>(s_sort) + T * IPT;
+    {
+      int s = seg0;
+#pragma unroll
+      for (int k = 0; k < IPT; ++k)
+        if (uhead[k]) s_seg[s++] = tid * IPT + k;
+    }
+    __syncthreads();
+    int uend[IPT], uw[IPT], nmulti = 0;
+    {
+      int s = seg0 - 1;
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int p = tid * IPT + k;
+        uend[k] = p + 1;
+        uw[k] = 0;
+        if (key[k] != kNone) {
+          if (uhead[k]) ++s;
+          const int b = s_seg[max(s, 0)], e = s + 1 < n_useg ? s_seg[s + 1] : nvalid;
+          uend[k] = e;
+          const int len = e - b;
+          if (len == 1)
+            uw[k] = 1;
+          else if (b / tpb == (e - 1) / tpb)
+            uw[k] = p == b ? len : -1;
+        }
+        nmulti += uhead[k] && uw[k] == 0;
+      }
+    }
+    int mpre = 0, n_multi = 0;
+    __syncthreads();  // sscan reuse
+    Scan().exclusive_scan(nmulti, mpre, 0, n_multi, sscan, rocprim::plus<int>());
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = tid * IPT + k;
+      if (key[k] == kNone) continue;
+      reinterpret_cast<int2*>(v.trec + 4LL * p)[1] = make_int2((int)key[k], uw[k]);
+      if (uhead[k] && uw[k] == 0) {  // a segment K2 finishes
+        store_rec(v.mrec + (int64_t)mpre * kRec, (int)key[k], p, uend[k], 0, 0, 0, 0, 0);
+        ++mpre;
+      }
+    }
+    if (tid == 0) {
+      v.meta[0] = nvalid;
+      v.meta[1] = n_useg;
+      v.meta[4] = n_multi;
+    }
+    return;
+  }
+
+  // ---- item part q: references whose item lies in [lo, lo + 2^rb) ----
+  const int q = role - 1;
+  const int rb = max(item_bits - kItemPartBits, 0);
+  const uint32_t lo = (uint32_t)q << rb;
+  __syncthreads();  // s_i/s_j in sorted order; s_key free
+  uint32_t ik[IPT2];
+  int below = 0, mine = 0;  // references of this thread in the parts before / in this part
+#pragma unroll
+  for (int k = 0; k < IPT2; ++k) {
+    const int r = tid * IPT2 + k;
+    ik[k] = kNone;
+    if (r < 2 * nvalid) {
+      const uint32_t item = (uint32_t)(r < nvalid ? s_i[r] : s_j[r - nvalid]);
+      if (item >= lo && ((item - lo) >> rb) == 0) ik[k] = item;
+      below += item < lo;
+      mine += ik[k] != kNone;
+    }
+  }
+  int cpre0 = 0, ctot0 = 0;  // (refs before << 16 | refs here), each <= 2B <= 8192
+  Scan().exclusive_scan(below << 16 | mine, cpre0, 0, ctot0, sscan, rocprim::plus<int>());
+  const int rbase = ctot0 >> 16, n_mine = ctot0 & 0xFFFF;
+  // the sorted references come out E2 per thread: 4 (half the single-workgroup builder's 8) while
+  // the part holds at most 4T of the batch's 2B references (a part averages B / 2), else 8
+  auto part = [&](auto e2) {
+  constexpr int E2 = decltype(e2)::value;
+  uint32_t ok_[E2], ov[E2];
+  const int nv = nvalid;
+  const int total = bucket_sort_sparse<T, IPT2, E2>(
+      ik, lo, rb, bs,
+      [&](int r) { return (uint32_t)(r < nv ? s_i[r] : s_j[r - nv]); },
+      [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, ok_, ov);
+#pragma unroll
+  for (int k = 0; k < E2; ++k) s_key[tid * E2 + k] = ok_[k];
+  __syncthreads();
+  const uint32_t iprev = tid ? s_key[tid * E2 - 1] : kNone;
+  const uint32_t inext = tid + 1 < T ? s_key[(tid + 1) * E2] : kNone;
+  uint32_t hm = 0, sm = 0, lm = 0;
+  int iheads = 0, mheads = 0, nlong = 0;
+#pragma unroll
+  for (int k = 0; k < E2; ++k) {
+    const int r = tid * E2 + k;  // local position
+    if (ok_[k] == kNone) continue;
+    const bool h = (k ? ok_[k - 1] : iprev) != ok_[k];
+    const bool so = k1_items && h && (k + 1 < E2 ? ok_[k + 1] : inext) != ok_[k];
+    const bool lg = h && !so && r + kLongSeg < T * E2 && s_key[r + kLongSeg] == ok_[k];
+    hm |= (uint32_t)h << k;
+    sm |= (uint32_t)so << k;
+    lm |= (uint32_t)lg << k;
+    iheads += h;
+    mheads += h && !so;
+    nlong += lg;
+    v.refs[rbase + r] = (int32_t)ov[k];
+    s_refs[r] = (int32_t)ov[k];
+    // the triplet's item word: row | first reference of its item | only reference
+    const int32_t word = (int32_t)ok_[k] | (h ? (int32_t)0x80000000 : 0) | (so ? 0x40000000 : 0);
+    v.trec[4LL * (ov[k] >> 1) + (ov[k] & 1)] = word;
+  }
+  uint64_t cpre = 0, ctot = 0;
+  ScanL().exclusive_scan((uint64_t)iheads | (uint64_t)mheads << 16 | (uint64_t)nlong << 32, cpre, 0ull,
+                         ctot, sscan64, rocprim::plus<uint64_t>());
+  auto field = [](uint64_t x, int f) { return (int)((x >> (16 * f)) & 0xFFFF); };
+  const int iseg0 = field(cpre, 0), n_iseg = field(ctot, 0);
+  const int mseg0 = field(cpre, 1), n_mseg = field(ctot, 1);
+  const int n_long = field(ctot, 2);
+  {
+    int s = iseg0;
+#pragma unroll
+    for (int k = 0; k < E2; ++k)
+      if ((hm >> k) & 1) s_ioff[s++] = tid * E2 + k;
+  }
+  if (tid == 0) s_ioff[n_iseg] = total;
+  // publish this part's counts, then collect the parts before (the first q threads, one each)
+  uint64_t* xch = xch_of(v);
+  if (tid == 0) {
+    __hip_atomic_store(xch + 2 * q, (uint64_t)tag << 32 | (uint32_t)(n_iseg | n_mseg << 16),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(xch + 2 * q + 1, (uint64_t)tag << 32 | (uint32_t)n_long, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid < q) {
+    uint64_t a, b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t polls = 0;; ++polls) {
+      a = __hip_atomic_load(xch + 2 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      b = __hip_atomic_load(xch + 2 * tid + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag) break;
+      __builtin_amdgcn_s_sleep(1);
+      if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
+        atomicOr(err, 16);
+        a = b = 0;
+        break;
+      }
+    }
+    s_prev[tid][0] = (int)(a & 0xFFFF);
+    s_prev[tid][1] = (int)((a >> 16) & 0xFFFF);
+    s_prev[tid][2] = (int)(b & 0xFFFFFFFF);
+  }
+  __syncthreads();  // s_ioff, s_refs, s_prev
+  if (tid < 3) {
+    int acc = 0;
+    for (int m = 0; m < q; ++m) acc += s_prev[m][tid];
+    s_base[tid] = acc;
+  }
+  __syncthreads();
+  const int ibase = s_base[0], mbase = s_base[1], lbase = s_base[2];
+  // item records of the K2-served segments, and the long ones' copies (k_build_batches's)
+  {
+    int s = iseg0, ms = mbase + mseg0, lpre = lbase + field(cpre, 2);
+#pragma unroll
+    for (int k = 0; k < E2; ++k) {
+      const int r = tid * E2 + k;
+      if (!((hm >> k) & 1)) continue;
+      if ((sm >> k) & 1) {
+        ++s;
+        continue;
+      }
+      const int end = s_ioff[s + 1];
+      const int len = end - r;
+      const int lng = ((lm >> k) & 1) && lpre < kMaxLongItems;
+      int pk[kInlineRefs / 2];
+#pragma unroll
+      for (int m = 0; m < kInlineRefs / 2; ++m) {
+        const int a = s_refs[min(r + 2 * m, total - 1)], b = s_refs[min(r + 2 * m + 1, total - 1)];
+        pk[m] = (2 * m < len ? a : 0) | ((2 * m + 1 < len ? b : 0) << 16);
+      }
+      store_rec(v.irec + (int64_t)ms * kRec, (int)ok_[k], (rbase + r) | (len << 15) | (lng << 30),
+                pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
+      if (lng)
+        store_rec(v.lrec + (int64_t)lpre * kRec, (int)ok_[k], rbase + r, rbase + end, ibase + s, 0, 0,
+                  0, 1);
+      lpre += (lm >> k) & 1;
+      ++s;
+      ++ms;
+    }
+  }
+  if (q == kItemParts - 1 && tid == 0) {
+    v.meta[2] = mbase + n_mseg;
+    v.meta[3] = min(lbase + n_long, kMaxLongItems);
+  }
+  };
+  if (n_mine <= T * 4)
+    part(std::integral_constant<int, 4>{});
+  else
+    part(std::integral_constant<int, 8>{});
+}
+
 #ifdef BPRMF_BUILD_STAMPS
 extern "C" int bprmf_debug_build_stamps(uint64_t* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), sizeof(uint64_t) * 32) == hipSuccess ? 0 : -3;
@@ -585,6 +992,16 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   k_build_batches<IPT_, BUCKET_, W1_><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(               \
       a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,  \
       slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci)
+  // one rank, triplets already in memory: the split builder (1 + kItemParts workgroups per batch;
+  // BPRMF_SPLIT_ITEMS=0 keeps the one-workgroup build, A/B)
+  const char* spe = getenv("BPRMF_SPLIT_ITEMS");
+  if (w1 && ru && B >= 16 && B <= kBuildThreads * 4 && !radix && !(spe && spe[0] == '0')) {
+    static uint32_t tag = 0;  // the launch's tag on the parts' exchanged counts (never 0)
+    if (++tag == 0) ++tag;
+    k_build_split<<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
+        n_slots, B, ru, ri, rj, u_rows, i_rows, ub, ib, tpb, k1_items, bb, err, ci, tag);
+    return hipGetLastError();
+  }
   if (B <= kBuildThreads * 4 && !radix) {
     if (w1) BPRMF_BUILD(4, true, true);
     else BPRMF_BUILD(4, true, false);

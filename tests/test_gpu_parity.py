@@ -262,8 +262,8 @@ def test_batch_builders_agree_bitwise(rl, golden, monkeypatch, B):
     pos, U, I = _ml100k_pos(golden)
     outs = []
     for env in ({}, {"BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_BUILD": "0"},
-                {"BPRMF_SPLIT_BUILD": "1", "BPRMF_RADIX_BUILD": "1"}):
-        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_BUILD"):
+                {"BPRMF_SPLIT_BUILD": "1", "BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_ITEMS": "0"}):
+        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_BUILD", "BPRMF_SPLIT_ITEMS"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -292,20 +292,57 @@ def test_replay_bucket_builder_empty_slots_and_duplicates(rl, monkeypatch):
     i[:B] = 7
     j[B:B + 50] = i[B:B + 50]
     outs = []
-    for radix in (False, True):
-        monkeypatch.delenv("BPRMF_RADIX_BUILD", raising=False)
-        if radix:
-            monkeypatch.setenv("BPRMF_RADIX_BUILD", "1")
+    for env in ({}, {"BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_ITEMS": "0"}):
+        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_ITEMS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         m = _model(rl, U, I, d, B, lr=0.05, wd=0.01)
         m.set_weights(P0, Q0)
         m.train_triplets(u, i, j)
         outs.append(m.get_weights())
-    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    for P, Q in outs[1:]:
+        assert np.array_equal(outs[0][0], P) and np.array_equal(outs[0][1], Q)
     P, Q = P0.copy(), Q0.copy()
     for s in range(0, n, B):
         O.bpr_step_dense(P, Q, u[s:s + B], i[s:s + B], j[s:s + B], 0.05, 0.01)
     np.testing.assert_allclose(outs[0][0], P, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(outs[0][1], Q, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("skew", ["one_part", "hot_and_empty"])
+def test_split_builder_skewed_parts(rl, monkeypatch, skew):
+    """The split builder's item parts cut the item id space in four equal ranges.  Every
+    reference in one range (the part falls back to 8 sorted references per thread: more than 4T
+    of them), or hot items in one range and empty ranges: the split build equals the one-workgroup
+    build bitwise, and both equal the dense oracle."""
+    g = np.random.default_rng(21)
+    U, I, d, B = 2000, 1000, 32, 4096
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    n = 3 * B + 123
+    u = g.integers(0, U, n)
+    if skew == "one_part":  # item ids < 1024 -> 10 bits, parts of 256 ids: all in part 1
+        i, j = g.integers(256, 512, n), g.integers(256, 512, n)
+    else:  # a few hot items in part 0, parts 2 and 3 empty
+        i = np.where(g.random(n) < 0.5, g.integers(0, 4, n), g.integers(0, 512, n))
+        j = g.integers(0, 512, n)
+    outs = []
+    for env in ({}, {"BPRMF_SPLIT_ITEMS": "0"}):
+        monkeypatch.delenv("BPRMF_SPLIT_ITEMS", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = _model(rl, U, I, d, B, lr=0.05, wd=0.01)
+        m.set_weights(P0, Q0)
+        st = m.train_triplets(u, i, j)
+        outs.append((m.get_weights(), st["loss"]))
+    assert np.array_equal(outs[0][0][0], outs[1][0][0]) and np.array_equal(outs[0][0][1], outs[1][0][1])
+    assert outs[0][1] == outs[1][1]
+    P, Q = P0.copy(), Q0.copy()
+    for s in range(0, n, B):
+        O.bpr_step_dense(P, Q, u[s:s + B], i[s:s + B], j[s:s + B], 0.05, 0.01)
+    np.testing.assert_allclose(outs[0][0][0], P, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(outs[0][0][1], Q, rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("d,B", [(32, 4096), (128, 1000), (384, 256), (8, 64)])

@@ -567,8 +567,15 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_batches(
 // the launch's tag) and waits for parts 0 .. q-1's before it writes records.  The batch buffer
 // comes out identical to k_build_batches's, bit for bit (refs, records, trec, meta).
 // ================================================================================================
-constexpr int kItemParts = 4;
-constexpr int kItemPartBits = 2;  // log2(kItemParts)
+#ifndef BPRMF_ITEM_PARTS
+#define BPRMF_ITEM_PARTS 8
+#endif
+constexpr int kItemParts = BPRMF_ITEM_PARTS;  // 2, 4 or 8 (8: 20-step calls 11.42-11.51 us/step, 4: 11.62-11.66, 2: 11.80-11.92) (-DBPRMF_ITEM_PARTS: A/B builds)
+constexpr int kItemPartBits = kItemParts == 8 ? 3 : kItemParts == 4 ? 2 : 1;
+static_assert(kItemParts == 1 << kItemPartBits, "item parts: a power of two <= 8");
+// sorted references per thread while a part holds at most that many per thread (a part averages
+// 2B / kItemParts of the batch's references), else 8
+constexpr int kPartE2 = kItemParts >= 8 ? 2 : kItemParts == 4 ? 4 : 8;
 
 // bucket_sort over the VALID elements (key != kNone) of a blocked E-per-thread input whose keys lie
 // in [lo, lo + 2^bits): the same order (stable by key, ties by input position), but absent
@@ -812,7 +819,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
 
   // ---- item part q: references whose item lies in [lo, lo + 2^rb) ----
   const int q = role - 1;
-  const int rb = max(item_bits - kItemPartBits, 0);
+  const int rb = max(item_bits - kItemPartBits, 0);  // parts of 2^rb item ids
   const uint32_t lo = (uint32_t)q << rb;
   __syncthreads();  // s_i/s_j in sorted order; s_key free
   uint32_t ik[IPT2];
@@ -831,8 +838,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   int cpre0 = 0, ctot0 = 0;  // (refs before << 16 | refs here), each <= 2B <= 8192
   Scan().exclusive_scan(below << 16 | mine, cpre0, 0, ctot0, sscan, rocprim::plus<int>());
   const int rbase = ctot0 >> 16, n_mine = ctot0 & 0xFFFF;
-  // the sorted references come out E2 per thread: 4 (half the single-workgroup builder's 8) while
-  // the part holds at most 4T of the batch's 2B references (a part averages B / 2), else 8
+  // the sorted references come out E2 per thread: kPartE2 while the part holds at most that many
+  // per thread, else 8 (the single-workgroup builder's)
   auto part = [&](auto e2) {
   constexpr int E2 = decltype(e2)::value;
   uint32_t ok_[E2], ov[E2];
@@ -950,8 +957,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     v.meta[3] = min(lbase + n_long, kMaxLongItems);
   }
   };
-  if (n_mine <= T * 4)
-    part(std::integral_constant<int, 4>{});
+  if (n_mine <= T * kPartE2)
+    part(std::integral_constant<int, kPartE2>{});
   else
     part(std::integral_constant<int, 8>{});
 }

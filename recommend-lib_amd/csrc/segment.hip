@@ -674,6 +674,21 @@ static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
   return reinterpret_cast<uint64_t*>(v.ukey);
 }
 
+// diagnostic build only (-DBPRMF_BUILD_STAMPS): batch 0's user workgroup stamps g_build_stamps[0..4],
+// its first item part [8..15], its last item part [16..23] (absolute s_memrealtime)
+#ifdef BPRMF_BUILD_STAMPS
+#define SPSTAMP(k)                                                                           \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x <= kItemParts && (blockIdx.x == 0 || blockIdx.x == 1 || \
+                                                         blockIdx.x == kItemParts))          \
+      g_build_stamps[(blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 8 : 16) + (k)] =               \
+          __builtin_amdgcn_s_memrealtime();                                                  \
+  } while (0)
+#else
+#define SPSTAMP(k) \
+  do {             \
+  } while (0)
+#endif
 __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     int64_t n_slots, int B, const int32_t* __restrict__ ru, const int32_t* __restrict__ ri,
     const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int user_bits, int item_bits,
@@ -715,6 +730,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     }
     if (ci.loss && tid < ci.nloss) ci.loss[tid] = 0.0;
   }
+  SPSTAMP(0);
 
   // 1. the batch's triplets in slot order, keyed by user row (as k_build_batches)
   uint32_t key[IPT], val[IPT];
@@ -736,8 +752,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       }
     }
   }
+  SPSTAMP(1);
   const int nvalid = bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
                                          [](int q) { return (uint32_t)q; });
+  SPSTAMP(2);
   // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
   int32_t my_i[IPT], my_j[IPT];
 #pragma unroll
@@ -797,6 +815,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       }
     }
     int mpre = 0, n_multi = 0;
+    SPSTAMP(3);
     __syncthreads();  // sscan reuse
     Scan().exclusive_scan(nmulti, mpre, 0, n_multi, sscan, rocprim::plus<int>());
 #pragma unroll
@@ -814,6 +833,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       v.meta[1] = n_useg;
       v.meta[4] = n_multi;
     }
+    SPSTAMP(4);
     return;
   }
 
@@ -838,6 +858,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   int cpre0 = 0, ctot0 = 0;  // (refs before << 16 | refs here), each <= 2B <= 8192
   Scan().exclusive_scan(below << 16 | mine, cpre0, 0, ctot0, sscan, rocprim::plus<int>());
   const int rbase = ctot0 >> 16, n_mine = ctot0 & 0xFFFF;
+  SPSTAMP(3);
   // the sorted references come out E2 per thread: kPartE2 while the part holds at most that many
   // per thread, else 8 (the single-workgroup builder's)
   auto part = [&](auto e2) {
@@ -848,6 +869,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       ik, lo, rb, bs,
       [&](int r) { return (uint32_t)(r < nv ? s_i[r] : s_j[r - nv]); },
       [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, ok_, ov);
+  SPSTAMP(4);
 #pragma unroll
   for (int k = 0; k < E2; ++k) s_key[tid * E2 + k] = ok_[k];
   __syncthreads();
@@ -888,6 +910,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       if ((hm >> k) & 1) s_ioff[s++] = tid * E2 + k;
   }
   if (tid == 0) s_ioff[n_iseg] = total;
+  SPSTAMP(5);
   // publish this part's counts, then collect the parts before (the first q threads, one each)
   uint64_t* xch = xch_of(v);
   if (tid == 0) {
@@ -922,6 +945,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   }
   __syncthreads();
   const int ibase = s_base[0], mbase = s_base[1], lbase = s_base[2];
+  SPSTAMP(6);
   // item records of the K2-served segments, and the long ones' copies (k_build_batches's)
   {
     int s = iseg0, ms = mbase + mseg0, lpre = lbase + field(cpre, 2);
@@ -956,6 +980,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     v.meta[2] = mbase + n_mseg;
     v.meta[3] = min(lbase + n_long, kMaxLongItems);
   }
+  SPSTAMP(7);
   };
   if (n_mine <= T * kPartE2)
     part(std::integral_constant<int, kPartE2>{});

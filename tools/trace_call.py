@@ -8,7 +8,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-starts = [k for k, r in enumerate(rows) if "k_build_batches" in r["Kernel_Name"]]
+starts = [k for k, r in enumerate(rows) if "k_build_batches" in r["Kernel_Name"] or "k_build_split" in r["Kernel_Name"]]
 first = starts[-1]
 if first > 0 and "k_sample" in rows[first - 1]["Kernel_Name"]:
     first -= 1

@@ -23,7 +23,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "build":
 
 os.environ["BPRMF_DIAG_LIB"] = LIB
 # the step kernels never run on a diagnostic build's batches (some are wrong on purpose)
-os.environ["BPRMF_DIAG_BUILD_ONLY"] = "1"
+if "--split" not in sys.argv:
+    os.environ["BPRMF_DIAG_BUILD_ONLY"] = "1"
 import ctypes  # noqa: E402
 
 import numpy as np  # noqa: E402
@@ -34,6 +35,23 @@ L = rl._lib.load()
 L.bprmf_debug_build_stamps.argtypes = [ctypes.c_void_p]
 pos = syn.make_positives(138493, 26744, 10_000_000, 20261015)
 res = {}
+if "--split" in sys.argv:  # the split builder (k_build_split): user workgroup, first / last item part
+    m = rl.BPRMF(138493, 26744, 128, batch_size=4096, seed=1, device=0)
+    m.set_train(pos)
+    rows = []
+    for rep in range(8):
+        m.train_steps(0, 20 * rep, 20)
+        st = np.zeros(32, np.uint64)
+        assert L.bprmf_debug_build_stamps(st.ctypes.data) == 0
+        rows.append((st.astype(np.int64) - int(st[0])) * 0.01)  # us from the user workgroup's start
+    med = np.median(np.array(rows[2:]), axis=0)
+    names_u = ["start", "loads", "user sort", "segments", "end"]
+    names_i = ["start", "loads", "user sort", "ref keys", "sparse sort", "heads/refs", "exchange", "end"]
+    res["user workgroup (us from its start)"] = {n: round(float(med[k]), 2) for k, n in enumerate(names_u)}
+    res["first item part"] = {n: round(float(med[8 + k]), 2) for k, n in enumerate(names_i)}
+    res["last item part"] = {n: round(float(med[16 + k]), 2) for k, n in enumerate(names_i)}
+    print(json.dumps(res, indent=1))
+    sys.exit(0)
 for radix in ("0",) if "--quick" in sys.argv else ("0", "1"):
     for split in ("1",) if "--quick" in sys.argv else ("1", "0"):
         os.environ["BPRMF_SPLIT_BUILD"] = split

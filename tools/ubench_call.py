@@ -56,7 +56,15 @@ if os.environ.get("UB_SPIN"):  # busy the GPU for ~UB_SPIN ms of unrelated work 
         x = x @ x
         x = x / x.norm()
         torch.cuda.synchronize()
+if os.environ.get("UB_GC") == "0":  # no Python garbage collection inside the timed calls
+    import gc
+    gc.collect()
+    gc.disable()
 for c in range(N):
+    if os.environ.get("UB_SPINCPU"):  # busy the host core for UB_SPINCPU ms before the call
+        t1 = time.perf_counter()
+        while time.perf_counter() - t1 < float(os.environ["UB_SPINCPU"]) * 1e-3:
+            pass
     e, s = divmod(first, n_steps)
     if s + K > n_steps:
         e, s = e + 1, 0

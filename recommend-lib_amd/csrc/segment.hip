@@ -667,11 +667,14 @@ static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E
   return total;
 }
 
-// The parts' counts for the batch, in 64-bit words {tag, payload} (one store each, write-through):
-// xch[2q] = tag << 32 | n_iseg | n_mseg << 16, xch[2q + 1] = tag << 32 | n_long.  The area is the
-// batch's ukey range (sharded mode only; 8-byte aligned).
+// The parts' counts for the batch, in 64-bit words {tag, payload} (one store each, write-through),
+// kXchWords per part: [0] tag << 32 | n_iseg | n_mseg << 16, [1] tag << 32 | n_long, and sharded
+// [2 + o / 2] tag << 32 | cnt[o] | cnt[o + 1] << 16 with cnt[o] = the part's segments of owners
+// below o.  The area is the batch's ioff range from its second int (8-byte aligned, 2B ints; the
+// bucket builds never store ioff), so B >= kItemParts * kXchWords.
+constexpr int kXchWords = 2 + kMaxWorld / 2;
 static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
-  return reinterpret_cast<uint64_t*>(v.ukey);
+  return reinterpret_cast<uint64_t*>(v.ioff + 1);
 }
 
 // diagnostic build only (-DBPRMF_BUILD_STAMPS): batch 0's user workgroup stamps g_build_stamps[0..4],
@@ -689,10 +692,16 @@ static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
   do {             \
   } while (0)
 #endif
+// SL (the sharded runner's batches): users are global ids (local row u / world), items are keyed
+// owner-major ((item % world) * iloc + item / world) and written as SLOTS: the segment index (slot
+// stride 0) or owner * slot_stride + index within the owner's range; ukey and own as
+// k_build_batches writes them.  !SL: one rank, item rows.
+template <bool SL>
 __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     int64_t n_slots, int B, const int32_t* __restrict__ ru, const int32_t* __restrict__ ri,
-    const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int user_bits, int item_bits,
-    int tpb, int k1_items, BatchBuf bb, int32_t* __restrict__ err, CursorInit ci, uint32_t tag) {
+    const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int world_in, int64_t iloc,
+    int slot_stride, int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb,
+    int32_t* __restrict__ err, CursorInit ci, uint32_t tag) {
   constexpr int T = kBuildThreads;
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
@@ -706,7 +715,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   __shared__ int32_t s_j[T * IPT];
   __shared__ int32_t s_ninv;
   __shared__ int s_base[3];  // item parts: segments, K2 records, long records of the parts before
-  __shared__ int s_prev[kItemParts][3];
+  __shared__ int s_prev[kItemParts][3 + kMaxWorld];
+  __shared__ int s_lopre[kMaxWorld];      // SL: this part's first segment of each owner (local)
+  __shared__ int s_opre[kMaxWorld + 1];   // SL: the batch's first segment of each owner (global)
+  const int world = SL ? world_in : 1;
   uint32_t* s_key = reinterpret_cast<uint32_t*>(s_sort);
   uint32_t* s_u = reinterpret_cast<uint32_t*>(s_sort) + 2 * T * IPT;
   int32_t* s_refs = reinterpret_cast<int32_t*>(s_sort) + T * IPT2;
@@ -723,6 +735,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   const int64_t b0 = batch * (int64_t)B;
   const int nb = (int)max<int64_t>(0, min<int64_t>(B, n_slots - b0));
   const BatchView v = bb.view(batch);
+  if (tid < kMaxWorld) s_lopre[tid] = -1;
   if (batch == 0 && role == 0 && ci.cursor) {  // set_cursor's work (kernels.hip k_set_cursor)
     if (tid == 0) {
       ci.cursor[0] = ci.t;
@@ -732,7 +745,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   }
   SPSTAMP(0);
 
-  // 1. the batch's triplets in slot order, keyed by user row (as k_build_batches)
+  // 1. the batch's triplets in slot order, keyed by (local) user row (as k_build_batches)
   uint32_t key[IPT], val[IPT];
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
@@ -740,7 +753,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     key[k] = kNone;
     val[k] = (uint32_t)p;
     if (p < nb && ru[b0 + p] >= 0) {  // u < 0: an empty slot
-      const int32_t u = ru[b0 + p], i = ri[b0 + p], j = rj[b0 + p];
+      const int32_t u = SL ? ru[b0 + p] / world : ru[b0 + p], i = ri[b0 + p], j = rj[b0 + p];
       if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
           (uint64_t)j < (uint64_t)i_rows) {
         key[k] = (uint32_t)u;
@@ -837,10 +850,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     return;
   }
 
-  // ---- item part q: references whose item lies in [lo, lo + 2^rb) ----
+  // ---- item part q: references whose item key lies in [lo, lo + 2^rb) ----
   const int q = role - 1;
-  const int rb = max(item_bits - kItemPartBits, 0);  // parts of 2^rb item ids
+  const int rb = max(item_bits - kItemPartBits, 0);  // parts of 2^rb keys
   const uint32_t lo = (uint32_t)q << rb;
+  auto key_of_item = [&](uint32_t item) -> uint32_t {
+    return SL ? (item % (uint32_t)world) * (uint32_t)iloc + item / (uint32_t)world : item;
+  };
   __syncthreads();  // s_i/s_j in sorted order; s_key free
   uint32_t ik[IPT2];
   int below = 0, mine = 0;  // references of this thread in the parts before / in this part
@@ -849,9 +865,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     const int r = tid * IPT2 + k;
     ik[k] = kNone;
     if (r < 2 * nvalid) {
-      const uint32_t item = (uint32_t)(r < nvalid ? s_i[r] : s_j[r - nvalid]);
-      if (item >= lo && ((item - lo) >> rb) == 0) ik[k] = item;
-      below += item < lo;
+      const uint32_t kk = key_of_item((uint32_t)(r < nvalid ? s_i[r] : s_j[r - nvalid]));
+      if (kk >= lo && ((kk - lo) >> rb) == 0) ik[k] = kk;
+      below += kk < lo;
       mine += ik[k] != kNone;
     }
   }
@@ -867,7 +883,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   const int nv = nvalid;
   const int total = bucket_sort_sparse<T, IPT2, E2>(
       ik, lo, rb, bs,
-      [&](int r) { return (uint32_t)(r < nv ? s_i[r] : s_j[r - nv]); },
+      [&](int r) { return key_of_item((uint32_t)(r < nv ? s_i[r] : s_j[r - nv])); },
       [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, ok_, ov);
   SPSTAMP(4);
 #pragma unroll
@@ -882,7 +898,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     const int r = tid * E2 + k;  // local position
     if (ok_[k] == kNone) continue;
     const bool h = (k ? ok_[k - 1] : iprev) != ok_[k];
-    const bool so = k1_items && h && (k + 1 < E2 ? ok_[k + 1] : inext) != ok_[k];
+    const bool so = !SL && k1_items && h && (k + 1 < E2 ? ok_[k + 1] : inext) != ok_[k];
     const bool lg = h && !so && r + kLongSeg < T * E2 && s_key[r + kLongSeg] == ok_[k];
     hm |= (uint32_t)h << k;
     sm |= (uint32_t)so << k;
@@ -892,9 +908,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     nlong += lg;
     v.refs[rbase + r] = (int32_t)ov[k];
     s_refs[r] = (int32_t)ov[k];
-    // the triplet's item word: row | first reference of its item | only reference
-    const int32_t word = (int32_t)ok_[k] | (h ? (int32_t)0x80000000 : 0) | (so ? 0x40000000 : 0);
-    v.trec[4LL * (ov[k] >> 1) + (ov[k] & 1)] = word;
+    if (!SL) {  // the triplet's item word: row | first reference of its item | only reference
+      const int32_t word = (int32_t)ok_[k] | (h ? (int32_t)0x80000000 : 0) | (so ? 0x40000000 : 0);
+      v.trec[4LL * (ov[k] >> 1) + (ov[k] & 1)] = word;
+    }
   }
   uint64_t cpre = 0, ctot = 0;
   ScanL().exclusive_scan((uint64_t)iheads | (uint64_t)mheads << 16 | (uint64_t)nlong << 32, cpre, 0ull,
@@ -906,52 +923,109 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   {
     int s = iseg0;
 #pragma unroll
-    for (int k = 0; k < E2; ++k)
-      if ((hm >> k) & 1) s_ioff[s++] = tid * E2 + k;
+    for (int k = 0; k < E2; ++k) {
+      if (!((hm >> k) & 1)) continue;
+      if (SL) {  // an owner's first segment of this part: its head follows another owner's key
+        const uint32_t o = ok_[k] / (uint32_t)iloc;
+        const uint32_t pk = k ? ok_[k - 1] : iprev;
+        if (pk == kNone || pk / (uint32_t)iloc != o) s_lopre[o] = s;
+      }
+      s_ioff[s++] = tid * E2 + k;
+    }
   }
   if (tid == 0) s_ioff[n_iseg] = total;
+  __syncthreads();  // s_ioff, s_refs, s_lopre
   SPSTAMP(5);
   // publish this part's counts, then collect the parts before (the first q threads, one each)
-  uint64_t* xch = xch_of(v);
+  uint64_t* xch = xch_of(v) + (int64_t)kXchWords * q;
   if (tid == 0) {
-    __hip_atomic_store(xch + 2 * q, (uint64_t)tag << 32 | (uint32_t)(n_iseg | n_mseg << 16),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(xch + 2 * q + 1, (uint64_t)tag << 32 | (uint32_t)n_long, __ATOMIC_RELAXED,
+    const uint64_t tg = (uint64_t)tag << 32;
+    __hip_atomic_store(xch, tg | (uint32_t)(n_iseg | n_mseg << 16), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(xch + 1, tg | (uint32_t)n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SL) {  // owners without segments here start where the next owner does
+      int next = n_iseg;
+      for (int o = world - 1; o >= 0; --o) {
+        if (s_lopre[o] < 0) s_lopre[o] = next;
+        next = s_lopre[o];
+      }
+      for (int o = 0; o < world; o += 2) {
+        const uint32_t c = (uint32_t)s_lopre[o] | (o + 1 < world ? (uint32_t)s_lopre[o + 1] << 16 : 0u);
+        __hip_atomic_store(xch + 2 + o / 2, tg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
+  const int nw = SL ? 2 + (world + 1) / 2 : 2;  // words per part
   if (tid < q) {
-    uint64_t a, b;
+    const uint64_t* px = xch_of(v) + (int64_t)kXchWords * tid;
+    uint64_t w[kXchWords];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t polls = 0;; ++polls) {
-      a = __hip_atomic_load(xch + 2 * tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      b = __hip_atomic_load(xch + 2 * tid + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag) break;
+      bool all = true;
+#pragma unroll
+      for (int m = 0; m < kXchWords; ++m) {  // registers only (fixed indices)
+        w[m] = m < nw ? __hip_atomic_load(px + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        all &= m >= nw || (uint32_t)(w[m] >> 32) == tag;
+      }
+      if (all) break;
       __builtin_amdgcn_s_sleep(1);
       if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
         atomicOr(err, 16);
-        a = b = 0;
+#pragma unroll
+        for (int m = 0; m < kXchWords; ++m) w[m] = 0;
         break;
       }
     }
-    s_prev[tid][0] = (int)(a & 0xFFFF);
-    s_prev[tid][1] = (int)((a >> 16) & 0xFFFF);
-    s_prev[tid][2] = (int)(b & 0xFFFFFFFF);
+    s_prev[tid][0] = (int)(w[0] & 0xFFFF);
+    s_prev[tid][1] = (int)((w[0] >> 16) & 0xFFFF);
+    s_prev[tid][2] = (int)(w[1] & 0xFFFFFFFF);
+    if (SL) {
+#pragma unroll
+      for (int m = 2; m < kXchWords; ++m) {  // owners 2(m-2) and 2(m-2)+1 (past world: unused)
+        s_prev[tid][3 + 2 * (m - 2)] = (int)(w[m] & 0xFFFF);
+        s_prev[tid][4 + 2 * (m - 2)] = (int)((w[m] >> 16) & 0xFFFF);
+      }
+    }
   }
-  __syncthreads();  // s_ioff, s_refs, s_prev
+  __syncthreads();  // s_prev
   if (tid < 3) {
     int acc = 0;
     for (int m = 0; m < q; ++m) acc += s_prev[m][tid];
     s_base[tid] = acc;
   }
+  if (SL && tid < world) {  // the batch's segments of owners below tid: the parts before + this one
+    int acc = s_lopre[tid];
+    for (int m = 0; m < q; ++m) acc += s_prev[m][3 + tid];
+    s_opre[tid] = acc;
+  }
   __syncthreads();
   const int ibase = s_base[0], mbase = s_base[1], lbase = s_base[2];
+  if (SL && tid == 0) s_opre[world] = ibase + n_iseg;  // (the last part: the batch's segment count)
+  __syncthreads();
   SPSTAMP(6);
-  // item records of the K2-served segments, and the long ones' copies (k_build_batches's)
+  // slot of the batch's item segment sg (k_build_batches's slot_of)
+  auto slot_of = [&](int sg) -> int {
+    if (!SL || !slot_stride) return sg;
+    int lo_o = 0, hi_o = world - 1;  // largest owner o with s_opre[o] <= sg
+    while (lo_o < hi_o) {
+      const int mid = (lo_o + hi_o + 1) >> 1;
+      if (s_opre[mid] <= sg) lo_o = mid; else hi_o = mid - 1;
+    }
+    return lo_o * slot_stride + (sg - s_opre[lo_o]);
+  };
+  // item records of the K2-served segments, and the long ones' copies (k_build_batches's); SL:
+  // the distinct items' local rows and every reference's triplet word (slot | first reference)
   {
     int s = iseg0, ms = mbase + mseg0, lpre = lbase + field(cpre, 2);
+    int sr = iseg0 - 1;  // segment of this thread's first reference if it is not a head
 #pragma unroll
     for (int k = 0; k < E2; ++k) {
       const int r = tid * E2 + k;
+      if (SL && ok_[k] != kNone) {
+        const bool h = (hm >> k) & 1;
+        if (h) ++sr;
+        v.trec[4LL * (ov[k] >> 1) + (ov[k] & 1)] = slot_of(ibase + sr) | (h ? (int32_t)0x80000000 : 0);
+      }
       if (!((hm >> k) & 1)) continue;
       if ((sm >> k) & 1) {
         ++s;
@@ -966,19 +1040,24 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
         const int a = s_refs[min(r + 2 * m, total - 1)], b = s_refs[min(r + 2 * m + 1, total - 1)];
         pk[m] = (2 * m < len ? a : 0) | ((2 * m + 1 < len ? b : 0) << 16);
       }
-      store_rec(v.irec + (int64_t)ms * kRec, (int)ok_[k], (rbase + r) | (len << 15) | (lng << 30),
-                pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
+      const int sg = ibase + s;
+      if (SL) v.ukey[sg] = (int32_t)(ok_[k] % (uint32_t)iloc);
+      store_rec(v.irec + (int64_t)ms * kRec, SL ? slot_of(sg) : (int)ok_[k],
+                (rbase + r) | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
       if (lng)
-        store_rec(v.lrec + (int64_t)lpre * kRec, (int)ok_[k], rbase + r, rbase + end, ibase + s, 0, 0,
-                  0, 1);
+        store_rec(v.lrec + (int64_t)lpre * kRec, (int)ok_[k], rbase + r, rbase + end, slot_of(sg), 0,
+                  0, 0, 1);
       lpre += (lm >> k) & 1;
       ++s;
       ++ms;
     }
   }
-  if (q == kItemParts - 1 && tid == 0) {
-    v.meta[2] = mbase + n_mseg;
-    v.meta[3] = min(lbase + n_long, kMaxLongItems);
+  if (q == kItemParts - 1) {
+    if (tid == 0) {
+      v.meta[2] = mbase + n_mseg;
+      v.meta[3] = min(lbase + n_long, kMaxLongItems);
+    }
+    if (SL && tid < world) v.own[tid] = s_opre[tid + 1] - s_opre[tid];
   }
   SPSTAMP(7);
   };
@@ -1024,14 +1103,20 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   k_build_batches<IPT_, BUCKET_, W1_><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(               \
       a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,  \
       slots ? slot_stride : 0, ub, ib, tpb, k1_items, bb, err, ci)
-  // one rank, triplets already in memory: the split builder (1 + kItemParts workgroups per batch;
-  // BPRMF_SPLIT_ITEMS=0 keeps the one-workgroup build, A/B)
+  // triplets already in memory: the split builder (1 + kItemParts workgroups per batch; one rank,
+  // or the sharded runner's slots; BPRMF_SPLIT_ITEMS=0 keeps the one-workgroup build, A/B)
   const char* spe = getenv("BPRMF_SPLIT_ITEMS");
-  if (w1 && ru && B >= 16 && B <= kBuildThreads * 4 && !radix && !(spe && spe[0] == '0')) {
+  if ((w1 || slots) && ru && B >= kItemParts * kXchWords && B <= kBuildThreads * 4 && !radix &&
+      !(spe && spe[0] == '0')) {
     static uint32_t tag = 0;  // the launch's tag on the parts' exchanged counts (never 0)
     if (++tag == 0) ++tag;
-    k_build_split<<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
-        n_slots, B, ru, ri, rj, u_rows, i_rows, ub, ib, tpb, k1_items, bb, err, ci, tag);
+    if (w1)
+      k_build_split<false><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
+          n_slots, B, ru, ri, rj, u_rows, i_rows, 1, iloc, 0, ub, ib, tpb, k1_items, bb, err, ci, tag);
+    else
+      k_build_split<true><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
+          n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slot_stride, ub, ib, tpb, 0, bb, err,
+          ci, tag);
     return hipGetLastError();
   }
   if (B <= kBuildThreads * 4 && !radix) {

@@ -230,6 +230,37 @@ def test_runner_sampler_matches_python_orchestration_and_is_reproducible(rl, gol
             np.testing.assert_allclose(x, z, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_runner_split_builder_equals_one_workgroup_build(rl, golden, monkeypatch, world):
+    """The runner's batches (owner-major item slots, padded per owner) from the split builder (one
+    user and eight item-part workgroups per batch) and from the one-workgroup builder give the
+    same training bit for bit, sampled chunks of both lengths included."""
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    Uu, Ii = int(f["U"]), int(f["I"])
+    B, seed, d = 1024, 9, 32
+    sh = rl.sharded
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("BPRMF_SPLIT_ITEMS", env)
+
+        def runner(comm, r, key):
+            m = sh.ShardedBPRMF(Uu, Ii, d, batch_size=B, seed=seed, device=0, comm=comm)
+            S = m.set_train(pos)
+            m.attach_runner("loopback", key=key)
+            m.train_steps(0, 0, S)
+            st = m.train_steps(1, 2, 7)
+            return m.get_weights(), st["loss"]
+
+        key = 3000 + 10 * world + int(env)
+        outs.append(_runner_threads(rl, world, key, lambda c, r: runner(c, r, key)))
+    for r in range(world):
+        (Pa, Qa), la = outs[0][r]
+        (Pb, Qb), lb = outs[1][r]
+        assert np.array_equal(Pa, Pb) and np.array_equal(Qa, Qb)
+        assert la == lb
+
+
 def test_runner_rccl_transport_one_rank(rl):
     """The RCCL transport (library-owned communicator, unique id broadcast by the process group)
     at world 1, graph-captured or eager, with or without RCCL carrying the self blocks, gives the

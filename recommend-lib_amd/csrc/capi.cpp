@@ -562,6 +562,10 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
     out->exec = nullptr;
     return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
   }
+  // the executable graph's device-side setup now (set_train) rather than inside its first replay
+  // (BPRMF_GRAPH_UPLOAD=0: lazily, A/B)
+  const char* up = getenv("BPRMF_GRAPH_UPLOAD");
+  if (!(up && up[0] == '0')) HIPCHK(hipGraphUpload(out->exec, h->stream));
   return 0;
 }
 

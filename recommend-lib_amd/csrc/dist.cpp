@@ -413,6 +413,7 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   if (int r = tr->alloc_shared(h, X_MAX, sizeof(int32_t) * 2 * W, &p)) return r;
   d->vals = static_cast<int32_t*>(p);
   if (int r = dalloc(&d->d_cap, 1)) return r;
+  HIPCHK(hipMemsetAsync(d->d_cap, 0, sizeof(int32_t), h->stream));  // the split builder's max starts at 0
   if (int r = dalloc(&d->ids_send, ids)) return r;
   if (int r = dalloc(&d->rows_send, rows)) return r;
   if (int r = dalloc(&d->grads_send, rows)) return r;
@@ -609,6 +610,7 @@ static int launch_dist_graph(bprmf_handle* h, int64_t n, int cap, const int32_t*
       ge->exec = nullptr;
       return fail(BPRMF_E_HIP, "sharded step graph instantiate: %s", hipGetErrorString(e));
     }
+    HIPCHK(hipGraphUpload(ge->exec, h->stream));  // its device-side setup before its first replay
   }
   HIPCHK(hipGraphLaunch(ge->exec, h->stream));
   return 0;
@@ -626,7 +628,22 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   const BatchBuf bb{h->d_batch, B};
   const int par = (int)(d->chunks & 1);
   const int32_t seq = (int32_t)(d->chunks + 1);
-  HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, loss_zero_slots(h)));
+  // the cursor, the call's loss slots and the chunk's capacity max: the builder's first workgroup
+  // and its item parts (one launch fewer each), or their own launches (every per-wave loss slot to
+  // zero; the one-workgroup build)
+  CursorInit ci;
+  ci.cursor = h->d_tbase;
+  ci.t = h->t;
+  ci.loss = h->d_loss;
+  ci.nloss = loss_zero_slots(h);
+  ci.own_max = d->d_cap;  // zero: the previous chunk's pair_out (or the allocation) cleared it
+  if (ci.nloss > kSegLossSlots) {
+    HIPCHK(set_cursor(h->d_tbase, h->t, 0, h->stream, h->d_loss, ci.nloss));
+    ci.cursor = nullptr;
+    ci.loss = nullptr;
+    ci.nloss = 0;
+  }
+  bool own_max_done = false;
   int64_t first_slot = 0, n_slots = n * B;
   if (!ru) {
     int64_t N;
@@ -643,20 +660,22 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
                     tu + 2 * h->trip_cap, h->d_err, h->stream));
       HIPCHK(build_batches(sampler_args(h), epoch, 0, n_slots, B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true, d->S, n, bb,
-                           h->d_err, h->stream, k1_triplets_per_block(h->geom)));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci, &own_max_done));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
-                           h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom)));
+                           h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream,
+                           k1_triplets_per_block(h->geom), ci, &own_max_done));
     }
   }
   // exchange capacity of the chunk: the largest request count of any (rank, step, owner)
-  HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
+  if (!own_max_done) HIPCHK(dist_own_max(bb, n, W, d->d_cap, h->stream));
   if (int r = d->tr->max_i32(h, d->d_cap, d->vals + par * W, seq)) return r;
   // cap and the error word back in one wait: a tiny kernel writes them and then a sequence
   // number into the mapped status block, and the host spins on that number
   volatile int32_t* hv = reinterpret_cast<volatile int32_t*>(h->h_status + 8);
   const uint64_t cseq = ++h->status_seq;
-  HIPCHK(pair_out(d->d_cap, h->d_err, h->h_status_dev + 8, h->h_status_dev + kSeqCapOff, cseq, h->stream));
+  HIPCHK(pair_out(d->d_cap, h->d_err, h->h_status_dev + 8, h->h_status_dev + kSeqCapOff, cseq, h->stream,
+                  d->d_cap));
   if (int r = wait_mapped_seq(h, kSeqCapOff, cseq)) return r;
   int32_t cap = hv[0];
   if (hv[1]) {

@@ -144,9 +144,10 @@ hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, doub
 hipError_t status_out(const void* d_status, void* h_status_dev, int words, hipStream_t s,
                       void* seq_dev = nullptr, uint64_t seq = 0);
 hipError_t advance_cursor(int32_t* cursor, int32_t n, hipStream_t s);
-// a[0] and b[0] into mapped host memory dst[0..1], then seq into seq_dev (mapped)
+// a[0] and b[0] into mapped host memory dst[0..1], then seq into seq_dev (mapped); zero != null:
+// then *zero = 0 (the sharded runner's capacity word, ready for the next chunk's builder)
 hipError_t pair_out(const int32_t* a, const int32_t* b, void* dst_dev, void* seq_dev, uint64_t seq,
-                    hipStream_t s);
+                    hipStream_t s, int32_t* zero = nullptr);
 hipError_t init_normal(const Geom& g, float* W, int64_t rows, float std, uint32_t k0, uint32_t k1,
                        uint32_t table_tag, int world, int rank, hipStream_t s);
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* ou,
@@ -168,12 +169,15 @@ struct CursorInit {
   int32_t t = 0, k = 0;
   double* loss = nullptr;
   int nloss = 0;
+  // sharded runner: the split builder raises *own_max (zero before the launch) to the chunk's
+  // largest per-owner segment count (dist_own_max's result), and says so in *own_max_done
+  int32_t* own_max = nullptr;
 };
 hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slot, int64_t n_slots,
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
-                         const CursorInit& ci = CursorInit{});
+                         const CursorInit& ci = CursorInit{}, bool* own_max_done = nullptr);
 // triplets per K1 workgroup for a geometry (the builder marks user segments that lie in one)
 int k1_triplets_per_block(const Geom& g);
 // Per-step buffers of the step kernels.  pstride != 0 (single GPU): contrib / ugrad / xloss hold

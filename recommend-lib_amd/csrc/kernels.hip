@@ -388,10 +388,11 @@ hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, doub
 }
 
 // two int32 device words (a[0], b[0]) into mapped host memory dst[0..1], then seq (as k_status_out)
-__global__ void k_pair_out(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int32_t* dst,
-                           uint64_t* seq_dst, uint64_t seq) {
+__global__ void k_pair_out(const int32_t* a, const int32_t* __restrict__ b, int32_t* dst,
+                           uint64_t* seq_dst, uint64_t seq, int32_t* zero) {
   if (threadIdx.x == 0) {
     __hip_atomic_store(dst, *a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (zero) *zero = 0;
     __hip_atomic_store(dst + 1, *b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(seq_dst, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -399,8 +400,9 @@ __global__ void k_pair_out(const int32_t* __restrict__ a, const int32_t* __restr
 }
 
 hipError_t pair_out(const int32_t* a, const int32_t* b, void* dst_dev, void* seq_dev, uint64_t seq,
-                    hipStream_t s) {
-  k_pair_out<<<1, 64, 0, s>>>(a, b, static_cast<int32_t*>(dst_dev), static_cast<uint64_t*>(seq_dev), seq);
+                    hipStream_t s, int32_t* zero) {
+  k_pair_out<<<1, 64, 0, s>>>(a, b, static_cast<int32_t*>(dst_dev), static_cast<uint64_t*>(seq_dev), seq,
+                              zero);
   return hipGetLastError();
 }
 

@@ -1058,6 +1058,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       v.meta[3] = min(lbase + n_long, kMaxLongItems);
     }
     if (SL && tid < world) v.own[tid] = s_opre[tid + 1] - s_opre[tid];
+    if (SL && ci.own_max && tid == 0) {  // dist_own_max's work, batch by batch
+      int m = 0;
+      for (int o = 0; o < world; ++o) m = max(m, s_opre[o + 1] - s_opre[o]);
+      atomicMax(ci.own_max, m);
+    }
   }
   SPSTAMP(7);
   };
@@ -1083,7 +1088,8 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
-                         const CursorInit& ci) {
+                         const CursorInit& ci, bool* own_max_done) {
+  if (own_max_done) *own_max_done = false;
   if (n_batches <= 0) return hipSuccess;
   if (ci.cursor && ci.loss && ci.nloss > kBuildThreads) return hipErrorInvalidValue;
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
@@ -1117,6 +1123,7 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
       k_build_split<true><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
           n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slot_stride, ub, ib, tpb, 0, bb, err,
           ci, tag);
+    if (own_max_done) *own_max_done = !w1 && ci.own_max;
     return hipGetLastError();
   }
   if (B <= kBuildThreads * 4 && !radix) {

@@ -17,9 +17,13 @@ for r in 1 2 3; do
 done
 timeout -k 10 240 python bench.py --no-cpu-baseline > "$out/bench.log" 2>&1 || { tail -5 "$out/bench.log"; exit 1; }
 grep '^{' "$out/bench.log" > "$out/bench.json"
+timeout -k 10 240 python bench.py --steps 20 --warmup 5 --semantics hogwild --no-cpu-baseline > "$out/bench20_hog.log" 2>&1 || { tail -5 "$out/bench20_hog.log"; exit 1; }
+grep '^{' "$out/bench20_hog.log" > "$out/bench20_hog.json"
+timeout -k 10 240 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline > "$out/bench20_sh.log" 2>&1 || { tail -5 "$out/bench20_sh.log"; exit 1; }
+grep '^{' "$out/bench20_sh.log" > "$out/bench20_sh.json"
 python3 - "$out" <<'PY'
 import json, sys
-for f in ("bench20.jsonl", "bench.json"):
+for f in ("bench20.jsonl", "bench.json", "bench20_hog.json", "bench20_sh.json"):
     for line in open(sys.argv[1] + "/" + f):
         d = json.loads(line)
         print(f, d["value"], d["ms_per_step"], d["roofline"]["avg_us_per_step"], d["roofline"]["frac"])

@@ -15,6 +15,7 @@
 
 #include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/block/block_scan.hpp>
+#include <atomic>
 #include <type_traits>
 
 #include "device_common.h"
@@ -1114,8 +1115,11 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   const char* spe = getenv("BPRMF_SPLIT_ITEMS");
   if ((w1 || slots) && ru && B >= kItemParts * kXchWords && B <= kBuildThreads * 4 && !radix &&
       !(spe && spe[0] == '0')) {
-    static uint32_t tag = 0;  // the launch's tag on the parts' exchanged counts (never 0)
-    if (++tag == 0) ++tag;
+    // the launch's tag on the parts' exchanged counts: a fresh value per launch (one counter for
+    // every handle and thread; a batch's words from an earlier launch carry an older tag), never 0
+    static std::atomic<uint32_t> next_tag{0};
+    uint32_t tag = ++next_tag;
+    if (tag == 0) tag = ++next_tag;
     if (w1)
       k_build_split<false><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
           n_slots, B, ru, ri, rj, u_rows, i_rows, 1, iloc, 0, ub, ib, tpb, k1_items, bb, err, ci, tag);

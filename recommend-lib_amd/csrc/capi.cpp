@@ -701,12 +701,11 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
       if (int r = ensure_trip(h, n)) return r;
       int32_t* tu = h->d_trip;
       trace_mark();
-      HIPCHK(sample(sampler_args(h), epoch, first_slot, n, tu, tu + h->trip_cap,
-                    tu + 2 * h->trip_cap, h->d_err, h->stream));
-      trace_mark();
-      HIPCHK(build_batches(sampler_args(h), epoch, 0, n, (int)B, tu, tu + h->trip_cap,
+      // the grid-wide sampler's triplets staged in d_trip: sampled inside the split builder's
+      // launch, or by k_sample before the build
+      HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, 1, false, 0, nb, bb,
-                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci, nullptr, true));
       trace_mark();
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n, (int)B, ru, ri, rj, h->U,

@@ -118,6 +118,37 @@ static __device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restric
   return k + lo;
 }
 
+// One slot of the device sampler (BPRData.ng_sample + the shuffled DataLoader,
+// util/data_loader.py:680-690, BPRMFRecommender.py:141): slot -> triplet q = perm(slot) ->
+// positive q / num_ng -> (global user u, item i) and the negative j, uniform over u's
+// non-positives.  false: u holds every item (j = -1).  k_sample and the split builder's in-launch
+// sampling both call this, so their triplets are the same bits.
+static __device__ __forceinline__ bool sample_slot(const SamplerArgs& a, uint32_t epoch, uint64_t slot,
+                                                   int32_t& u, int32_t& i, int32_t& j) {
+  const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
+#if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 2)  // diagnostic: no shuffle (timing only)
+  const uint64_t q = slot;
+#else
+  const uint64_t q = permute(slot, N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
+#endif
+  const int64_t p = div_small(q, (uint32_t)a.num_ng);
+  u = a.pos_u[p];
+  i = a.pos_i[p];
+  const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
+  const int64_t ul = u / a.world;
+  const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
+  const int64_t free_items = a.item_num - deg;
+  j = -1;
+  if (free_items <= 0) return false;
+  const uint32_t k = bounded_from(d0, q, epoch, (uint32_t)free_items, a.k0, a.k1);
+#if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 1)  // diagnostic: no search (timing only)
+  j = (int32_t)k;
+#else
+  j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
+#endif
+  return true;
+}
+
 // (1 - lr*wd)^k in double by squaring (deterministic IEEE order), rounded once to fp32.
 // (1 - lr*wd)^k for a row whose last k steps were pure weight decay.  log2a = log2(1 - lr*wd) is
 // formed in double on the host; k*log2a in double, one v_exp_f32 (relative error ~1e-7, far below

@@ -656,11 +656,10 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     if (!ru && n_slots > 0 && split_build(n)) {  // short chunk: grid-wide sampler first
       if (int r = ensure_trip(h, n_slots)) return r;
       int32_t* tu = h->d_trip;
-      HIPCHK(sample(sampler_args(h), epoch, first_slot, n_slots, tu, tu + h->trip_cap,
-                    tu + 2 * h->trip_cap, h->d_err, h->stream));
-      HIPCHK(build_batches(sampler_args(h), epoch, 0, n_slots, B, tu, tu + h->trip_cap,
+      HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, tu, tu + h->trip_cap,
                            tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true, d->S, n, bb,
-                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci, &own_max_done));
+                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci, &own_max_done,
+                           true));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
                            h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream,

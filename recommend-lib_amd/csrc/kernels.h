@@ -177,7 +177,11 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
-                         const CursorInit& ci = CursorInit{}, bool* own_max_done = nullptr);
+                         const CursorInit& ci = CursorInit{}, bool* own_max_done = nullptr,
+                         bool sample_first = false);
+// (sample_first: ru/ri/rj are staging arrays [n_slots] the call fills with the device sampler's
+// triplets of slots first_slot.. of `epoch` before building from them: inside the split builder's
+// launch where it applies, else by a k_sample launch)
 // triplets per K1 workgroup for a geometry (the builder marks user segments that lie in one)
 int k1_triplets_per_block(const Geom& g);
 // Per-step buffers of the step kernels.  pstride != 0 (single GPU): contrib / ugrad / xloss hold

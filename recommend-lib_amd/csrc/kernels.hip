@@ -29,32 +29,10 @@ __global__ __launch_bounds__(kBlock) void k_sample(SamplerArgs a, uint32_t epoch
                                                    int32_t* __restrict__ oi,
                                                    int32_t* __restrict__ oj,
                                                    int32_t* __restrict__ err) {
-  const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count;
        s += (int64_t)gridDim.x * blockDim.x) {
-#if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 2)  // diagnostic: no shuffle (timing only)
-    const uint64_t q = (uint64_t)(first + s);
-#else
-    const uint64_t q = permute((uint64_t)(first + s), N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
-#endif
-    const int64_t p = div_small(q, (uint32_t)a.num_ng);
-    const int32_t u = a.pos_u[p];
-    const int32_t i = a.pos_i[p];
-    const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
-    const int64_t ul = u / a.world;
-    const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
-    const int64_t free_items = a.item_num - deg;
-    int32_t j = -1;
-    if (free_items > 0) {
-      const uint32_t k = bounded_from(d0, q, epoch, (uint32_t)free_items, a.k0, a.k1);
-#if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 1)  // diagnostic: no search (timing only)
-      j = (int32_t)k;
-#else
-      j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
-#endif
-    } else {
-      atomicOr(err, 2);
-    }
+    int32_t u, i, j;
+    if (!sample_slot(a, epoch, (uint64_t)(first + s), u, i, j)) atomicOr(err, 2);
     ou[s] = u;
     oi[s] = i;
     oj[s] = j;

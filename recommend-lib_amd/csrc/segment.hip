@@ -697,12 +697,18 @@ static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
 // owner-major ((item % world) * iloc + item / world) and written as SLOTS: the segment index (slot
 // stride 0) or owner * slot_stride + index within the owner's range; ukey and own as
 // k_build_batches writes them.  !SL: one rank, item rows.
-template <bool SL>
+// SMP: the launch samples the batches itself (no k_sample launch before it): each of a batch's
+// 1 + kItemParts workgroups draws its share of the batch's slots (sample_slot, the same bits as
+// k_sample) into the staging arrays ru/ri/rj (write-through), marks the batch's sampling board
+// (after the parts' exchange words in the same area) and waits for the others' marks; the loads
+// below then read the staged triplets past the L2 (sc1).
+template <bool SL, bool SMP>
 __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     int64_t n_slots, int B, const int32_t* __restrict__ ru, const int32_t* __restrict__ ri,
     const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int world_in, int64_t iloc,
     int slot_stride, int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb,
-    int32_t* __restrict__ err, CursorInit ci, uint32_t tag) {
+    int32_t* __restrict__ err, CursorInit ci, uint32_t tag, SamplerArgs sa, uint32_t epoch,
+    int64_t first_slot) {
   constexpr int T = kBuildThreads;
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
@@ -745,6 +751,38 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     if (ci.loss && tid < ci.nloss) ci.loss[tid] = 0.0;
   }
   SPSTAMP(0);
+  if constexpr (SMP) {  // 0. this workgroup's share of the batch's slots, then everyone's
+    const int share = (B + kItemParts) / (kItemParts + 1);
+    const int s0 = role * share, s1 = min(nb, s0 + share);
+    for (int p = s0 + tid; p < s1; p += T) {
+      int32_t u, i, j;
+      if (!sample_slot(sa, epoch, (uint64_t)(first_slot + b0 + p), u, i, j)) atomicOr(err, 2);
+      __hip_atomic_store(const_cast<int32_t*>(ru) + b0 + p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(const_cast<int32_t*>(ri) + b0 + p, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(const_cast<int32_t*>(rj) + b0 + p, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are acknowledged
+    __syncthreads();                                    // ... and every wave's
+    uint64_t* board = xch_of(v) + (int64_t)kItemParts * kXchWords;
+    if (tid == 0) __hip_atomic_store(board + role, (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid <= kItemParts && tid != role) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t polls = 0;; ++polls) {
+        if ((uint32_t)__hip_atomic_load(board + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) break;
+        __builtin_amdgcn_s_sleep(1);
+        if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
+          atomicOr(err, 16);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // a staged word of the batch: written in this launch by other CUs (SMP: read past the L2)
+  auto staged = [](const int32_t* p) -> int32_t {
+    if constexpr (SMP) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+  };
 
   // 1. the batch's triplets in slot order, keyed by (local) user row (as k_build_batches)
   uint32_t key[IPT], val[IPT];
@@ -753,8 +791,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     const int p = tid * IPT + k;
     key[k] = kNone;
     val[k] = (uint32_t)p;
-    if (p < nb && ru[b0 + p] >= 0) {  // u < 0: an empty slot
-      const int32_t u = SL ? ru[b0 + p] / world : ru[b0 + p], i = ri[b0 + p], j = rj[b0 + p];
+    const int32_t ug = p < nb ? staged(ru + b0 + p) : -1;
+    if (ug >= 0) {  // u < 0: an empty slot
+      const int32_t u = SL ? ug / world : ug, i = staged(ri + b0 + p), j = staged(rj + b0 + p);
       if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
           (uint64_t)j < (uint64_t)i_rows) {
         key[k] = (uint32_t)u;
@@ -1089,9 +1128,10 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
                          int B, const int32_t* ru, const int32_t* ri, const int32_t* rj,
                          int64_t u_rows, int64_t i_rows, int world, bool slots, int slot_stride,
                          int64_t n_batches, BatchBuf bb, int32_t* err, hipStream_t s, int tpb,
-                         const CursorInit& ci, bool* own_max_done) {
+                         const CursorInit& ci, bool* own_max_done, bool sample_first) {
   if (own_max_done) *own_max_done = false;
   if (n_batches <= 0) return hipSuccess;
+  if (sample_first && (!ru || !ri || !rj)) return hipErrorInvalidValue;
   if (ci.cursor && ci.loss && ci.nloss > kBuildThreads) return hipErrorInvalidValue;
   if (B <= 0 || B > kMaxSegBatch || world <= 0 || world > kMaxWorld) return hipErrorInvalidValue;
   const int64_t iloc = (i_rows + world - 1) / world;
@@ -1113,23 +1153,38 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // triplets already in memory: the split builder (1 + kItemParts workgroups per batch; one rank,
   // or the sharded runner's slots; BPRMF_SPLIT_ITEMS=0 keeps the one-workgroup build, A/B)
   const char* spe = getenv("BPRMF_SPLIT_ITEMS");
-  if ((w1 || slots) && ru && B >= kItemParts * kXchWords && B <= kBuildThreads * 4 && !radix &&
-      !(spe && spe[0] == '0')) {
+  const bool split = (w1 || slots) && ru && B >= kItemParts * kXchWords + kItemParts + 1 &&
+                     B <= kBuildThreads * 4 && !radix && !(spe && spe[0] == '0');
+  // sample_first: ru/ri/rj are staging arrays for slots first_slot .. first_slot + n_slots; the
+  // split builder samples them itself (BPRMF_SPLIT_SAMPLE=0: k_sample first, A/B), any other
+  // build after a k_sample launch
+  const char* sse = getenv("BPRMF_SPLIT_SAMPLE");
+  const bool smp = sample_first && split && !(sse && sse[0] == '0');
+  if (sample_first && !smp) {
+    const hipError_t e = sample(a, epoch, first_slot, n_slots, const_cast<int32_t*>(ru),
+                                const_cast<int32_t*>(ri), const_cast<int32_t*>(rj), err, s);
+    if (e != hipSuccess) return e;
+  }
+  if (split) {
     // the launch's tag on the parts' exchanged counts: a fresh value per launch (one counter for
     // every handle and thread; a batch's words from an earlier launch carry an older tag), never 0
     static std::atomic<uint32_t> next_tag{0};
     uint32_t tag = ++next_tag;
     if (tag == 0) tag = ++next_tag;
-    if (w1)
-      k_build_split<false><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
-          n_slots, B, ru, ri, rj, u_rows, i_rows, 1, iloc, 0, ub, ib, tpb, k1_items, bb, err, ci, tag);
-    else
-      k_build_split<true><<<(unsigned)(n_batches * (kItemParts + 1)), kBuildThreads, 0, s>>>(
-          n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slot_stride, ub, ib, tpb, 0, bb, err,
-          ci, tag);
+    const unsigned grid = (unsigned)(n_batches * (kItemParts + 1));
+#define BPRMF_SPLIT(SL_, SMP_, W_, STRIDE_, K1_)                                                 \
+  k_build_split<SL_, SMP_><<<grid, kBuildThreads, 0, s>>>(                                       \
+      n_slots, B, ru, ri, rj, u_rows, i_rows, W_, iloc, STRIDE_, ub, ib, tpb, K1_, bb, err, ci, tag, \
+      a, epoch, first_slot)
+    if (w1 && smp) BPRMF_SPLIT(false, true, 1, 0, k1_items);
+    else if (w1) BPRMF_SPLIT(false, false, 1, 0, k1_items);
+    else if (smp) BPRMF_SPLIT(true, true, world, slot_stride, 0);
+    else BPRMF_SPLIT(true, false, world, slot_stride, 0);
+#undef BPRMF_SPLIT
     if (own_max_done) *own_max_done = !w1 && ci.own_max;
     return hipGetLastError();
   }
+  if (sample_first) first_slot = 0;  // the builds below replay the staged triplets
   if (B <= kBuildThreads * 4 && !radix) {
     if (w1) BPRMF_BUILD(4, true, true);
     else BPRMF_BUILD(4, true, false);

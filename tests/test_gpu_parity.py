@@ -256,14 +256,17 @@ def test_device_sampled_training_equals_replay_of_oracle_triplets(rl, golden):
 
 @pytest.mark.parametrize("B", [4096, 1000, 96])
 def test_batch_builders_agree_bitwise(rl, golden, monkeypatch, B):
-    """The bucket-sort batch builder (B <= 4096), the rocPRIM radix builder, and the grid-wide
-    sampler ahead of the builder vs the sampler inside it all give the same batches, so training
-    is bitwise identical (partial last batches included: the ml-100k epoch is not a multiple of B)."""
+    """The bucket-sort batch builder (B <= 4096), the rocPRIM radix builder, the split builder
+    (sampling inside its own launch, or after a k_sample launch), and the grid-wide sampler ahead
+    of the builder vs the sampler inside the one-workgroup builder all give the same batches, so
+    training is bitwise identical (partial last batches included: the ml-100k epoch is not a
+    multiple of B)."""
     pos, U, I = _ml100k_pos(golden)
     outs = []
     for env in ({}, {"BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_BUILD": "0"},
-                {"BPRMF_SPLIT_BUILD": "1", "BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_ITEMS": "0"}):
-        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_BUILD", "BPRMF_SPLIT_ITEMS"):
+                {"BPRMF_SPLIT_BUILD": "1", "BPRMF_RADIX_BUILD": "1"}, {"BPRMF_SPLIT_ITEMS": "0"},
+                {"BPRMF_SPLIT_SAMPLE": "0"}):
+        for k in ("BPRMF_RADIX_BUILD", "BPRMF_SPLIT_BUILD", "BPRMF_SPLIT_ITEMS", "BPRMF_SPLIT_SAMPLE"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

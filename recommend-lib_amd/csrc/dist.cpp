@@ -50,6 +50,10 @@ struct Xchg {  // one all-to-all of per-peer blocks
 
 struct Transport {
   virtual ~Transport() = default;
+  // another rank's kernels run on this rank's GPU (one-GPU rehearsals, in-process shards): no
+  // launch may wait on workgroups of its own grid that come after it (the split builder's
+  // in-launch sampling board does), since a peer's spinning workgroups can hold the CUs they need
+  virtual bool shares_device() const { return false; }
   virtual int exchange(bprmf_handle* h, const Xchg& x) = 0;
   // in-place max over ranks of one device int32; vals: [world] scratch peers may write into
   virtual int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) {
@@ -137,6 +141,7 @@ struct IpcTransport final : Transport {
   int32_t* board(int b) const { return boards + (size_t)b * kBoardMax; }
   bool opened = false;
   bool shared_device = false;  // some peer runs on this rank's GPU (rehearsals on one device)
+  bool shares_device() const override { return shared_device; }
   // owner workgroups per launch: they spin on the peers' gradient flags before applying, so with
   // ranks sharing one GPU a full grid of them could hold every CU a peer needs to produce those
   // gradients (measured: 2 ranks, ~1,500 owner workgroups, timed out); one rank per GPU: no cap
@@ -287,6 +292,7 @@ static std::mutex g_loops_m;
 static std::map<int64_t, LoopGroup*> g_loops;
 
 struct LoopTransport final : Transport {
+  bool shares_device() const override { return true; }  // in-process shards on one GPU
   int64_t key = 0;
   LoopGroup* g = nullptr;
   ~LoopTransport() override {
@@ -656,10 +662,15 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     if (!ru && n_slots > 0 && split_build(n)) {  // short chunk: grid-wide sampler first
       if (int r = ensure_trip(h, n_slots)) return r;
       int32_t* tu = h->d_trip;
-      HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, tu, tu + h->trip_cap,
-                           tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true, d->S, n, bb,
-                           h->d_err, h->stream, k1_triplets_per_block(h->geom), ci, &own_max_done,
-                           true));
+      // sampled inside the split builder's launch on one rank per GPU, else by k_sample first
+      const bool in_launch = !d->tr->shares_device();
+      if (!in_launch)
+        HIPCHK(sample(sampler_args(h), epoch, first_slot, n_slots, tu, tu + h->trip_cap,
+                      tu + 2 * h->trip_cap, h->d_err, h->stream));
+      HIPCHK(build_batches(sampler_args(h), epoch, in_launch ? first_slot : 0, n_slots, B, tu,
+                           tu + h->trip_cap, tu + 2 * h->trip_cap, h->U, h->cfg.item_num, W, true,
+                           d->S, n, bb, h->d_err, h->stream, k1_triplets_per_block(h->geom), ci,
+                           &own_max_done, in_launch));
     } else {
       HIPCHK(build_batches(sampler_args(h), epoch, first_slot, n_slots, B, ru, ri, rj, h->U,
                            h->cfg.item_num, W, true, d->S, n, bb, h->d_err, h->stream,

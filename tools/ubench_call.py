@@ -47,7 +47,7 @@ if os.environ.get("UB_WARM_SPLIT"):  # the same W warm-up steps as two calls
     m.train_steps(0, W // 2, W - W // 2)
 else:
     m.train_steps(0, 0, W)
-first, walls, inner = W, [], []
+first, walls, inner, calls = W, [], [], []
 if os.environ.get("UB_SPIN"):  # busy the GPU for ~UB_SPIN ms of unrelated work before the first call
     x = torch.randn(2048, 2048, device="cuda")
     torch.cuda.synchronize()
@@ -71,8 +71,10 @@ for c in range(N):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st = m.train_steps(e, s, K)
+    t1 = time.perf_counter()
     torch.cuda.synchronize()
     walls.append(time.perf_counter() - t0)
+    calls.append(t1 - t0)
     inner.append(st["seconds"])
     first = e * n_steps + s + K
 w = np.array(walls[5:]) * 1e6 / K
@@ -81,6 +83,8 @@ first_calls = [round(x * 1e6 / K, 2) for x in walls[:6]]
 first_inner = [round(x * 1e6 / K, 2) for x in inner[:6]]
 print(json.dumps({"steps_per_call": K, "calls": len(w), "first_calls_us_per_step": first_calls,
                   "first_calls_library_us_per_step": first_inner,
+                  "first_calls_python_call_us": [round(x * 1e6, 1) for x in calls[:6]],
+                  "first_calls_wall_us": [round(x * 1e6, 1) for x in walls[:6]],
                   "us_per_step_median": round(float(np.median(w)), 3),
                   "us_per_step_min": round(float(w.min()), 3),
                   "library_us_per_step_median": round(float(np.median(i)), 3)}))

@@ -15,6 +15,8 @@
 // Reference semantics: the same SGD step as BPRMFRecommender.py:172-176 on the union batch.
 #include <algorithm>
 
+#include <stdlib.h>
+
 #include "device_common.h"
 #include "dist_body.h"
 
@@ -72,9 +74,14 @@ static __device__ __forceinline__ int find_row(const int32_t* __restrict__ list,
 // request it then (the leader serves those positions from the row it just wrote); gfree[k][p][idx]
 // = 1 when position (p, idx) of step k holds a row that step k-1 did not apply (k = 0: every row),
 // gathered on its own.
-__global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
-                             int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
-                             int32_t* __restrict__ gfree) {
+// One lane per (position, peer q): a group of G = next_pow2(world) lanes per position does its W
+// searches side by side (three binary searches a lane: step k-1, k and k+1 of peer q's list, one
+// dependent chain each) instead of one thread walking ~3W searches in sequence; the group's "any
+// peer" answers (the row was applied last step; a lower peer requests it too) are ballots.
+// (BPRMF_PLAN_LANES=0, A/B: the one-thread-per-position form, every peer's searches in sequence)
+__global__ void k_owner_plan_seq(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
+                                 int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
+                                 int32_t* __restrict__ gfree) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= n * world * (int64_t)cap) return;
   const int idx = (int)(x % cap);
@@ -106,6 +113,53 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
     rec[q] = pos < 0 ? -1 : q * cap + pos;
     if (k + 1 < n) dep[q] = find_row(ids_recv + ((int64_t)q * n + k + 1) * cap, cap, (uint32_t)row);
   }
+}
+
+__global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
+                             int gshift, int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
+                             int32_t* __restrict__ gfree) {
+  const int G = 1 << gshift;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t x = t >> gshift;
+  const int q = (int)(t & (G - 1));
+  const bool live = x < n * world * (int64_t)cap;  // the same for every lane of a group
+  int idx = 0, p = 0;
+  int64_t k = 0;
+  int32_t row = -1;
+  if (live) {
+    idx = (int)(x % cap);
+    p = (int)((x / cap) % world);
+    k = x / ((int64_t)cap * world);
+    row = ids_recv[((int64_t)p * n + k) * cap + idx];
+  }
+  const bool qv = live && q < world && row >= 0;
+  const bool prev = qv && k > 0 && find_row(ids_recv + ((int64_t)q * n + k - 1) * cap, cap, (uint32_t)row) >= 0;
+  const int cur = !qv ? -1 : q == p ? idx : find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row);
+  const int nxt = qv && k + 1 < n ? find_row(ids_recv + ((int64_t)q * n + k + 1) * cap, cap, (uint32_t)row) : -1;
+  // every lane of the wave takes part in the ballots (groups never straddle a wave: G <= 16)
+  const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+  const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << gbase;
+  const uint64_t any_prev = __ballot(prev) & gmask;
+  const uint64_t any_lower = __ballot(qv && q < p && cur >= 0) & gmask;
+  if (!live || q >= world) return;
+  int32_t* rec = aplan + x * world;
+  int32_t* dep = gdep + x * world;
+  if (row < 0) {
+    dep[q] = -1;
+    if (q == 0) {
+      rec[0] = -2;
+      gfree[x] = 0;
+    }
+    return;
+  }
+  if (q == 0) gfree[x] = any_prev ? 0 : 1;
+  if (any_lower) {  // a lower peer leads this row
+    dep[q] = -1;
+    if (q == 0) rec[0] = -2;
+    return;
+  }
+  rec[q] = cur < 0 ? -1 : q * cap + cur;
+  dep[q] = nxt;
 }
 
 template <int G4, int S>
@@ -351,8 +405,16 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
                            int32_t* gdep, int32_t* gfree, hipStream_t s) {
   if (n <= 0 || cap <= 0) return hipSuccess;
-  k_owner_plan<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap, aplan,
-                                                                      gdep, gfree);
+  const char* pl = getenv("BPRMF_PLAN_LANES");
+  if (pl && pl[0] == '0') {
+    k_owner_plan_seq<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap,
+                                                                          aplan, gdep, gfree);
+    return hipGetLastError();
+  }
+  int gshift = 0;
+  while ((1 << gshift) < world) ++gshift;  // world <= kMaxWorld = 16
+  k_owner_plan<<<blocks_for((n * world * (int64_t)cap) << gshift), kBlock, 0, s>>>(
+      ids_recv, n, world, cap, gshift, aplan, gdep, gfree);
   return hipGetLastError();
 }
 

@@ -693,6 +693,23 @@ static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
   do {             \
   } while (0)
 #endif
+// x / d for 32-bit unsigned x by a multiply-high and a shift (round-up method: l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1, q = (umulhi(m, x) + x) >> l, exact for every 32-bit x); the
+// sharded builder divides every reference by the world size and every head by the owner's row
+// count, runtime values a plain `/` turns into a ~40-instruction sequence
+struct FastDiv {
+  uint32_t d = 1, m = 1, l = 0;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t dd) : d(dd) {
+    while ((1ull << l) < dd) ++l;
+    m = (uint32_t)(((1ull << 32) * ((1ull << l) - dd)) / dd + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t x) const {
+    return (uint32_t)(((uint64_t)__umulhi(m, x) + x) >> l);
+  }
+  __device__ __forceinline__ uint32_t mod(uint32_t x) const { return x - div(x) * d; }
+};
+
 // SL (the sharded runner's batches): users are global ids (local row u / world), items are keyed
 // owner-major ((item % world) * iloc + item / world) and written as SLOTS: the segment index (slot
 // stride 0) or owner * slot_stride + index within the owner's range; ukey and own as
@@ -708,7 +725,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int world_in, int64_t iloc,
     int slot_stride, int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb,
     int32_t* __restrict__ err, CursorInit ci, uint32_t tag, SamplerArgs sa, uint32_t epoch,
-    int64_t first_slot) {
+    int64_t first_slot, FastDiv wdiv, FastDiv ldiv) {
   constexpr int T = kBuildThreads;
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
@@ -793,7 +810,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     val[k] = (uint32_t)p;
     const int32_t ug = p < nb ? staged(ru + b0 + p) : -1;
     if (ug >= 0) {  // u < 0: an empty slot
-      const int32_t u = SL ? ug / world : ug, i = staged(ri + b0 + p), j = staged(rj + b0 + p);
+      const int32_t u = SL ? (int32_t)wdiv.div((uint32_t)ug) : ug, i = staged(ri + b0 + p),
+                    j = staged(rj + b0 + p);
       if ((uint64_t)u < (uint64_t)u_rows && (uint64_t)i < (uint64_t)i_rows &&
           (uint64_t)j < (uint64_t)i_rows) {
         key[k] = (uint32_t)u;
@@ -895,7 +913,12 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   const int rb = max(item_bits - kItemPartBits, 0);  // parts of 2^rb keys
   const uint32_t lo = (uint32_t)q << rb;
   auto key_of_item = [&](uint32_t item) -> uint32_t {
-    return SL ? (item % (uint32_t)world) * (uint32_t)iloc + item / (uint32_t)world : item;
+    if constexpr (SL) {
+      const uint32_t qw = wdiv.div(item);
+      return (item - qw * (uint32_t)world) * (uint32_t)iloc + qw;
+    } else {
+      return item;
+    }
   };
   __syncthreads();  // s_i/s_j in sorted order; s_key free
   uint32_t ik[IPT2];
@@ -966,9 +989,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     for (int k = 0; k < E2; ++k) {
       if (!((hm >> k) & 1)) continue;
       if (SL) {  // an owner's first segment of this part: its head follows another owner's key
-        const uint32_t o = ok_[k] / (uint32_t)iloc;
+        const uint32_t o = ldiv.div(ok_[k]);
         const uint32_t pk = k ? ok_[k - 1] : iprev;
-        if (pk == kNone || pk / (uint32_t)iloc != o) s_lopre[o] = s;
+        if (pk == kNone || ldiv.div(pk) != o) s_lopre[o] = s;
       }
       s_ioff[s++] = tid * E2 + k;
     }
@@ -1081,7 +1104,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
         pk[m] = (2 * m < len ? a : 0) | ((2 * m + 1 < len ? b : 0) << 16);
       }
       const int sg = ibase + s;
-      if (SL) v.ukey[sg] = (int32_t)(ok_[k] % (uint32_t)iloc);
+      if (SL) v.ukey[sg] = (int32_t)ldiv.mod(ok_[k]);
       store_rec(v.irec + (int64_t)ms * kRec, SL ? slot_of(sg) : (int)ok_[k],
                 (rbase + r) | (len << 15) | (lng << 30), pk[0], pk[1], pk[2], pk[3], pk[4], pk[5]);
       if (lng)
@@ -1175,7 +1198,7 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
 #define BPRMF_SPLIT(SL_, SMP_, W_, STRIDE_, K1_)                                                 \
   k_build_split<SL_, SMP_><<<grid, kBuildThreads, 0, s>>>(                                       \
       n_slots, B, ru, ri, rj, u_rows, i_rows, W_, iloc, STRIDE_, ub, ib, tpb, K1_, bb, err, ci, tag, \
-      a, epoch, first_slot)
+      a, epoch, first_slot, FastDiv((uint32_t)W_), FastDiv((uint32_t)iloc))
     if (w1 && smp) BPRMF_SPLIT(false, true, 1, 0, k1_items);
     else if (w1) BPRMF_SPLIT(false, false, 1, 0, k1_items);
     else if (smp) BPRMF_SPLIT(true, true, world, slot_stride, 0);

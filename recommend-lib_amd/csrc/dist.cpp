@@ -437,7 +437,7 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   DistState* d = h->dist;
   const int64_t W = h->cfg.world;
-  const int64_t ap = n * W * std::max(cap, 1) * (2 * W + 1);
+  const int64_t ap = n * W * std::max(cap, 1) * (3 * W + 1);  // rec, gdep, gfree, pflag
   if (ap <= d->aplan_n[par]) return 0;
   if (d->aplan[par]) HIPCHK(hipFree(d->aplan[par]));
   d->aplan[par] = nullptr;
@@ -713,7 +713,8 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     d->tr->self_exchange = se;
     if (r) return r;
     HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, aplan + n * W * (int64_t)cap * W,
-                           aplan + 2 * n * W * (int64_t)cap * W, h->stream));
+                           aplan + 2 * n * W * (int64_t)cap * W, h->stream,
+                           aplan + 2 * n * W * (int64_t)cap * W + n * W * (int64_t)cap));
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));

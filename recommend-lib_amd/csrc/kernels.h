@@ -278,8 +278,9 @@ hipError_t max_vals(const int32_t* vals, int world, int32_t* out, hipStream_t s)
 hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s);
 hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
                          hipStream_t s);
+// pflag: [n][W][cap][W] scratch of the list-pair form (null: the one-kernel forms)
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           int32_t* gdep, int32_t* gfree, hipStream_t s);
+                           int32_t* gdep, int32_t* gfree, hipStream_t s, int32_t* pflag = nullptr);
 // ---- the fused sharded step over the IPC transport (step.hip; two launches per step) ----
 // K2 whose per-slot gradients go straight to the owners: slot s of owner p = s / S lands at
 // dst[p] + (s % S) * ld; once every workgroup's stores are acknowledged the launch's last

@@ -207,7 +207,9 @@ def main():
         return el
 
     run(0, a.warmup)
+    xs0 = m.exchange_stats() if sharded and not a.python_orchestration else None
     el = timed(a.warmup, a.steps)
+    xs1 = m.exchange_stats() if xs0 is not None else None
     kp = None
     if not a.no_profile:  # live per-kernel HIP events over the same number of steps
         m.profile(True)
@@ -220,8 +222,12 @@ def main():
         roof = None
         if kp and (kp["step_graph"]["count"] or kp["user_step"]["count"]):
             us = {k: v["ms"] / v["count"] * 1e3 for k, v in kp.items() if v["count"]}
-            if "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
-                step_us, what = us["step_graph"], ("sharded step: owner gather + row exchange + "
+            if "step_graph" in us and sharded and world == 1 and not a.python_orchestration:
+                # one rank: the runner dispatches to the single-GPU fused step (nothing to exchange)
+                step_us, what = us["step_graph"], ("world 1: the single-GPU fused step launches (the "
+                                                   "runner has no peer to exchange with)")
+            elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
+                step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
             elif "step_graph" in us and hog:  # one k_hogwild launch per chunk
                 step_us, what = us["step_graph"], ("k_hogwild (in-kernel sampling + gather + dots + "
@@ -232,14 +238,35 @@ def main():
             else:  # eager (sharded): events around the two kernels of sampled steps
                 step_us, what = us["user_step"] + us["item_step"], "user_step + item_step"
             ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9
+            # PMC bytes only for the kernel they were counted on: the single-GPU fused step (or
+            # the hogwild kernel); a sharded line (world > 1) gets them only from an entry measured
+            # on the sharded kernels themselves, keyed by world size
             tkey = f"ml20m_d{d}_B{B}" + ("_hogwild" if hog else "")
+            if sharded and not (world == 1 and not a.python_orchestration):
+                tkey = f"sharded_w{world}_ml20m_d{d}_B{B}"
             traffic, tsrc = load_traffic(tkey) if (U, I) == (U_ML20M, I_ML20M) else (None, None)
+            if traffic is None and sharded:
+                tsrc = ("none: no rocprofv3 --pmc pass has counted the sharded kernels at this world "
+                        "size (a single-GPU figure would describe other kernels)")
             roof = dict(bound="hbm", kernel=what, achieved=round(ach, 1), peak=HBM_PEAK_GBS,
                         unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                         traffic=traffic, traffic_source=tsrc,
                         algorithmic_bytes_per_launch=B * bytes_per_triplet(d),
                         avg_us_per_step=round(step_us, 3),
                         avg_launch_us={k: round(v, 3) for k, v in us.items()})
+            if sharded:
+                # per rank: `achieved` counts this rank's algorithmic bytes (its B triplets' rows
+                # and ids) over its own step time; the exchange bytes below are separate (xGMI
+                # link traffic, not HBM reads of this rank's step)
+                roof["bytes_counted"] = ("per rank: B*(24d+12) algorithmic bytes of the rank's own "
+                                         "batch per step; exchange bytes reported separately")
+        xch = None
+        if xs0 is not None and xs1 is not None:
+            ns = max(1, xs1["steps"] - xs0["steps"])
+            xch = {k: (xs1[k] - xs0[k]) // ns for k in ("row_bytes", "grad_bytes", "id_bytes")}
+            xch = {"per_rank_per_step": xch, "peer_links": world - 1, "steps": xs1["steps"] - xs0["steps"],
+                   "note": ("bytes this rank sent to its peers per step as the transport moved them "
+                            "(padded to the chunk's exchange capacity; world 1 sends nothing)")}
         cpu = None
         if not a.no_cpu_baseline and world == 1 and not sharded:
             cpu = cpu_baseline(pos, U, I, d, B)
@@ -261,6 +288,8 @@ def main():
                                         "in-flight window; NOT the reference step)" if hog else
                                         "exact batch-synchronous SGD (reference step), lazy weight decay")},
                "roofline": roof, "cpu_baseline": cpu}
+        if sharded:
+            out["exchange"] = xch
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

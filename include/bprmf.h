@@ -225,10 +225,23 @@ int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group);
  * 157-178 over this shard's users); stats: this shard's triplets and loss. */
 int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
                            bprmf_stats* stats);
+/* Bytes this rank sent to its peers since the transport was attached, as the transport moved
+ * them (padded to each chunk's exchange capacity): item rows (owner -> requesters), gradients
+ * (requester -> owners), request lists (once per chunk), and the steps they cover.  World 1
+ * sends nothing (bprmf_dist_train_steps then runs the single-GPU step). */
+int bprmf_dist_exchange_stats(bprmf_handle* h, int64_t* steps, int64_t* row_bytes,
+                              int64_t* grad_bytes, int64_t* id_bytes);
 /* Replay: u/i/j[n_steps * batch_size] host triplets (global ids, this shard's users; u < 0 marks
  * an empty slot), batch_size slots per step. */
 int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
                             int64_t n_steps, bprmf_stats* stats);
+
+/* ---- test hooks (no reference counterpart) ------------------------------------------------ */
+/* The launch tag the next split batch build of this process will carry (segment.hip): the tests
+ * use it to plant stale words that an unsafe tag scheme would mistake for this launch's. */
+int bprmf_debug_next_build_tag(uint32_t* tag);
+/* Fill every int32 of the handle's batch buffer with `value` (stale memory, deliberately). */
+int bprmf_debug_fill_batches(bprmf_handle* h, int32_t value);
 
 /* ---- ingestion: ratings files -> dense-coded rows (util/data_loader.py:27-146, :410-548) ---- */
 /* Host-only (no GPU).  Lines "<user> <sep> <item> <sep> <rating> <sep> <timestamp>" with any

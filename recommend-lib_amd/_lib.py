@@ -100,6 +100,8 @@ SIGNATURES = {
     "bprmf_dist_init_ipc": [_P, _P],
     "bprmf_dist_train_steps": [_P, ctypes.c_uint32, _I64, _I64, _P],
     "bprmf_dist_train_replay": [_P, _P, _P, _P, _I64, _P],
+    "bprmf_dist_exchange_stats": [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                                  ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     "bprmf_row_stride": [_P, ctypes.POINTER(ctypes.c_int32)],
     "bprmf_dataset_load": [ctypes.c_char_p, ctypes.c_float, ctypes.c_int32, ctypes.c_int32,
                            ctypes.POINTER(ctypes.c_void_p)],
@@ -109,6 +111,8 @@ SIGNATURES = {
     "bprmf_dataset_candidates": [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                  ctypes.POINTER(_I64), _P, _P],
     "bprmf_dataset_free": [_P],
+    "bprmf_debug_next_build_tag": [ctypes.POINTER(ctypes.c_uint32)],
+    "bprmf_debug_fill_batches": [_P, ctypes.c_int32],
     "bprmf_profile": [_P, ctypes.c_int32],
     "bprmf_profile_read": [_P, ctypes.POINTER(KProf)],
     # include/ncf.h
@@ -191,6 +195,13 @@ def load():
         f.restype = RESTYPES.get(name, ctypes.c_int)
     _lib = L
     return L
+
+
+def next_build_tag():
+    """The launch tag the process's next split batch build will carry (test hook)."""
+    t = ctypes.c_uint32()
+    check(load().bprmf_debug_next_build_tag(ctypes.byref(t)))
+    return t.value
 
 
 def check(rc):

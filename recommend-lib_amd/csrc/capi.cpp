@@ -465,7 +465,22 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   h->d_batch = nullptr;
   h->batch_cap = 0;
   if (int r = dalloc(&h->d_batch, n_batches * BatchBuf::stride_for((int)B))) return r;
+  // zeroed once: the split builder's exchange and sampling-board words (segment.hip) must never
+  // see an earlier allocation's ints (a recycled block holds another handle's records, and those
+  // small numbers once matched a fresh process's first launch tags)
+  HIPCHK(hipMemsetAsync(h->d_batch, 0, sizeof(int32_t) * n_batches * BatchBuf::stride_for((int)B),
+                        h->stream));
   h->batch_cap = n_batches;
+  return 0;
+}
+
+extern "C" int bprmf_debug_fill_batches(bprmf_handle* h, int32_t value) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (!h->d_batch) return fail(BPRMF_E_STATE, "no batch buffer yet");
+  if (int r = set_dev(h)) return r;
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_batch, value,
+                           (size_t)h->batch_cap * BatchBuf::stride_for(h->cfg.batch_size), h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
 
@@ -502,6 +517,7 @@ StepBufs bprmf::step_bufs(const bprmf_handle* h) {
   b.pend_p = h->fused ? h->d_pend_p : nullptr;
   b.qrows = h->I;
   b.prows = h->U;
+  b.build_err = h->d_err;
   return b;
 }
 

@@ -352,6 +352,10 @@ struct DistState {
   int cap = 0;           // rows per peer per step of the current chunk
   int64_t nmax = 0;      // steps per chunk
   int64_t chunks = 0;    // chunks run (parity, per-chunk sequence numbers)
+  // bytes this rank sent over peer links since attach (padded to the exchange capacity, what the
+  // transport moves): item rows (owner -> requesters), gradients (requester -> owners), request
+  // lists (once per chunk); steps they cover (bprmf_dist_exchange_stats)
+  int64_t x_steps = 0, x_rows = 0, x_grads = 0, x_ids = 0;
   int64_t aplan_n[2] = {0, 0};
   int32_t* ids_send = nullptr;     // [W][n][cap]
   int32_t* ids_recv = nullptr;     // shared, 2 parities x [W][nmax][S]
@@ -696,6 +700,13 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   if (graph) cap = std::min(d->S, (cap + 63) / 64 * 64);  // few distinct plans: graphs get reused
   d->cap = cap;
   if (int r = ensure_aplan(h, par, n, cap)) return r;
+  {
+    const int64_t peers = W - 1, rowb = (int64_t)cap * h->geom.ld * (int64_t)sizeof(float);
+    d->x_steps += n;
+    d->x_rows += n * peers * rowb;
+    d->x_grads += n * peers * rowb;
+    d->x_ids += cap > 0 ? peers * n * cap * (int64_t)sizeof(int32_t) : 0;
+  }
   int32_t* ids_recv = d->ids_recv + (int64_t)par * W * d->nmax * d->S;
   int32_t* aplan = d->aplan[par];
   if (cap > 0) {
@@ -851,12 +862,29 @@ int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group) {
   return dist_attach(h, tr);
 }
 
+int bprmf_dist_exchange_stats(bprmf_handle* h, int64_t* steps, int64_t* row_bytes,
+                              int64_t* grad_bytes, int64_t* id_bytes) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  const DistState* d = h->dist;
+  if (steps) *steps = d ? d->x_steps : 0;
+  if (row_bytes) *row_bytes = d ? d->x_rows : 0;
+  if (grad_bytes) *grad_bytes = d ? d->x_grads : 0;
+  if (id_bytes) *id_bytes = d ? d->x_ids : 0;
+  return 0;
+}
+
 int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
                            bprmf_stats* st) {
   if (!h || first_step < 0 || n_steps < 0) return fail(BPRMF_E_INVALID, "bad arguments");
   if (!h->dist || !h->dist->tr->ready())
     return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
   if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
+  // one rank: nothing to exchange, so the single-GPU fused step runs (the same sampler stream,
+  // the same step; BPRMF_DIST_W1_RUNNER=1 keeps the runner, to measure it)
+  if (h->cfg.world == 1 && !h->dist->tr->self_exchange) {
+    const char* e = getenv("BPRMF_DIST_W1_RUNNER");
+    if (!(e && e[0] == '1')) return bprmf_train_steps(h, epoch, first_step, n_steps, st);
+  }
   if (int r = begin_call(h)) return r;
   const int64_t chunk = dist_chunk_steps(h);
   for (int64_t s = 0; s < n_steps; s += chunk)

@@ -197,7 +197,11 @@ struct StepBufs {
   int32_t* pend_q = nullptr;
   int32_t* pend_p = nullptr;
   int64_t qrows = 0, prows = 0;
+  // single GPU: the call's error word; a batch build that timed out (bit 16, segment.hip) leaves
+  // its batches unfinished, so every step workgroup then returns without touching a row
+  const int32_t* build_err = nullptr;
 };
+constexpr int32_t kErrBuild = 16;
 // sharded K1 over the IPC transport: wait for the peers' row flags first (flags == null: none)
 struct PeerWait {
   const int32_t* flags = nullptr;

@@ -673,7 +673,13 @@ static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E
 // [2 + o / 2] tag << 32 | cnt[o] | cnt[o + 1] << 16 with cnt[o] = the part's segments of owners
 // below o.  The area is the batch's ioff range from its second int (8-byte aligned, 2B ints; the
 // bucket builds never store ioff), so B >= kItemParts * kXchWords.
+// A tag is never confused with what the area held before this launch: the batch buffer is zeroed
+// when it is allocated (stale ints of an earlier allocation would otherwise be small numbers like
+// the first tags of a process), later launches on it used other tags, and every tag has bit 31 set
+// (kTagMark), which the one-workgroup radix build's ioff positions (< 2^16) never have.
 constexpr int kXchWords = 2 + kMaxWorld / 2;
+constexpr uint32_t kTagMark = 0x80000000u;
+constexpr uint32_t kBoardMagic = 0x534D504Bu;  // "SMPK": high half of a sampling-board mark
 static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
   return reinterpret_cast<uint64_t*>(v.ioff + 1);
 }
@@ -780,12 +786,15 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are acknowledged
     __syncthreads();                                    // ... and every wave's
+    // the mark is the whole 64-bit word {kBoardMagic, tag}: a stale int pair in the buffer would
+    // have to equal both halves (the buffer is zeroed when allocated, capi.cpp ensure_seg)
     uint64_t* board = xch_of(v) + (int64_t)kItemParts * kXchWords;
-    if (tid == 0) __hip_atomic_store(board + role, (uint64_t)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t mark = (uint64_t)kBoardMagic << 32 | tag;
+    if (tid == 0) __hip_atomic_store(board + role, mark, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid <= kItemParts && tid != role) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (uint32_t polls = 0;; ++polls) {
-        if ((uint32_t)__hip_atomic_load(board + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) break;
+        if (__hip_atomic_load(board + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mark) break;
         __builtin_amdgcn_s_sleep(1);
         if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
           atomicOr(err, 16);
@@ -1141,6 +1150,18 @@ extern "C" int bprmf_debug_build_stamps(uint64_t* out) {
 }
 #endif
 
+// the split builder's launch tags: one counter for every handle and thread of the process, so
+// each launch's tag differs from every tag written into any batch buffer before it (2^31 launches
+// before a repeat); bit 31 always set (kTagMark)
+static std::atomic<uint32_t> g_build_tag{0};
+static uint32_t next_build_tag() { return kTagMark | (g_build_tag.fetch_add(1) + 1); }
+// test hook (include/bprmf.h): the tag the next split-builder launch of this process will carry
+extern "C" int bprmf_debug_next_build_tag(uint32_t* tag) {
+  if (!tag) return -1;
+  *tag = kTagMark | (g_build_tag.load() + 1);
+  return 0;
+}
+
 static int bits_for(int64_t n) {  // radix-sort bits covering ids in [0, n)
   int b = 1;
   while (b < 32 && (1LL << b) < n) ++b;
@@ -1189,11 +1210,7 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
     if (e != hipSuccess) return e;
   }
   if (split) {
-    // the launch's tag on the parts' exchanged counts: a fresh value per launch (one counter for
-    // every handle and thread; a batch's words from an earlier launch carry an older tag), never 0
-    static std::atomic<uint32_t> next_tag{0};
-    uint32_t tag = ++next_tag;
-    if (tag == 0) tag = ++next_tag;
+    const uint32_t tag = next_build_tag();
     const unsigned grid = (unsigned)(n_batches * (kItemParts + 1));
 #define BPRMF_SPLIT(SL_, SMP_, W_, STRIDE_, K1_)                                                 \
   k_build_split<SL_, SMP_><<<grid, kBuildThreads, 0, s>>>(                                       \

@@ -180,6 +180,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
   // blocks: the index is clamped into the batch's B records (never read past them)
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[min(p, B - 1)];
   const int n = bv.meta[0];
+  const bool dead = sb.build_err && (*sb.build_err & kErrBuild);  // the batch build failed
   const int64_t par = sb.pstride ? (int64_t)(t & 1) : 0;  // this step's half of the buffers
   float* contrib = sb.contrib + par * sb.pstride;
   float* ugrad = sb.ugrad + par * sb.pstride;
@@ -199,7 +200,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     }
     wait_peer_flags(pw->flags, pw->world, pw->self, t, pw->err);
   }
-  if (p < n) {
+  if (p < n && !dead) {
     // bit 31: the item's first reference in the batch; bit 30 (single GPU): its ONLY reference,
     // so this triplet finishes the item (no contribution row, no K2 record)
     const int32_t i = r.x & 0x3FFFFFFF, j = r.y & 0x3FFFFFFF;
@@ -462,11 +463,13 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const float* __restrict__ ugrad = sb.ugrad + par * sb.pstride;
   const float* __restrict__ xloss = sb.xloss ? sb.xloss + par * B : nullptr;
   if (!xloss) loss = nullptr;
+  const bool dead = sb.build_err && (*sb.build_err & kErrBuild);  // the batch build failed
   // the step's loss: the first loss_blocks(B, KB) workgroups (dispatched first, off the tail) each
   // sum log(1 + e^-x) over KB triplets, one per thread, in a fixed tree, and add it to their own
   // slot loss[b] (one writer per slot per launch; the host adds the slots once per call)
   const int lb = loss ? (B + KB - 1) / KB : 0;
   if (blk < lb) {
+    if (dead) return;
     __shared__ double red[KB / 64];
     const int n = bv.meta[0];
     const int p = blk * KB + threadIdx.x;
@@ -491,7 +494,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int n_multi = bv.meta[4];
     SSTAMP(1, 1);
     SROLE(1, 3);
-    if (m >= n_multi) return;
+    if (m >= n_multi || dead) return;
     const int32_t u = r0.x;
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
     float4 cur[S], g[S];
@@ -513,7 +516,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int n_long = bv.meta[3];
     SSTAMP(1, 1);
     SROLE(1, 1);
-    if (bid >= n_long) return;  // uniform over the block
+    if (bid >= n_long || dead) return;  // uniform over the block
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
     ItemRow<G4, S, SH> row;
@@ -574,7 +577,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   SSTAMP(1, 1);
   SROLE(1, 2);
   // record {item, beg | len << 15 | long << 30, refs 0..11 as 16-bit halves} (segment.hip)
-  if (s >= n_iseg || (r0.y >> 30)) return;  // past the batch's items, or a workgroup-served hot item
+  if (s >= n_iseg || (r0.y >> 30) || dead) return;  // past the batch's items, or a workgroup-served hot item
   const int32_t item = r0.x;
   const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
 #ifdef BPRMF_STEP_STAMPS

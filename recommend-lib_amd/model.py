@@ -213,6 +213,12 @@ class BPRMF:
         _lib.check(self._L.bprmf_profile_read(self._h, ctypes.byref(k)))
         return k.as_dict()
 
+    # -- test hooks ----------------------------------------------------------------------------
+    def debug_fill_batches(self, value):
+        """Fill the batch buffer with int32 `value` (deliberately stale memory; tests only)."""
+        v = int(value) & 0xFFFFFFFF
+        _lib.check(self._L.bprmf_debug_fill_batches(self._h, v - (1 << 32) if v >> 31 else v))
+
     # -- weights -------------------------------------------------------------------------------
     def local_rows(self):
         u, i = ctypes.c_int64(), ctypes.c_int64()

@@ -244,6 +244,11 @@ class HipShard:
                                                   j.ctypes.data, int(n_steps), ctypes.byref(st)))
         return st.as_dict()
 
+    def exchange_stats(self):
+        v = [ctypes.c_int64() for _ in range(4)]
+        _lib.check(self.L.bprmf_dist_exchange_stats(self.h, *map(ctypes.byref, v)))
+        return dict(zip(("steps", "row_bytes", "grad_bytes", "id_bytes"), (x.value for x in v)))
+
     def get_weights(self):
         return self.m.get_weights()
 
@@ -373,6 +378,11 @@ class ShardedBPRMF:
     def train_steps(self, epoch, first_step, n_steps):
         """Global steps [first_step, first_step + n_steps) of `epoch` on every rank (same args)."""
         return self.b.runner_train_steps(epoch, first_step, n_steps)
+
+    def exchange_stats(self):
+        """Bytes this rank sent to peers since attach_runner (rows, gradients, request lists) and
+        the steps they cover (the runner's padded exchange volume)."""
+        return self.b.exchange_stats()
 
     def train_epoch(self, epoch):
         return self.train_steps(epoch, 0, self.steps_per_epoch)

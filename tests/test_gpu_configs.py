@@ -274,3 +274,93 @@ def test_c5_shape_one_gpu_sampler_steps_and_decay(rl):
     np.testing.assert_allclose(Pc1, Pc0 * alpha ** steps, rtol=DECAY_RTOL)
     np.testing.assert_allclose(Qc1, Qc0 * alpha ** steps, rtol=DECAY_RTOL)
     assert np.abs(Qc0).max() > 0  # the init reached the table's last rows
+
+
+# ---- C5 through the sharded runner: 2 in-process shards, 56 GB of tables each -------------------
+def test_c5_shape_two_shards_runner_against_dense_oracle(rl):
+    """BASELINE config C5's model (10M users x 100M items, d=256; tables per BPRMFRecommender.py:
+    36-40) item- and user-sharded over 2 in-process shards of the library's runner (loopback
+    transport) on the one GPU: each shard holds 5M user rows and 50M item rows (51.2 GB of item
+    table, row offsets far past 2^32 floats in the owner gather, the landing buffers and the
+    slots).  Checked: each shard's sampler slices bit-exact against the oracle (shard seed), 3
+    runner steps against the dense reference step on the union batches (touched rows read back
+    with get_rows), untouched rows decayed by exactly (1 - lr*wd)^3, the loss."""
+    _free()
+    U, I, d, B, seed, steps, world = 10_000_000, 100_000_000, 256, 4096, 5, 3, 2
+    lr, wd = 0.01, 0.001
+    pos = _c5_positives(U, I, 2_000_000, 55)
+    sh = rl.sharded
+    grp = sh.ThreadGroup(world)
+    g = np.random.default_rng(2)
+    probe_u, probe_i = g.integers(0, U, 4000), g.integers(0, I, 4000)
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, seed=seed, device=0, comm=comm)
+        try:
+            m.set_train(pos)
+            h = m.b.m
+            N_r = h.epoch_size()[0]
+            slices = {first: h.sample(0, first, 20_000) for first in (0, N_r - 20_000)}
+            trip = h.sample(0, 0, steps * B)
+            grp.vals[r] = trip
+            comm.g.barrier.wait()
+            tu = np.concatenate([grp.vals[q][0] for q in range(world)])
+            ti = np.concatenate([np.concatenate([grp.vals[q][1], grp.vals[q][2]]) for q in range(world)])
+            comm.g.barrier.wait()
+            users, items = np.unique(tu), np.unique(ti)
+            cold_u = np.setdiff1d(probe_u, users)
+            cold_i = np.setdiff1d(np.concatenate([probe_i, [I - 2, I - 1]]), items)
+            mine = lambda a: a[a % world == r]  # noqa: E731
+            rows = {k: mine(v) for k, v in dict(u=users, i=items, cu=cold_u, ci=cold_i).items()}
+            read = lambda: {k: h.get_rows("user" if k in ("u", "cu") else "item", v // world)  # noqa: E731
+                            for k, v in rows.items()}
+            before = read()
+            m.attach_runner("loopback", key=5502)
+            st = m.train_steps(0, 0, steps)
+            after = read()
+            return dict(N=N_r, slices=slices, trip=trip, rows=rows, before=before, after=after, st=st)
+        finally:
+            m.b.m.close()
+
+    out = _runner_threads(rl, world, fn)
+    for r in range(world):  # each shard's sampler is the oracle's for its users and shard seed
+        mine = pos[pos[:, 0] % world == r]
+        indptr, indices = O.build_csr(mine[:, 0], mine[:, 1], U)
+        assert out[r]["N"] == 4 * len(mine)
+        for first, got in out[r]["slices"].items():
+            want = C.sample(mine[:, 0], mine[:, 1], indptr, indices, I, 4,
+                            (seed + r * 0x9E3779B97F4A7C15) & (2**64 - 1), 0, first, 20_000)
+            for x, y in zip(got, want):
+                assert np.array_equal(x, y), (r, first)
+    _free()
+    # the dense reference step on the union batches, over the touched rows only
+    cat = lambda key, c: np.concatenate([o[key][c] for o in out])  # noqa: E731
+    users = np.sort(cat("rows", "u"))
+    items = np.sort(cat("rows", "i"))
+    assert items.max() > 2 ** 26 and users.max() > 2 ** 23
+
+    def assemble(which, key, ids):
+        t = np.empty((len(ids), d), np.float32)
+        for o in out:
+            t[np.searchsorted(ids, o["rows"][key])] = o[which][key]
+        return t
+
+    ref = C.DenseTrainer(assemble("before", "u", users), assemble("before", "i", items), lr, wd)
+    loss = 0.0
+    for k in range(steps):
+        s = slice(k * B, (k + 1) * B)
+        bu = np.concatenate([o["trip"][0][s] for o in out])
+        bi = np.concatenate([o["trip"][1][s] for o in out])
+        bj = np.concatenate([o["trip"][2][s] for o in out])
+        loss += ref.step(np.searchsorted(users, bu).astype(np.int32),
+                         np.searchsorted(items, bi).astype(np.int32),
+                         np.searchsorted(items, bj).astype(np.int32))
+    np.testing.assert_allclose(assemble("after", "u", users), ref.P, rtol=0, atol=SHARD_ATOL)
+    np.testing.assert_allclose(assemble("after", "i", items), ref.Q, rtol=0, atol=SHARD_ATOL)
+    assert sum(o["st"]["loss"] for o in out) == pytest.approx(loss, rel=1e-5)
+    assert sum(o["st"]["triplets"] for o in out) == steps * world * B
+    alpha = np.float32(1.0) - np.float32(lr) * np.float32(wd)
+    for o in out:
+        for key in ("cu", "ci"):
+            np.testing.assert_allclose(o["after"][key], o["before"][key] * alpha ** steps, rtol=DECAY_RTOL)
+    assert any(np.abs(o["before"]["ci"]).max() > 0 for o in out)  # the init reached the last rows

@@ -50,18 +50,22 @@ def test_sharded_replay_equals_single_gpu_global_batch(rl, world):
         m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=GB, device=0, comm=comm)
         m.set_weights(sh.shard_rows(P0, r, world), sh.shard_rows(Q0, r, world))
         m.plan_replay(batches)
+        snaps = []
         for k in range(steps):
             m.step_replay(k)
-        return m.get_weights()
+            snaps.append(m.get_weights())  # every step's state, checked below
+        return snaps
 
     parts = _run_threads(rl, world, fn)
-    P = sh.unshard_rows([p[0] for p in parts], U)
-    Q = sh.unshard_rows([p[1] for p in parts], I)
     Pr, Qr = P0.copy(), Q0.copy()
-    for u, i, j in batches:
+    for k, (u, i, j) in enumerate(batches):
         O.bpr_step_dense(Pr, Qr, u, i, j, 0.05, 0.01)
-    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+        for r in range(world):
+            for name, got, want in (("P", parts[r][k][0], Pr[r::world]), ("Q", parts[r][k][1], Qr[r::world])):
+                bad = ~np.isclose(got, want, rtol=1e-5, atol=1e-6)
+                assert not bad.any(), (f"world {world}, step {k}, rank {r}: {name} differs from the "
+                                       f"dense oracle in {int(bad.sum())} of {bad.size} elements "
+                                       f"(max {np.abs(got - want).max():.3g})")
 
 
 @pytest.mark.parametrize("Uu,Ii", [(16, 32), (4, 8)])

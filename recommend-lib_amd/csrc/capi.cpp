@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "handle.h"
+#include "host_plan.h"
 
 using namespace bprmf;
 
@@ -112,8 +113,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   }
   h->hp.log2a = std::log2(h->hp.alpha);
   const int64_t W = cfg->world, R = cfg->rank;
-  h->U = (cfg->user_num - R + W - 1) / W;
-  h->I = (cfg->item_num - R + W - 1) / W;
+  h->U = shard_rows(cfg->user_num, (int)W, (int)R);
+  h->I = shard_rows(cfg->item_num, (int)W, (int)R);
   const uint64_t shard_seed = cfg->seed + (uint64_t)cfg->rank * 0x9E3779B97F4A7C15ull;
   h->k0 = (uint32_t)shard_seed;
   h->k1 = (uint32_t)(shard_seed >> 32);
@@ -240,38 +241,15 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   if (!h || (nnz > 0 && (!users || !items)) || nnz < 0) return fail(BPRMF_E_INVALID, "bad arguments");
   if (n_ex < 0 || (n_ex > 0 && (!ex_users || !ex_items))) return fail(BPRMF_E_INVALID, "bad exclusions");
   if (int r = set_dev(h)) return r;
-  const int64_t W = h->cfg.world, R = h->cfg.rank;
-  std::vector<int32_t> pu, pi;
-  pu.reserve(nnz / W + 16);
-  pi.reserve(nnz / W + 16);
-  for (int64_t k = 0; k < nnz; ++k) {
-    const int32_t u = users[k], i = items[k];
-    if (u < 0 || u >= h->cfg.user_num || i < 0 || i >= h->cfg.item_num)
-      return fail(BPRMF_E_RANGE, "positive %lld = (%d, %d) out of range", (long long)k, u, i);
-    if (u % W == R) {
-      pu.push_back(u);
-      pi.push_back(i);
-    }
-  }
+  ShardCsr csr;  // host_plan.cpp (sanitizer-tested host code)
+  if (int r = build_shard_csr(users, items, nnz, ex_users, ex_items, n_ex, h->cfg.user_num,
+                              h->cfg.item_num, h->cfg.world, h->cfg.rank, h->U, &csr))
+    return r;
+  const std::vector<int32_t>& pu = csr.pos_u;
+  const std::vector<int32_t>& pi = csr.pos_i;
+  const std::vector<int64_t>& indptr = csr.indptr;
+  const std::vector<int32_t>& indices = csr.indices;
   const int64_t n = (int64_t)pu.size();
-  // sorted, de-duplicated positive lists per local user (the dok train_mat): features + exclusions
-  std::vector<uint64_t> keys(n);
-  for (int64_t k = 0; k < n; ++k) keys[k] = ((uint64_t)(pu[k] / W) << 32) | (uint32_t)pi[k];
-  for (int64_t k = 0; k < n_ex; ++k) {
-    const int32_t u = ex_users[k], i = ex_items[k];
-    if (u < 0 || u >= h->cfg.user_num || i < 0 || i >= h->cfg.item_num)
-      return fail(BPRMF_E_RANGE, "train_mat entry (%d, %d) out of range", u, i);
-    if (u % W == R) keys.push_back(((uint64_t)(u / W) << 32) | (uint32_t)i);
-  }
-  std::sort(keys.begin(), keys.end());
-  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-  std::vector<int64_t> indptr(h->U + 1, 0);
-  std::vector<int32_t> indices(keys.size());
-  for (size_t k = 0; k < keys.size(); ++k) {
-    indptr[(keys[k] >> 32) + 1]++;
-    indices[k] = (int32_t)(keys[k] & 0xFFFFFFFFu);
-  }
-  for (int64_t u = 0; u < h->U; ++u) indptr[u + 1] += indptr[u];
   void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices};
   for (void* p : olds)
     if (p) HIPCHK(hipFree(p));

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "handle.h"
+#include "host_plan.h"
 
 namespace bprmf {
 
@@ -407,12 +408,14 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   d->tr = tr;
   tr->self_exchange = getenv("BPRMF_DIST_SELF_EXCHANGE") != nullptr;
   h->dist = d;
-  const int64_t W = h->cfg.world, B = h->cfg.batch_size;
-  const int64_t iloc = (h->cfg.item_num + W - 1) / W;
-  d->S = (int)std::min<int64_t>(2 * B, iloc);
-  d->nmax = dist_chunk_steps(h);
-  const int64_t rows = W * d->S * h->geom.ld;
-  const int64_t ids = W * d->nmax * d->S;
+  const int64_t W = h->cfg.world;
+  RunnerGeom rg;  // host_plan.cpp (sanitizer-tested host code)
+  if (int r = runner_geom(h->cfg.batch_size, h->cfg.item_num, (int)W, h->geom.ld, dist_chunk_steps(h), &rg))
+    return r;
+  d->S = rg.S;
+  d->nmax = rg.nmax;
+  const int64_t rows = rg.row_elems;
+  const int64_t ids = rg.id_elems;
   void* p = nullptr;
   if (int r = tr->alloc_shared(h, X_ROWS, sizeof(float) * rows, &p)) return r;
   d->rows_recv = static_cast<float*>(p);
@@ -440,8 +443,7 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
 
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   DistState* d = h->dist;
-  const int64_t W = h->cfg.world;
-  const int64_t ap = n * W * std::max(cap, 1) * (3 * W + 1);  // rec, gdep, gfree, pflag
+  const int64_t ap = aplan_words(n, h->cfg.world, cap);  // rec, gdep, gfree, pflag
   if (ap <= d->aplan_n[par]) return 0;
   if (d->aplan[par]) HIPCHK(hipFree(d->aplan[par]));
   d->aplan[par] = nullptr;
@@ -695,9 +697,10 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   if (hv[1]) {
     if (int r = check_err_flag(h)) return r;
   }
-  if (cap < 0 || cap > d->S) return fail(BPRMF_E_STATE, "exchange capacity %d outside [0, %d]", cap, d->S);
   const bool graph = h->use_graphs && d->tr->capturable() && cap > 0;
-  if (graph) cap = std::min(d->S, (cap + 63) / 64 * 64);  // few distinct plans: graphs get reused
+  const int raw = cap;
+  cap = exchange_capacity(raw, d->S, graph);  // graphs: rounded to 64 rows, so plans get reused
+  if (cap < 0) return fail(BPRMF_E_STATE, "exchange capacity %d outside [0, %d]", raw, d->S);
   d->cap = cap;
   if (int r = ensure_aplan(h, par, n, cap)) return r;
   {
@@ -815,15 +818,8 @@ int bprmf_dist_init_ipc(bprmf_handle* h, const uint8_t* blobs) {
   if (tr->opened) return fail(BPRMF_E_STATE, "ipc transport already initialised");
   if (int r = set_dev(h)) return r;
   for (int b = 0; b < kIpcHandles; ++b) tr->remote[b].assign(tr->world, nullptr);
-  {
-    const size_t off = kIpcHandles * sizeof(hipIpcMemHandle_t);
-    const char* mine = reinterpret_cast<const char*>(blobs) + (size_t)tr->rank * BPRMF_IPC_BLOB_BYTES + off;
-    for (int p = 0; p < tr->world; ++p)
-      if (p != tr->rank &&
-          strncmp(mine, reinterpret_cast<const char*>(blobs) + (size_t)p * BPRMF_IPC_BLOB_BYTES + off,
-                  kBusIdBytes) == 0)
-        tr->shared_device = true;
-  }
+  tr->shared_device = ipc_shares_device(blobs, tr->world, tr->rank, BPRMF_IPC_BLOB_BYTES,
+                                        kIpcHandles * sizeof(hipIpcMemHandle_t), kBusIdBytes);
   for (int p = 0; p < tr->world; ++p)
     for (int b = 0; b < kIpcHandles; ++b) {
       if (p == tr->rank) {

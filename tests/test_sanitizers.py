@@ -2,7 +2,9 @@
 
 tests/sanitize/Makefile builds ASan + UBSan variants of the host ingestion of libbprmf_amd
 (csrc/ingest.cpp + csrc/status.cpp: the restatement of util/data_loader.py:27-146,444-548) and of
-the C oracles (oracle/bpr_cpu.c, oracle/mf_cpu.c).  This test runs the CPU suites that drive them
+the C oracles (oracle/bpr_cpu.c, oracle/mf_cpu.c), and of the host-only planning logic of the
+handle and its sharded runner (csrc/host_plan.cpp, driven by tests/sanitize/host_plan_check.cpp).
+This test runs the CPU suites that drive them
 in a child pytest with libasan preloaded (Python itself is not instrumented), the ingestion loaded
 from the sanitizer build (BPRMF_DIAG_LIB) and the oracles from theirs (BPRMF_ORACLE_LIB_DIR).
 Any ASan report or UBSan finding aborts the child (-fno-sanitize-recover, halt_on_error), so the
@@ -56,6 +58,19 @@ def test_sanitizer_build_is_instrumented(san_build):
         r = subprocess.run(["nm", "-D", os.path.join(san_build, name)], capture_output=True, text=True)
         assert "__asan_" in r.stdout, name
         assert "__ubsan_" in r.stdout, name
+
+
+def test_host_plan_clean_under_asan_ubsan(san_build):
+    """The handle's and the sharded runner's host-only planning code (csrc/host_plan.cpp: shard
+    positive lists, runner geometry, exchange capacity, IPC blob comparison) under ASan + UBSan,
+    every result checked against a restatement (tests/sanitize/host_plan_check.cpp)."""
+    exe = os.path.join(san_build, "host_plan_check")
+    r = subprocess.run(["nm", exe], capture_output=True, text=True)
+    assert "__asan_" in r.stdout and "__ubsan_" in r.stdout
+    r = subprocess.run([exe], env=_env(san_build), capture_output=True, text=True, timeout=600)
+    log = r.stdout[-4000:] + r.stderr[-4000:]
+    assert "AddressSanitizer" not in log and "runtime error:" not in log, log
+    assert r.returncode == 0 and "host_plan_check: ok" in r.stdout, log
 
 
 @pytest.mark.parametrize("suite", SUITES)

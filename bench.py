@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild"],
                     help="exact: the reference's batch-synchronous step (default, the headline); "
                          "hogwild: opt-in relaxed synchronisation (a separate, labelled line)")
+    ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
+                    help="exact step's duplicate-row sums: segmented (sorted, one writer per row, "
+                         "bitwise reproducible; the headline) or atomic (f32 atomics; a labelled line)")
     ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend (gloo: rehearse several ranks on one GPU, IPC "
                          "transport; RCCL refuses two ranks on one device)")
@@ -144,6 +147,8 @@ def main():
     hog = a.semantics == "hogwild"
     if hog and sharded:
         raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
+    if a.step == "atomic" and (sharded or hog):
+        raise SystemExit("--step atomic is the single-GPU exact step's alternative")
     if sharded:
         import torch.distributed as dist
         if "RANK" not in os.environ:  # --sharded without a launcher: a one-rank group
@@ -158,7 +163,7 @@ def main():
     pos = syn.make_positives(U, I, a.positives, a.seed)
     if not sharded:
         m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed, device=local,
-                     semantics=a.semantics)
+                     semantics=a.semantics, step=a.step)
         m.set_train(pos)
         n_steps = m.epoch_size()[1]
 
@@ -235,13 +240,17 @@ def main():
             elif "step_graph" in us:  # events around each chunk's step launches (GPU-bound)
                 step_us, what = us["step_graph"], ("fused step launches (K2 of step t + K1 of step "
                                                    "t+1 per launch; a chunk is K1, n-1 fused, K2)")
+            elif a.step == "atomic" and "user_step" in us:  # fwd_scatter + apply_refs per step
+                step_us, what = us["user_step"] + us["item_step"], ("atomic step: k_fwd_scatter (gathers, "
+                                                                    "dots, f32-atomic gradient scatter) + "
+                                                                    "k_apply_refs (decay + SGD per touched row)")
             else:  # eager (sharded): events around the two kernels of sampled steps
                 step_us, what = us["user_step"] + us["item_step"], "user_step + item_step"
             ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9
             # PMC bytes only for the kernel they were counted on: the single-GPU fused step (or
             # the hogwild kernel); a sharded line (world > 1) gets them only from an entry measured
             # on the sharded kernels themselves, keyed by world size
-            tkey = f"ml20m_d{d}_B{B}" + ("_hogwild" if hog else "")
+            tkey = f"ml20m_d{d}_B{B}" + ("_hogwild" if hog else "") + ("_atomic" if a.step == "atomic" else "")
             if sharded and not (world == 1 and not a.python_orchestration):
                 tkey = f"sharded_w{world}_ml20m_d{d}_B{B}"
             traffic, tsrc = load_traffic(tkey) if (U, I) == (U_ML20M, I_ML20M) else (None, None)
@@ -286,6 +295,9 @@ def main():
                           "semantics": ("relaxed (hogwild: per-triplet lock-free updates, weight decay "
                                         "once per row per step, staleness bounded by the launch's "
                                         "in-flight window; NOT the reference step)" if hog else
+                                        "exact batch-synchronous SGD (reference step), lazy weight decay, "
+                                        "duplicate rows summed by f32 atomics (not bitwise reproducible)"
+                                        if a.step == "atomic" else
                                         "exact batch-synchronous SGD (reference step), lazy weight decay")},
                "roofline": roof, "cpu_baseline": cpu}
         if sharded:

@@ -43,6 +43,14 @@ typedef enum {
  * bounded by the launch's in-flight window.  Single-GPU handles only. */
 enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1 };
 
+/* How an EXACT step sums duplicate rows' gradients ("ship both").  SEGMENTED: the
+ * batch is sorted by user and by item and every row is summed by one writer in a fixed order,
+ * bitwise reproducible (batch_size <= 8192; the sharded runner needs it).  ATOMIC: f32 atomics
+ * into per-row gradient accumulators, then one pass applies every touched row; any batch size,
+ * the same step up to the order of the fp32 sums (not bitwise reproducible).  Larger batches
+ * than 8192 always take ATOMIC. */
+enum { BPRMF_STEP_SEGMENTED = 0, BPRMF_STEP_ATOMIC = 1 };
+
 typedef struct {
   int64_t user_num;     /* rows of embed_user  (BPRMFRecommender.py:36) — global count */
   int64_t item_num;     /* rows of embed_item  (BPRMFRecommender.py:37) — global count */
@@ -58,7 +66,8 @@ typedef struct {
   int32_t world;        /* 1 for a single GPU */
   int32_t semantics;    /* BPRMF_SEM_EXACT (0, default): the reference's batch-synchronous step;
                            BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
-  int32_t reserved[3];
+  int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
+  int32_t reserved[2];
 } bprmf_config;
 
 typedef struct {

@@ -100,6 +100,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0) or BPRMF_SEM_HOGWILD (1)");
   if (cfg->semantics == BPRMF_SEM_HOGWILD && cfg->world != 1)
     return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
+  if (cfg->step_mode != BPRMF_STEP_SEGMENTED && cfg->step_mode != BPRMF_STEP_ATOMIC)
+    return fail(BPRMF_E_INVALID, "step_mode must be BPRMF_STEP_SEGMENTED (0) or BPRMF_STEP_ATOMIC (1)");
+  if (cfg->step_mode == BPRMF_STEP_ATOMIC && cfg->world != 1)
+    return fail(BPRMF_E_UNSUPPORTED, "the atomic step: single-GPU handles only (the sharded runner sums by segments)");
   auto* h = new bprmf_handle();
   h->cfg = *cfg;
   h->semantics = cfg->semantics;
@@ -422,7 +426,9 @@ bool bprmf::split_build(int64_t nb) {
   return nb <= 512;
 }
 
-bool bprmf::seg_mode(const bprmf_handle* h) { return h->cfg.batch_size <= kMaxSegBatch; }
+bool bprmf::seg_mode(const bprmf_handle* h) {
+  return h->cfg.batch_size <= kMaxSegBatch && h->cfg.step_mode != BPRMF_STEP_ATOMIC;
+}
 
 int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   const int64_t B = h->cfg.batch_size;
@@ -559,7 +565,14 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
   // the executable graph's device-side setup now (set_train) rather than inside its first replay
   // (BPRMF_GRAPH_UPLOAD=0: lazily, A/B)
   const char* up = getenv("BPRMF_GRAPH_UPLOAD");
-  if (!(up && up[0] == '0')) HIPCHK(hipGraphUpload(out->exec, h->stream));
+  if (!(up && up[0] == '0')) {
+    const hipError_t eu = hipGraphUpload(out->exec, h->stream);
+    if (eu != hipSuccess) {  // the caller never keeps a failed graph: destroy it here
+      hipGraphExecDestroy(out->exec);
+      out->exec = nullptr;
+      return fail(BPRMF_E_HIP, "step graph upload: %s", hipGetErrorString(eu));
+    }
+  }
   return 0;
 }
 

@@ -622,7 +622,12 @@ static int launch_dist_graph(bprmf_handle* h, int64_t n, int cap, const int32_t*
       ge->exec = nullptr;
       return fail(BPRMF_E_HIP, "sharded step graph instantiate: %s", hipGetErrorString(e));
     }
-    HIPCHK(hipGraphUpload(ge->exec, h->stream));  // its device-side setup before its first replay
+    const hipError_t eu = hipGraphUpload(ge->exec, h->stream);  // device-side setup before its first replay
+    if (eu != hipSuccess) {
+      (void)!hipGraphExecDestroy(ge->exec);
+      ge->exec = nullptr;
+      return fail(BPRMF_E_HIP, "sharded step graph upload: %s", hipGetErrorString(eu));
+    }
   }
   HIPCHK(hipGraphLaunch(ge->exec, h->stream));
   return 0;

@@ -78,25 +78,11 @@ static __device__ __forceinline__ float4 hw_sgd(float4 v, float4 g, float lr, fl
                      fmaf(-lr, fmaf(wdf, v.z, g.z), v.z), fmaf(-lr, fmaf(wdf, v.w, g.w), v.w));
 }
 
-// One triplet's slot -> (u, i, j): the sampler spec of k_sample (kernels.hip), lane-parallel.
+// One triplet's slot -> (u, i, j): the device sampler itself (device_common.h sample_slot, the
+// function k_sample and the split builder call), so hogwild's triplets are the same bits.
 static __device__ __forceinline__ void hw_sample(const SamplerArgs& a, uint32_t epoch, uint64_t slot,
                                                  int32_t& u, int32_t& i, int32_t& j, int32_t* err) {
-  const uint64_t N = (uint64_t)a.npos * (uint64_t)a.num_ng;
-  const uint64_t q = permute(slot, N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
-  const int64_t p = div_small(q, (uint32_t)a.num_ng);
-  u = a.pos_u[p];
-  i = a.pos_i[p];
-  const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);
-  const int64_t ul = u / a.world;
-  const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
-  const int64_t free_items = a.item_num - deg;
-  j = -1;
-  if (free_items > 0) {
-    const uint32_t k = bounded_from(d0, q, epoch, (uint32_t)free_items, a.k0, a.k1);
-    j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
-  } else {
-    atomicOr(err, 2);
-  }
+  if (!sample_slot(a, epoch, slot, u, i, j)) atomicOr(err, 2);
 }
 
 constexpr int kHwUnroll = 2;  // triplets per lane group per round (rows in flight per buffer)

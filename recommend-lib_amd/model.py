@@ -39,6 +39,10 @@ def _as_pairs(train_set):
 # (the default); "hogwild" is the opt-in relaxed mode (lock-free per-triplet updates, weight decay
 # still once per row per step; single GPU)
 SEMANTICS = {"exact": 0, "hogwild": 1}
+# how an exact step sums duplicate rows (include/bprmf.h BPRMF_STEP_*): "segmented" = sorted,
+# one writer per row, bitwise reproducible (batch_size <= 8192); "atomic" = f32 atomics, any batch
+# size, the same step up to the order of the fp32 sums
+STEP_MODES = {"segmented": 0, "atomic": 1}
 
 
 class BPRMF:
@@ -49,11 +53,13 @@ class BPRMF:
     `seed` makes init, negative sampling and the epoch shuffle reproducible (the reference is
     unseeded).  `semantics="hogwild"` opts into relaxed synchronisation (not the reference's
     step; faster, nondeterministic; see DESIGN.md §5b for its HR@10 / NDCG@10 against exact).
+    `step="atomic"` sums duplicate rows with f32 atomics instead of the sorted one-writer sums
+    (any batch size; the reference step up to fp32 summation order, not bitwise reproducible).
     """
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, epochs=20, init_std=0.01, seed=0, device=0, rank=0, world=1,
-                 verbose=False, semantics="exact"):
+                 verbose=False, semantics="exact", step="segmented"):
         self.user_num, self.item_num = int(user_num), int(item_num)
         self.factor_num = int(factor_num)
         self.lr, self.wd = float(lr), float(wd)
@@ -64,6 +70,9 @@ class BPRMF:
         if semantics not in SEMANTICS:
             raise ValueError(f"semantics must be one of {sorted(SEMANTICS)}")
         self.semantics = semantics
+        if step not in STEP_MODES:
+            raise ValueError(f"step must be one of {sorted(STEP_MODES)}")
+        self.step_mode = step
         self.epoch = 0
         self.history = []
         L = _lib.load()
@@ -71,7 +80,8 @@ class BPRMF:
                           factor_num=self.factor_num, lr=self.lr, weight_decay=self.wd,
                           batch_size=self.batch_size, num_ng=self.num_ng, init_std=float(init_std),
                           seed=self.seed & (2**64 - 1), device=self.device, rank=self.rank,
-                          world=self.world, semantics=SEMANTICS[semantics])
+                          world=self.world, semantics=SEMANTICS[semantics],
+                          step_mode=STEP_MODES[step])
         h = ctypes.c_void_p()
         _lib.check(L.bprmf_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

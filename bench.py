@@ -121,9 +121,11 @@ def main():
     ap.add_argument("--python-orchestration", action="store_true",
                     help="sharded: per-step Python orchestration over torch.distributed instead of "
                          "the library's runner")
-    ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild"],
+    ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild", "local"],
                     help="exact: the reference's batch-synchronous step (default, the headline); "
                          "hogwild: opt-in relaxed synchronisation (a separate, labelled line)")
+    ap.add_argument("--local-steps", type=int, default=0,
+                    help="--semantics local: steps between the XCD replicas' merges (0: 16)")
     ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
                     help="exact step's duplicate-row sums: segmented (sorted, one writer per row, "
                          "bitwise reproducible; the headline) or atomic (f32 atomics; a labelled line)")
@@ -144,7 +146,7 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     sharded = world > 1 or a.sharded
-    hog = a.semantics == "hogwild"
+    hog = a.semantics in ("hogwild", "local")
     if hog and sharded:
         raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
     if a.step == "atomic" and (sharded or hog):
@@ -163,7 +165,7 @@ def main():
     pos = syn.make_positives(U, I, a.positives, a.seed)
     if not sharded:
         m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed, device=local,
-                     semantics=a.semantics, step=a.step)
+                     semantics=a.semantics, step=a.step, local_steps=a.local_steps)
         m.set_train(pos)
         n_steps = m.epoch_size()[1]
 
@@ -234,6 +236,10 @@ def main():
             elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
+            elif "step_graph" in us and a.semantics == "local":  # periods: k_hogwild + k_local_merge
+                step_us, what = us["step_graph"], ("k_hogwild<LOCAL> (in-kernel sampling + gather + dots "
+                                                   "+ sigmoid + SGD scatter, hot items in per-XCD replicas) "
+                                                   "+ k_local_merge every period")
             elif "step_graph" in us and hog:  # one k_hogwild launch per chunk
                 step_us, what = us["step_graph"], ("k_hogwild (in-kernel sampling + gather + dots + "
                                                    "sigmoid + SGD scatter, one launch per chunk)")
@@ -250,7 +256,8 @@ def main():
             # PMC bytes only for the kernel they were counted on: the single-GPU fused step (or
             # the hogwild kernel); a sharded line (world > 1) gets them only from an entry measured
             # on the sharded kernels themselves, keyed by world size
-            tkey = f"ml20m_d{d}_B{B}" + ("_hogwild" if hog else "") + ("_atomic" if a.step == "atomic" else "")
+            tkey = (f"ml20m_d{d}_B{B}" + (f"_{a.semantics}" if hog else "")
+                    + ("_atomic" if a.step == "atomic" else ""))
             if sharded and not (world == 1 and not a.python_orchestration):
                 tkey = f"sharded_w{world}_ml20m_d{d}_B{B}"
             traffic, tsrc = load_traffic(tkey) if (U, I) == (U_ML20M, I_ML20M) else (None, None)
@@ -287,6 +294,7 @@ def main():
                "data": "synthetic ml-20m-shaped positives (lognormal user degree, Zipf items), "
                        "random N(0,0.01^2) init; no dataset download",
                "config": {"workload": "BPR-MF training, ml-20m shape", "users": U, "items": I,
+                          **({"local_steps": a.local_steps or 16} if a.semantics == "local" else {}),
                           "positives": int(len(pos)), "factor_num": d, "batch_size_per_gpu": B,
                           "global_batch": B * world, "num_ng": 4, "lr": 0.01, "wd": 0.001,
                           "parallelism": (f"users+items row-sharded x{world}, "
@@ -294,7 +302,10 @@ def main():
                                           if sharded else "single GPU"),
                           "semantics": ("relaxed (hogwild: per-triplet lock-free updates, weight decay "
                                         "once per row per step, staleness bounded by the launch's "
-                                        "in-flight window; NOT the reference step)" if hog else
+                                        "in-flight window; NOT the reference step)" if a.semantics == "hogwild" else
+                                        "relaxed (local: hogwild for users and cold items, the hot items "
+                                        "in one replica per XCD merged every local_steps steps; NOT the "
+                                        "reference step)" if a.semantics == "local" else
                                         "exact batch-synchronous SGD (reference step), lazy weight decay, "
                                         "duplicate rows summed by f32 atomics (not bitwise reproducible)"
                                         if a.step == "atomic" else

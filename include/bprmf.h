@@ -41,7 +41,13 @@ typedef enum {
  * each triplet is applied on its own as soon as its rows arrive, lock-free (concurrent updates
  * of a row may overwrite each other), weight decay still once per row per step; staleness is
  * bounded by the launch's in-flight window.  Single-GPU handles only. */
-enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1 };
+enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
+/* LOCAL (bounded staleness, opt-in): HOGWILD for users and for all but the most popular items;
+ * the hot items (the top min(I, 4096) by positive count) are trained in one replica per XCD of the
+ * GPU (each XCD's waves see their own XCD's updates at once, the other XCDs' only at the next
+ * merge), and every `local_steps` steps (default 16) the replicas are merged: new = decayed base +
+ * sum over XCDs of each replica's change.  Staleness across XCDs is bounded by `local_steps`
+ * steps; single-GPU handles only. */
 
 /* How an EXACT step sums duplicate rows' gradients ("ship both").  SEGMENTED: the
  * batch is sorted by user and by item and every row is summed by one writer in a fixed order,
@@ -67,7 +73,8 @@ typedef struct {
   int32_t semantics;    /* BPRMF_SEM_EXACT (0, default): the reference's batch-synchronous step;
                            BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
   int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
-  int32_t reserved[2];
+  int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 16) */
+  int32_t reserved[1];
 } bprmf_config;
 
 typedef struct {

@@ -126,6 +126,73 @@ def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
     return loss, sP, sQ
 
 
+def local_serial(P, Q, u, i, j, lr, wd, B, hot, period, t0=0):
+    """The opt-in bounded-staleness mode (semantics "local", csrc/hogwild.hip LOCAL + k_local_merge)
+    run serially on ONE XCD (its SERIAL test build: one lane group, slot order, so one replica
+    changes): the spec that build must reproduce.  NOT the reference step.
+      users and cold items: exactly hogwild_serial's rule (stamps, per-step weight decay);
+      hot items (`hot`: item ids): read and written in the XCD's replica, which starts each period
+      equal to the base row b0 (current at the period's first step t_a); a replica update is
+      W - lr g (no weight-decay term, no stamp);
+      a period ends every `period` steps and at the end of the slots: the base row becomes
+      fma(b0, (1 - lr wd)^(t_b - t_a), replica - b0) (the other XCDs' replicas add exactly 0),
+      current at t_b, and the replica restarts from it.
+    In place on float32 P, Q.  Returns (loss, sP, sQ)."""
+    sP = np.full(P.shape[0], t0, np.int64)
+    sQ = np.full(Q.shape[0], t0, np.int64)
+    hot = set(int(x) for x in hot)
+    log2a = math.log2(1.0 - float(lr) * float(wd))
+    lr32, wd32 = np.float32(lr), np.float32(wd)
+
+    def dec(k):
+        return np.float32(2.0 ** np.float32(k * log2a)) if k > 0 else np.float32(1)
+
+    def bring(W, st, r, t):
+        if st[r] < t:
+            return (W[r] * dec(t - 1 - st[r])).astype(np.float32), True
+        return W[r].copy(), False
+
+    rep = {h: Q[h].copy() for h in hot}  # base rows current at t0 (stamps t0)
+    t_a = t0
+    loss = 0.0
+    n = len(u)
+    for s in range(n):
+        t = t0 + 1 + s // B
+        uu, ii, jj = int(u[s]), int(i[s]), int(j[s])
+        pu, fu = bring(P, sP, uu, t)
+        vi, fi = (rep[ii].copy(), False) if ii in hot else bring(Q, sQ, ii, t)
+        vj, fj = (rep[jj].copy(), False) if jj in hot else bring(Q, sQ, jj, t)
+        x = np.float32(np.dot(pu.astype(np.float64), vi.astype(np.float64)) -
+                       np.dot(pu.astype(np.float64), vj.astype(np.float64)))
+        c = np.float32(1.0) / (np.float32(1.0) + np.float32(np.exp(np.float64(x))))
+        loss += float(np.logaddexp(0.0, -float(x)))
+        gu, gi, gj = -c * (vi - vj), -c * pu, c * pu
+        P[uu] = pu - lr32 * (gu + (wd32 if fu else np.float32(0)) * pu)
+        if fu:
+            sP[uu] = t
+        upd = [(ii, vi, gi + gj, fi)] if ii == jj else [(ii, vi, gi, fi), (jj, vj, gj, fj)]
+        for r, v, g, f in upd:
+            new = v - lr32 * (g + (wd32 if f else np.float32(0)) * v)
+            if r in hot:
+                rep[r] = new
+            else:
+                Q[r] = new
+                if f:
+                    sQ[r] = t
+        last = s + 1 == n
+        if last or ((s + 1) % B == 0 and t - t_a >= period):
+            t_b = t
+            fk = dec(t_b - t_a)
+            for h in hot:
+                b0 = Q[h].copy()  # stamp t_a
+                Q[h] = (b0.astype(np.float64) * np.float64(fk) +
+                        (rep[h] - b0).astype(np.float64)).astype(np.float32)
+                sQ[h] = t_b
+                rep[h] = Q[h].copy()
+            t_a = t_b
+    return loss, sP, sQ
+
+
 # ----------------------------------------------------------------------------------------------
 # 2. sampler specification (bit-exact target for the HIP sampler)
 # ----------------------------------------------------------------------------------------------

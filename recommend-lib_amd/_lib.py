@@ -26,7 +26,8 @@ class Config(ctypes.Structure):
                 ("num_ng", ctypes.c_int32), ("init_std", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("device", ctypes.c_int32), ("rank", ctypes.c_int32),
                 ("world", ctypes.c_int32), ("semantics", ctypes.c_int32),
-                ("step_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2)]
+                ("step_mode", ctypes.c_int32), ("local_steps", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 1)]
 
 
 class NcfConfig(ctypes.Structure):  # ncf_config, include/ncf.h

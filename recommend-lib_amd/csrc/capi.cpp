@@ -96,10 +96,12 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_INVALID, "lr, weight_decay and init_std must be >= 0");
   Geom g;
   if (!make_geom(cfg->factor_num, &g)) return fail(BPRMF_E_UNSUPPORTED, "factor_num must be in [1, 1024]");
-  if (cfg->semantics != BPRMF_SEM_EXACT && cfg->semantics != BPRMF_SEM_HOGWILD)
-    return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0) or BPRMF_SEM_HOGWILD (1)");
-  if (cfg->semantics == BPRMF_SEM_HOGWILD && cfg->world != 1)
-    return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
+  if (cfg->semantics != BPRMF_SEM_EXACT && cfg->semantics != BPRMF_SEM_HOGWILD &&
+      cfg->semantics != BPRMF_SEM_LOCAL)
+    return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0), _HOGWILD (1) or _LOCAL (2)");
+  if (cfg->semantics != BPRMF_SEM_EXACT && cfg->world != 1)
+    return fail(BPRMF_E_UNSUPPORTED, "relaxed semantics: single-GPU handles only");
+  if (cfg->local_steps < 0) return fail(BPRMF_E_INVALID, "local_steps must be >= 0");
   if (cfg->step_mode != BPRMF_STEP_SEGMENTED && cfg->step_mode != BPRMF_STEP_ATOMIC)
     return fail(BPRMF_E_INVALID, "step_mode must be BPRMF_STEP_SEGMENTED (0) or BPRMF_STEP_ATOMIC (1)");
   if (cfg->step_mode == BPRMF_STEP_ATOMIC && cfg->world != 1)
@@ -107,6 +109,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   auto* h = new bprmf_handle();
   h->cfg = *cfg;
   h->semantics = cfg->semantics;
+  if (cfg->local_steps > 0) h->local_steps = cfg->local_steps;
   h->geom = g;
   h->hp.lr = cfg->lr;
   h->hp.wd = cfg->weight_decay;
@@ -192,7 +195,7 @@ int bprmf_destroy(bprmf_handle* h) {
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p};
+                  h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -236,6 +239,44 @@ int bprmf_row_stride(bprmf_handle* h, int32_t* ld) {
   return 0;
 }
 
+// semantics LOCAL: the hot items (the most frequent positives; BPRMF_LOCAL_HOT overrides how many)
+// get one replica row per XCD, filled from the base table (a refresh merge at the current step)
+static int local_refresh(bprmf_handle* h) {
+  if (!h->d_qrep) return 0;
+  LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->t, h->t, true, h->stream));
+  h->rep_t = h->t;
+  return 0;
+}
+
+static int local_setup(bprmf_handle* h, const std::vector<int32_t>& pos_items) {
+  const int64_t I = h->I;
+  int64_t H = std::min<int64_t>(4096, std::max<int64_t>(1, I / 4));
+  if (const char* e = getenv("BPRMF_LOCAL_HOT")) H = std::max<int64_t>(0, std::min<int64_t>(I, atoll(e)));
+  std::vector<int64_t> cnt(I, 0);
+  for (int32_t i : pos_items) ++cnt[i];
+  std::vector<int32_t> order(I);
+  for (int64_t i = 0; i < I; ++i) order[i] = (int32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
+  std::vector<int32_t> hot(I, -1), rows(std::max<int64_t>(H, 1));
+  for (int64_t k = 0; k < H; ++k) {
+    rows[k] = order[k];
+    hot[order[k]] = (int32_t)k;
+  }
+  const size_t rep_bytes = sizeof(float) * (size_t)kLocalXcds * H * h->geom.ld;
+  for (void* p : {(void*)h->d_hot, (void*)h->d_hot_rows, (void*)h->d_qrep})
+    if (p) HIPCHK(hipFree(p));
+  h->d_hot = h->d_hot_rows = nullptr;
+  h->d_qrep = nullptr;
+  h->hot_H = H;
+  if (int r = dalloc(&h->d_hot, I)) return r;
+  if (int r = dalloc(&h->d_hot_rows, std::max<int64_t>(H, 1))) return r;
+  if (H > 0) HIPCHK(hipMalloc((void**)&h->d_qrep, rep_bytes));
+  HIPCHK(hipMemcpy(h->d_hot, hot.data(), 4 * I, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_hot_rows, rows.data(), 4 * rows.size(), hipMemcpyHostToDevice));
+  return local_refresh(h);
+}
+
 int bprmf_set_train(bprmf_handle* h, const int32_t* users, const int32_t* items, int64_t nnz) {
   return bprmf_set_train_ex(h, users, items, nnz, nullptr, nullptr, 0);
 }
@@ -271,6 +312,8 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   if (!indices.empty())
     HIPCHK(hipMemcpy(h->d_indices, indices.data(), 4 * indices.size(), hipMemcpyHostToDevice));
   h->npos = n;
+  if (h->semantics == BPRMF_SEM_LOCAL)
+    if (int r = local_setup(h, pi)) return r;
   const uint64_t N = (uint64_t)n * (uint64_t)h->cfg.num_ng;
   feistel_dims(N, &h->feistel_a, &h->feistel_c);
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
@@ -642,6 +685,39 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   const int64_t B = h->cfg.batch_size;
   const int64_t nb = (n + B - 1) / B;
   if ((int64_t)h->t + nb >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  if (h->semantics == BPRMF_SEM_LOCAL) {
+    // periods of local_steps steps: one hogwild launch (hot items in the XCD replicas), then the
+    // merge; the call's last period is merged too, so the base table is current when it returns
+    if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
+    const SamplerArgs sa = sampler_args(h);
+    const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+    hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
+    if (ea) HIPCHK(hipEventRecord(ea, h->stream));
+    for (int64_t s0 = 0; s0 < n;) {
+      const int64_t left = h->local_steps - (h->t - h->rep_t);  // steps left in this period
+      const int64_t m = std::min<int64_t>(n - s0, std::max<int64_t>(1, left) * B);
+      const int64_t mb = (m + B - 1) / B;
+      HIPCHK(hogwild(h->geom, ru ? nullptr : &sa, epoch, first_slot + s0, ru ? ru + s0 : nullptr,
+                     ri ? ri + s0 : nullptr, rj ? rj + s0 : nullptr, m, h->P, h->Q, h->hp, h->t, (int)B,
+                     h->d_loss, h->d_err, h->stream, la.H > 0 ? &la : nullptr));
+      h->t += (int32_t)mb;
+      *steps_done += mb;
+      s0 += m;
+      if (la.H > 0 && (h->t - h->rep_t >= h->local_steps || s0 >= n)) {
+        HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
+        h->rep_t = h->t;
+      }
+    }
+    if (ea) {
+      hipEvent_t eb = prof_event(h);
+      if (eb) {
+        HIPCHK(hipEventRecord(eb, h->stream));
+        h->prof_rec[BPRMF_KPROF_STEPS].push_back({ea, eb});
+        h->prof_weight[BPRMF_KPROF_STEPS] += nb - 1;
+      }
+    }
+    return 0;
+  }
   if (h->semantics == BPRMF_SEM_HOGWILD) {
     // one launch for the chunk: triplets sampled in the kernel (or replayed), each applied on its
     // own (hogwild.hip); the loss goes to the segmented path's kSegLossSlots slots
@@ -903,7 +979,7 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   std::vector<int32_t> st(std::max(h->U, h->I), h->t);
   if (h->U) HIPCHK(hipMemcpy(h->P.stamp, st.data(), 4 * h->U, hipMemcpyHostToDevice));
   if (h->I) HIPCHK(hipMemcpy(h->Q.stamp, st.data(), 4 * h->I, hipMemcpyHostToDevice));
-  return 0;
+  return local_refresh(h);  // LOCAL: the replicas start from the new rows
 }
 
 int bprmf_get_weights(bprmf_handle* h, float* P, float* Q) {

@@ -62,7 +62,14 @@ struct bprmf_handle {
   float* d_xloss = nullptr;    // [2][B] x per triplet (K1 -> K2's loss workgroups)
   int32_t* d_pend_q = nullptr;  // [2][I] step that last marked an item row (fused step)
   int32_t* d_pend_p = nullptr;  // [2][U] the same for user rows K2 finishes
-  int32_t semantics = BPRMF_SEM_EXACT;  // cfg.semantics (BPRMF_SEM_HOGWILD: hogwild.hip)
+  int32_t semantics = BPRMF_SEM_EXACT;  // cfg.semantics (BPRMF_SEM_HOGWILD / LOCAL: hogwild.hip)
+  // BPRMF_SEM_LOCAL: the hot items' per-XCD replicas (hogwild.hip k_local_merge)
+  int32_t* d_hot = nullptr;       // [I] replica slot of an item, -1 = cold
+  int32_t* d_hot_rows = nullptr;  // [H] item of each slot
+  float* d_qrep = nullptr;        // [kLocalXcds][H][ld]
+  int64_t hot_H = 0;
+  int32_t rep_t = 0;              // the step every replica row is current at (the last merge)
+  int32_t local_steps = 16;       // steps per period (cfg.local_steps)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan

@@ -92,14 +92,25 @@ template <int S, int UNR>
 struct HwRound {
   float4 pu[UNR][S], vi[UNR][S], vj[UNR][S];
   int32_t su[UNR], si[UNR], sj[UNR], uu[UNR], ii[UNR], jj[UNR];
+  int32_t hi[UNR], hj[UNR];  // LOCAL: the items' replica slots (-1: cold, the shared table)
   bool ok[UNR];
 };
 
+// semantics "local" (kernels.h LocalArgs): the hot items' rows live in one replica
+// per XCD, rep + (xcc * H + slot) * ld, written back (plain stores: the line stays in the XCD's L2,
+// where every wave of that XCD reads it with nt loads); hot[item] = slot or -1
+// this wave's XCD (0-7): which replica it trains (read, not assumed: any placement is correct)
+static __device__ __forceinline__ int hw_xcc() {
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7;  // hwreg(HW_REG_XCC_ID, 0, 4)
+}
+
 // issue the round starting at slot k0 of the wave's chunk (ids from the lanes that sampled them)
-template <int G4, int S, int UNR, int GPW, bool SERIAL>
+template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
 static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
                                                int32_t mi, int32_t mj, const Table& P,
-                                               const Table& Q, int ld, int sub, int gw, int fl) {
+                                               const Table& Q, int ld, int sub, int gw, int fl,
+                                               int32_t mhi = -1, int32_t mhj = -1,
+                                               const float* repx = nullptr) {
   const bool nt = fl & 1, noload = fl & 2;
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
@@ -107,11 +118,13 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
     R.uu[r] = __shfl(mu, src & 63);
     R.ii[r] = __shfl(mi, src & 63);
     R.jj[r] = __shfl(mj, src & 63);
+    R.hi[r] = LOCAL ? __shfl(mhi, src & 63) : -1;
+    R.hj[r] = LOCAL ? __shfl(mhj, src & 63) : -1;
     R.ok[r] = (SERIAL ? gw == 0 : true) && src < cnt && R.uu[r] >= 0;
     if (R.ok[r] && !noload) {
       const float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
-      const float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
-      const float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
+      const float* qi = (LOCAL && R.hi[r] >= 0 ? repx + (int64_t)R.hi[r] * ld : Q.W + (int64_t)R.ii[r] * ld) + 4 * sub;
+      const float* qj = (LOCAL && R.hj[r] >= 0 ? repx + (int64_t)R.hj[r] * ld : Q.W + (int64_t)R.jj[r] * ld) + 4 * sub;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         if (nt) {
@@ -125,8 +138,10 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
         }
       }
       R.su[r] = hw_ld_word(P.stamp + R.uu[r]);
-      R.si[r] = hw_ld_word(Q.stamp + R.ii[r]);
-      R.sj[r] = hw_ld_word(Q.stamp + R.jj[r]);
+      // a replica row has no stamp: it is current within its period (the merge applies the
+      // period's weight decay), so it reads as "already at this step"
+      R.si[r] = LOCAL && R.hi[r] >= 0 ? INT32_MAX : hw_ld_word(Q.stamp + R.ii[r]);
+      R.sj[r] = LOCAL && R.hj[r] >= 0 ? INT32_MAX : hw_ld_word(Q.stamp + R.jj[r]);
     } else {
       R.su[r] = R.si[r] = R.sj[r] = 0;
 #pragma unroll
@@ -136,11 +151,11 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
 }
 
 // compute and store the round at slot k0 (slot base + k0 + ... of step t0 + 1 + slot / B)
-template <int G4, int S, int UNR, int GPW, bool SERIAL>
+template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
 static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base, int k0,
                                                 const Table& P, const Table& Q, const Hyper& hp,
                                                 int ld, int32_t t0, int B, int sub, int gw,
-                                                float& lacc, int fl) {
+                                                float& lacc, int fl, float* repx = nullptr) {
   const float lr = hp.lr, wd = hp.wd;
   const bool nostore = fl & 4;
   const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
@@ -175,8 +190,9 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
     if (sub == 0) lacc += softplus(-x);       // -log sigmoid(x)
     float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
-    float* qi = Q.W + (int64_t)R.ii[r] * ld + 4 * sub;
-    float* qj = Q.W + (int64_t)R.jj[r] * ld + 4 * sub;
+    const bool hoti = LOCAL && R.hi[r] >= 0, hotj = LOCAL && R.hj[r] >= 0;
+    float* qi = (hoti ? repx + (int64_t)R.hi[r] * ld : Q.W + (int64_t)R.ii[r] * ld) + 4 * sub;
+    float* qj = (hotj ? repx + (int64_t)R.hj[r] * ld : Q.W + (int64_t)R.jj[r] * ld) + 4 * sub;
     const bool same = R.ii[r] == R.jj[r];  // i == j: one row, both gradients (stored once, as i)
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -199,8 +215,15 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
       else if (!nousers)
         hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
       if (!noitems) {
-        hw_st4(qi + 4 * G4 * k, hw_sgd(vi, gi, lr, fi1 ? wd : 0.f));
-        if (!same) hw_st4(qj + 4 * G4 * k, hw_sgd(vj, gj, lr, fj1 ? wd : 0.f));
+        // replica rows: written back into this XCD's L2 (plain stores), no weight-decay term
+        // (their stamps read INT32_MAX: fi1 / fj1 false); shared rows: write-through, as hogwild
+        const float4 ni = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f), nj = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
+        if (hoti) *reinterpret_cast<float4*>(qi + 4 * G4 * k) = ni;
+        else hw_st4(qi + 4 * G4 * k, ni);
+        if (!same) {
+          if (hotj) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = nj;
+          else hw_st4(qj + 4 * G4 * k, nj);
+        }
       }
     }
     if (sub == 0) {
@@ -220,14 +243,14 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
 // Rounds are double-buffered: round k+1's loads are issued BEFORE round k's stores, so waiting
 // for them does not wait for round k's write-through acknowledgements (gfx9 counts stores in
 // vmcnt, in order with the loads).
-template <int G4, int S, bool SAMPLE, bool SERIAL>
+template <int G4, int S, bool SAMPLE, bool SERIAL, bool LOCAL = false>
 __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoch, int64_t slot0,
                                                     const int32_t* __restrict__ tu,
                                                     const int32_t* __restrict__ ti,
                                                     const int32_t* __restrict__ tj, int64_t n,
                                                     Table P, Table Q, Hyper hp, int ld, int32_t t0,
                                                     int B, int tpw, int fl, double* __restrict__ loss,
-                                                    int32_t* __restrict__ err) {
+                                                    int32_t* __restrict__ err, LocalArgs la = LocalArgs{}) {
   constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round and unroll step
   constexpr int UNR = SERIAL ? 1 : kHwUnroll;
   constexpr int STEP = GPW * UNR;
@@ -237,9 +260,10 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
   const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
   float lacc = 0.f;
+  float* repx = LOCAL ? la.rep + (int64_t)hw_xcc() * la.H * ld : nullptr;  // this XCD's replica
   for (int64_t base = wave * tpw; base < n; base += nwaves * tpw) {
     const int cnt = (int)min<int64_t>(tpw, n - base);
-    int32_t mu = 0, mi = 0, mj = 0;
+    int32_t mu = 0, mi = 0, mj = 0, mhi = -1, mhj = -1;
     if (lane < cnt) {
       const int64_t s = base + lane;
       if (SAMPLE) {
@@ -254,24 +278,32 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
       if (mu < 0 || mu >= P.rows || mi < 0 || mi >= Q.rows || mj < 0 || mj >= Q.rows) {
         if (mj >= 0 || !SAMPLE) atomicOr(err, 1);
         mu = -1;
+      } else if (LOCAL) {  // the items' replica slots, looked up once by the sampling lane
+        mhi = la.hot[mi];
+        mhj = la.hot[mj];
       }
     }
     HwRound<S, UNR> A, Bf;
     if (SERIAL) {  // each triplet reads what the one before it stored: no prefetch
       for (int k0 = 0; k0 < cnt; k0 += STEP) {
-        hw_load<G4, S, UNR, GPW, SERIAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
-        hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi, mhj, repx);
+        hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl, repx);
       }
       continue;
     }
-    hw_load<G4, S, UNR, GPW, SERIAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
+    hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi, mhj, repx);
     for (int k0 = 0; k0 < cnt; k0 += 2 * STEP) {
       const bool more1 = k0 + STEP < cnt, more2 = k0 + 2 * STEP < cnt;
-      if (more1) hw_load<G4, S, UNR, GPW, SERIAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
-      hw_apply<G4, S, UNR, GPW, SERIAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
+      if (more1)
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi,
+                                                mhj, repx);
+      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl, repx);
       if (!more1) break;
-      if (more2) hw_load<G4, S, UNR, GPW, SERIAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl);
-      hw_apply<G4, S, UNR, GPW, SERIAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc, fl);
+      if (more2)
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl,
+                                                mhi, mhj, repx);
+      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc, fl,
+                                               repx);
     }
   }
   // the wave's loss into one of kSegLossSlots f64 slots (no-return atomics; order is not fixed,
@@ -281,6 +313,66 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
     for (int off = 32; off > 0; off >>= 1) lacc += __shfl_xor(lacc, off);
     if (lane == 0 && lacc != 0.f) atomicAdd(&loss[wave & (kSegLossSlots - 1)], (double)lacc);
   }
+}
+
+// LOCAL: end of a period (steps t0+1 .. t1): each hot item's new row is its value at t0 (the
+// replicas' common starting value), decayed over the period as torch's SGD decays every row every
+// step, plus each XCD's change to it, added in XCD order 0..7 (a fixed order); the base row takes
+// it with stamp t1 and every replica starts the next period from it.  refresh: no replica
+// changes (they are reset from the base; after set_weights / a flush).  One lane group per row.
+template <int G4, int S>
+__global__ __launch_bounds__(kBlock) void k_local_merge(Table Q, LocalArgs la,
+                                                        const int32_t* __restrict__ rows, Hyper hp,
+                                                        int ld, int32_t t0, int32_t t1, int refresh) {
+  const int sub = threadIdx.x & (G4 - 1);
+  const int64_t h = blockIdx.x * (int64_t)(kBlock / G4) + threadIdx.x / G4;
+  if (h >= la.H) return;
+  const int32_t item = rows[h];
+  float* w = Q.W + (int64_t)item * ld + 4 * sub;
+  const int32_t st = Q.stamp[item];
+  const float f0 = decay_pow(hp.log2a, t0 - st);  // the base at t0
+  const float fk = decay_pow(hp.log2a, t1 - t0);  // the period's weight decay
+  float4 b0[S], acc[S], rv[kLocalXcds][S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(w + 4 * G4 * k);
+    b0[k] = make_float4(v.x * f0, v.y * f0, v.z * f0, v.w * f0);
+    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (!refresh) {
+#pragma unroll
+    for (int x = 0; x < kLocalXcds; ++x) {  // every replica's row in flight at once
+      const float* r = la.rep + ((int64_t)x * la.H + h) * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) rv[x][k] = *reinterpret_cast<const float4*>(r + 4 * G4 * k);
+    }
+#pragma unroll
+    for (int x = 0; x < kLocalXcds; ++x)
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        acc[k] = make_float4(acc[k].x + (rv[x][k].x - b0[k].x), acc[k].y + (rv[x][k].y - b0[k].y),
+                             acc[k].z + (rv[x][k].z - b0[k].z), acc[k].w + (rv[x][k].w - b0[k].w));
+  }
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const float4 nv = make_float4(fmaf(b0[k].x, fk, acc[k].x), fmaf(b0[k].y, fk, acc[k].y),
+                                  fmaf(b0[k].z, fk, acc[k].z), fmaf(b0[k].w, fk, acc[k].w));
+    *reinterpret_cast<float4*>(w + 4 * G4 * k) = nv;
+#pragma unroll
+    for (int x = 0; x < kLocalXcds; ++x)
+      *reinterpret_cast<float4*>(la.rep + ((int64_t)x * la.H + h) * ld + 4 * sub + 4 * G4 * k) = nv;
+  }
+  if (sub == 0) Q.stamp[item] = t1;
+}
+
+hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_t* rows,
+                       const Hyper& hp, int32_t t0, int32_t t1, bool refresh, hipStream_t s) {
+  if (la.H <= 0) return hipSuccess;
+  BPRMF_DISPATCH4(g, ({
+    const unsigned blocks = (unsigned)((la.H + kBlock / G4_ - 1) / (kBlock / G4_));
+    k_local_merge<G4_, S_><<<blocks, kBlock, 0, s>>>(Q, la, rows, hp, g.ld, t0, t1, refresh ? 1 : 0);
+  }));
+  return hipGetLastError();
 }
 
 static bool hw_serial() {
@@ -303,7 +395,7 @@ static int hw_tpw(int64_t n) {
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
                    Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
-                   hipStream_t s) {
+                   hipStream_t s, const LocalArgs* lap) {
   if (n <= 0) return hipSuccess;
   const bool serial = hw_serial();
   const int tpw = serial ? 64 : hw_tpw(n);
@@ -337,6 +429,24 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 126);
   SamplerArgs a{};
   if (sa) a = *sa;
+  if (lap) {  // semantics "local": the hot items in per-XCD replicas
+    const LocalArgs la = *lap;
+    BPRMF_DISPATCH4(g, ({
+      if (serial && sa)
+        k_hogwild<G4_, S_, true, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
+                                                                  hp, g.ld, t0, B, tpw, fl, loss, err, la);
+      else if (serial)
+        k_hogwild<G4_, S_, false, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
+                                                                   hp, g.ld, t0, B, tpw, fl, loss, err, la);
+      else if (sa)
+        k_hogwild<G4_, S_, true, false, true><<<(unsigned)blocks, threads, 0, s>>>(
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la);
+      else
+        k_hogwild<G4_, S_, false, false, true><<<(unsigned)blocks, threads, 0, s>>>(
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la);
+    }));
+    return hipGetLastError();
+  }
   BPRMF_DISPATCH4(g, ({
     if (serial && sa)
       k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,

@@ -236,10 +236,22 @@ int item_long_blocks(int B);
 // relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
 // sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s
 // belongs to step t0 + 1 + s / B; loss into kSegLossSlots slots
+struct LocalArgs;
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
                    Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
-                   hipStream_t s);
+                   hipStream_t s, const LocalArgs* la = nullptr);
+// semantics "local" (hogwild.hip): the hot items' rows in one replica per XCD
+// (rep [8][H][ld]; hot[item] = replica slot or -1), merged every period: the base row (stamp
+// t0) decayed to t1 plus every replica's change, then copied back into the replicas
+struct LocalArgs {
+  const int32_t* hot = nullptr;
+  float* rep = nullptr;
+  int64_t H = 0;
+};
+constexpr int kLocalXcds = 8;
+hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_t* rows,
+                       const Hyper& hp, int32_t t0, int32_t t1, bool refresh, hipStream_t s);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

@@ -37,8 +37,9 @@ def _as_pairs(train_set):
 
 # step semantics (include/bprmf.h BPRMF_SEM_*): "exact" is the reference's batch-synchronous SGD
 # (the default); "hogwild" is the opt-in relaxed mode (lock-free per-triplet updates, weight decay
-# still once per row per step; single GPU)
-SEMANTICS = {"exact": 0, "hogwild": 1}
+# still once per row per step; single GPU); "local" is hogwild with the hot items
+# in per-XCD replicas merged every local_steps steps
+SEMANTICS = {"exact": 0, "hogwild": 1, "local": 2}
 # how an exact step sums duplicate rows (include/bprmf.h BPRMF_STEP_*): "segmented" = sorted,
 # one writer per row, bitwise reproducible (batch_size <= 8192); "atomic" = f32 atomics, any batch
 # size, the same step up to the order of the fp32 sums
@@ -53,13 +54,15 @@ class BPRMF:
     `seed` makes init, negative sampling and the epoch shuffle reproducible (the reference is
     unseeded).  `semantics="hogwild"` opts into relaxed synchronisation (not the reference's
     step; faster, nondeterministic; see DESIGN.md §5b for its HR@10 / NDCG@10 against exact).
+    `semantics="local"`: hogwild for users and cold items, the hot items trained in one replica
+    per XCD and merged every `local_steps` steps (default 16; bounded staleness).
     `step="atomic"` sums duplicate rows with f32 atomics instead of the sorted one-writer sums
     (any batch size; the reference step up to fp32 summation order, not bitwise reproducible).
     """
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, epochs=20, init_std=0.01, seed=0, device=0, rank=0, world=1,
-                 verbose=False, semantics="exact", step="segmented"):
+                 verbose=False, semantics="exact", step="segmented", local_steps=0):
         self.user_num, self.item_num = int(user_num), int(item_num)
         self.factor_num = int(factor_num)
         self.lr, self.wd = float(lr), float(wd)
@@ -81,7 +84,7 @@ class BPRMF:
                           batch_size=self.batch_size, num_ng=self.num_ng, init_std=float(init_std),
                           seed=self.seed & (2**64 - 1), device=self.device, rank=self.rank,
                           world=self.world, semantics=SEMANTICS[semantics],
-                          step_mode=STEP_MODES[step])
+                          step_mode=STEP_MODES[step], local_steps=int(local_steps))
         h = ctypes.c_void_p()
         _lib.check(L.bprmf_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

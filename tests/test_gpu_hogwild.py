@@ -131,3 +131,104 @@ def test_hogwild_rejects_sharded_handles(rl):
         rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="hogwild")
     with pytest.raises(ValueError):
         rl.BPRMF(10, 10, 8, semantics="bogus")
+
+
+# ---- semantics "local": hot items in per-XCD replicas, merged every local_steps steps ----------
+def _hot_positives(U, I, hot_items, g):
+    """Positives whose most frequent items are `hot_items` (in that order of frequency)."""
+    rows = []
+    for k, it in enumerate(hot_items):
+        for uu in range(U - k):  # item hot_items[k] has U - k positives
+            rows.append((uu, it))
+    for uu in range(U):
+        rows.append((uu, int(g.integers(len(hot_items), I))))
+    return np.unique(np.array(rows, np.int64), axis=0)
+
+
+@pytest.mark.parametrize("d,B,period", [(8, 16, 3), (32, 64, 2), (128, 32, 5)])
+def test_local_serial_replay_matches_oracle(rl, monkeypatch, d, B, period):
+    """The SERIAL build (one lane group on one XCD, slot order) against oracle/bpr_oracle.py:
+    local_serial: hogwild's rule for users and cold items, the hot items in the XCD's replica
+    (no weight-decay term inside a period) and the merge every `period` steps and at the call's
+    end (decayed base + the replica's change)."""
+    monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
+    monkeypatch.setenv("BPRMF_LOCAL_HOT", "6")
+    g = np.random.default_rng(d + period)
+    U, I, n = 23, 31, 300
+    hot = [4, 9, 0, 17, 22, 30]
+    pos = _hot_positives(U, I, hot, g)
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    u, i, j = g.integers(0, U, n), g.integers(0, I, n), g.integers(0, I, n)
+    i[::3] = 4       # hot items often
+    j[1::5] = 9
+    j[:7] = i[:7]    # i == j (hot and cold)
+    u[10:40] = 3
+    m = rl.BPRMF(U, I, d, lr=0.05, wd=0.01, batch_size=B, semantics="local", local_steps=period)
+    m.set_train(pos)  # the hot set: the 6 most frequent positives
+    m.set_weights(P0, Q0)
+    st = m.train_triplets(u, i, j)
+    T = st["steps"]
+    assert T == (n + B - 1) // B
+    P, Q = P0.copy(), Q0.copy()
+    loss, sP, sQ = O.local_serial(P, Q, u, i, j, 0.05, 0.01, B, hot, period)
+    a = np.float32(1 - 0.05 * 0.01)
+    Pg, Qg = m.get_weights()
+    Pw = P * np.power(np.float64(a), (T - sP))[:, None].astype(np.float32)
+    Qw = Q * np.power(np.float64(a), (T - sQ))[:, None].astype(np.float32)
+    np.testing.assert_allclose(Pg, Pw, rtol=1e-5, atol=HOG_ATOL)
+    np.testing.assert_allclose(Qg, Qw, rtol=1e-5, atol=HOG_ATOL)
+    assert st["loss"] == pytest.approx(loss, rel=1e-5)
+
+
+def test_local_untouched_rows_decay_exactly_and_replicas_follow_set_weights(rl):
+    """Rows never touched (hot ones included: a hot row's merge is then pure decay) end exactly as
+    exact mode's lazy decay leaves them; set_weights resets the replicas."""
+    g = np.random.default_rng(1)
+    U, I, d, B = 64, 64, 32, 8
+    pos = _hot_positives(U, I, list(range(10, 26)), g)
+    P0 = g.standard_normal((U, d)).astype(np.float32)
+    Q0 = g.standard_normal((I, d)).astype(np.float32)
+    h = rl.BPRMF(U, I, d, lr=0.1, wd=0.05, batch_size=B, semantics="local", local_steps=7)
+    x = rl.BPRMF(U, I, d, lr=0.1, wd=0.05, batch_size=B)
+    h.set_train(pos)
+    for m in (h, x):
+        m.set_weights(P0 * 3, Q0 * 3)  # replaced below: the replicas must follow
+        m.set_weights(P0, Q0)
+    n = 60 * B
+    u, i, j = g.integers(0, 4, n), g.integers(0, 4, n), g.integers(0, 4, n)
+    h.train_triplets(u, i, j)
+    x.train_triplets(u, i, j)
+    Ph, Qh = h.get_weights()
+    Px, Qx = x.get_weights()
+    np.testing.assert_allclose(Ph[4:], Px[4:], rtol=2e-6)
+    np.testing.assert_allclose(Qh[4:], Qx[4:], rtol=2e-6)
+    assert np.isfinite(Ph).all() and np.isfinite(Qh).all()
+
+
+def test_parallel_local_trains_ml100k_protocol(rl):
+    """F5 protocol (fo/tfo, d=32, B=4096, 20 epochs) in local mode: HR@10 / NDCG@10 inside the
+    reference's spread over seeds (mean +- 4 std), loss falling."""
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        ref = json.load(fh)
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    p = ref["protocol"]
+    gt = {int(u): set(f["gt_items"][f["gt_ptr"][k]:f["gt_ptr"][k + 1]].tolist())
+          for k, u in enumerate(f["gt_users"])}
+    m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
+                 batch_size=p["batch_size"], num_ng=p["num_ng"], seed=11, semantics="local")
+    m.fit(f["positives"].astype(np.int64), epochs=p["epochs"])
+    losses = [h["loss"] for h in m.history]
+    assert losses[-1] < 0.8 * losses[0]
+    P, Q = m.get_weights()
+    assert np.isfinite(P).all() and np.isfinite(Q).all()
+    kpi = rl.metrics.evaluate_topk(m, f["test_data"], gt, p["topk"])
+    print("local F5:", kpi, "reference:", ref["summary"])
+    for k in ("hr", "ndcg"):
+        mu, sd = ref["summary"][k]["mean"], ref["summary"][k]["std"]
+        assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)
+
+
+def test_local_rejects_sharded_handles(rl):
+    with pytest.raises(Exception):
+        rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="local")

@@ -218,3 +218,25 @@ def test_hogwild_spec_equals_reference_step_at_batch_one():
     np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
     assert loss == pytest.approx(lr_, rel=1e-5)
+
+
+def test_local_serial_spec_reduces_to_hogwild_and_merges_deltas():
+    """oracle.local_serial (semantics "local"): with no hot items it IS hogwild_serial; with hot
+    items and a period longer than the run, a hot row ends as its decayed start plus its change."""
+    g = np.random.default_rng(4)
+    U, I, d, B, n = 23, 31, 8, 16, 300
+    P = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    u, i, j = g.integers(0, U, n), g.integers(0, I, n), g.integers(0, I, n)
+    P1, Q1, P2, Q2 = P.copy(), Q.copy(), P.copy(), Q.copy()
+    a = O.hogwild_serial(P1, Q1, u, i, j, 0.05, 0.01, B)
+    b = O.local_serial(P2, Q2, u, i, j, 0.05, 0.01, B, [], 4)
+    assert a[0] == b[0] and np.array_equal(P1, P2) and np.array_equal(Q1, Q2)
+    # one hot item that no triplet touches: pure decay over the run, in one merge
+    i[i == 5] = 6
+    j[j == 5] = 6
+    P3, Q3 = P.copy(), Q.copy()
+    _, _, sQ = O.local_serial(P3, Q3, u, i, j, 0.05, 0.01, B, [5], 10 ** 6)
+    T = (n + B - 1) // B
+    assert sQ[5] == T
+    np.testing.assert_allclose(Q3[5], Q[5] * (1 - 0.05 * 0.01) ** T, rtol=1e-6)

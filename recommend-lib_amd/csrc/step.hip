@@ -441,6 +441,64 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
   }
 }
 
+// item segments one K2 lane group serves at most (k2_grid sizes the item grid for it): 6 at one
+// stripe (d <= 256); wider rows keep one per lane group (the rounds cost their registers 2-3 more
+// VGPRs there, and one wave per SIMD fewer at d = 512)
+template <int S>
+constexpr int item_rounds() { return S == 1 ? 6 : 1; }
+// one K2 item segment (record r0/r1): the sum of -/+ c P_u over its references in order, then the
+// update (single GPU) or the per-slot gradient (sharded)
+template <int G4, int S, bool SH, bool WT, bool PUB>
+static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const BatchView& bv,
+                                                       const Table& Q, const Hyper& hp, int ld,
+                                                       int32_t t, int sub,
+                                                       const float* __restrict__ contrib,
+                                                       float* __restrict__ grads, const GradRoute* gr) {
+  // record {item, beg | len << 15 | long << 30, refs 0..11 as 16-bit halves} (segment.hip)
+  if (r0.y >> 30) return;  // a workgroup-served hot item
+  const int32_t item = r0.x;
+  const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
+  ItemRow<G4, S, SH> row;
+  row.load(Q, item, ld, sub);
+  float4 g[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (len <= kInlineRefs) {  // the common case: every ref inline, all rows requested at once
+    const int32_t pk[6] = {r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    float4 rows[kInlineRefs][S];
+    int32_t rf[kInlineRefs];
+#pragma unroll
+    for (int m = 0; m < kInlineRefs; ++m) {
+      rf[m] = (pk[m >> 1] >> (16 * (m & 1))) & 0xFFFF;
+      if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+    }
+#pragma unroll
+    for (int m = 0; m < kInlineRefs; ++m)
+      if (m < len) acc_ref<S>(g, rows[m], rf[m]);
+  } else {  // lanes fetch G4 refs at once; rows requested F at a time before accumulating
+    // (F = 16 at S = 1, as on the hot-item path: a 13..16-reference item, the slowest K2 lane
+    // groups, then needs one round of row loads instead of two; the order of the sum is the same)
+    constexpr int F = S == 1 ? 16 : 8;
+    const int lane0 = (threadIdx.x & 63) - sub;
+    for (int base = beg; base < end; base += G4) {
+      const int32_t myref = base + sub < end ? bv.refs[base + sub] : 0;
+      const int cnt = min(G4, end - base);
+      for (int m0 = 0; m0 < cnt; m0 += F) {
+        float4 rows[F][S];
+        int32_t rf[F];
+#pragma unroll
+        for (int m = 0; m < F; ++m) {
+          rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
+          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+        }
+#pragma unroll
+        for (int m = 0; m < F; ++m)
+          if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
+      }
+    }
+  }
+  finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads, gr);  // SH: item field = slot
+}
 // K2 of step t, workgroup `blk` of its grid: loss workgroups, hot items (whole workgroups), item
 // segments (one lane group each), user segments spanning K1 workgroups.  PUB (fused step): every
 // updated row's stamp is published after the row (put_stamp), for K1 of step t+1 in the same
@@ -569,62 +627,31 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     SSTAMP(1, 3);
     return;
   }
-  const int s = (bid - long_blocks) * NG + grp;
-  const int sc = min(s, 2 * B - 1);
-  const int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
-  const int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
+  // item segments: lane group g of the item workgroups takes segments g, g + G, g + 2G, ... (G =
+  // item_blocks * NG lane groups).  The single-GPU step caps item_blocks (k2_grid): ~1,000 of a
+  // batch's ~5,700 items reach K2 there, and a grid sized for the 2B possible segments held
+  // ~900 workgroups that only loaded a record and left, dispatched ahead of K1 of the next step.
+  // At most item_rounds<S>() segments per lane group (k2_grid keeps item_blocks * NG >= 2B /
+  // rounds), in a fully unrolled sequence: a rolled loop here took 108 -> 162 VGPRs.
+  const int s0 = (bid - long_blocks) * NG + grp;
+  const int stride = item_blocks * NG;
+  const int sc = min(s0, 2 * B - 1);
+  int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
+  int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
   const int n_iseg = bv.meta[2];
   SSTAMP(1, 1);
   SROLE(1, 2);
-  // record {item, beg | len << 15 | long << 30, refs 0..11 as 16-bit halves} (segment.hip)
-  if (s >= n_iseg || (r0.y >> 30) || dead) return;  // past the batch's items, or a workgroup-served hot item
-  const int32_t item = r0.x;
-  const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
-#ifdef BPRMF_STEP_STAMPS
-  if (kStampHere && threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
-#endif
-  ItemRow<G4, S, SH> row;
-  row.load(Q, item, ld, sub);
-  float4 g[S];
+  if (dead) return;
 #pragma unroll
-  for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (len <= kInlineRefs) {  // the common case: every ref inline, all rows requested at once
-    const int32_t pk[6] = {r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-    float4 rows[kInlineRefs][S];
-    int32_t rf[kInlineRefs];
-#pragma unroll
-    for (int m = 0; m < kInlineRefs; ++m) {
-      rf[m] = (pk[m >> 1] >> (16 * (m & 1))) & 0xFFFF;
-      if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+  for (int round = 0; round < item_rounds<S>(); ++round) {
+    const int s = s0 + round * stride;
+    if (s >= n_iseg) break;  // past the batch's items
+    if (round) {
+      r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
+      r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
     }
-#pragma unroll
-    for (int m = 0; m < kInlineRefs; ++m)
-      if (m < len) acc_ref<S>(g, rows[m], rf[m]);
-  } else {  // lanes fetch G4 refs at once; rows requested F at a time before accumulating
-    // (F = 16 at S = 1, as on the hot-item path: a 13..16-reference item, the slowest K2 lane
-    // groups, then needs one round of row loads instead of two; the order of the sum is the same)
-    constexpr int F = S == 1 ? 16 : 8;
-    const int lane0 = (threadIdx.x & 63) - sub;
-    for (int base = beg; base < end; base += G4) {
-      const int32_t myref = base + sub < end ? bv.refs[base + sub] : 0;
-      const int cnt = min(G4, end - base);
-      for (int m0 = 0; m0 < cnt; m0 += F) {
-        float4 rows[F][S];
-        int32_t rf[F];
-#pragma unroll
-        for (int m = 0; m < F; ++m) {
-          rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
-          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
-        }
-#pragma unroll
-        for (int m = 0; m < F; ++m)
-          if (m0 + m < cnt) acc_ref<S>(g, rows[m], rf[m]);
-      }
-    }
+    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr);
   }
-  SSTAMP(1, 2);
-  finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads, gr);  // SH: item field = slot
-  SSTAMP(1, 3);
 }
 
 template <int G4, int S, bool SH, int KB, bool WT>
@@ -766,12 +793,30 @@ struct K2Grid {
   int lb, long_blocks, item_blocks, user_blocks;
   int total() const { return lb + long_blocks + item_blocks + user_blocks; }
 };
-template <int G4, int KB>
-static K2Grid k2_grid(int B, bool loss) {
+// item lane groups of the single-GPU step per 1024 triplets of the batch: K1 finishes the
+// single-reference items, so ~1,000 of a 4,096-triplet batch's ~5,700 distinct items reach K2
+// (ml-20m shape); 384 per 1024 gives those one lane group each, and a lane group loops when a
+// batch has more (BPRMF_K2_ITEM_LG overrides, 0 = one lane group per possible segment, A/B)
+static int k2_item_lg() {
+  static const int lg = [] {
+    const char* e = getenv("BPRMF_K2_ITEM_LG");
+    return e && *e ? atoi(e) : 384;
+  }();
+  return lg;
+}
+
+template <int G4, int S, int KB>
+static K2Grid k2_grid(int B, bool loss, bool capped = false) {
   constexpr int NG = KB / G4;
+  constexpr int R = item_rounds<S>();
   K2Grid k;
   k.long_blocks = item_long_blocks(B);
   k.item_blocks = (int)((2LL * B + NG - 1) / NG);
+  if (R > 1 && capped && k2_item_lg() > 0) {
+    const int need = (int)((2LL * B + (int64_t)R * NG - 1) / ((int64_t)R * NG));
+    k.item_blocks = std::min<int>(
+        k.item_blocks, std::max<int>(need, (int)(((int64_t)B * k2_item_lg() / 1024 + NG - 1) / NG)));
+  }
   // segments K2 finishes span K1 workgroups: at most one per workgroup boundary, and B/2
   const int tpb = kBlock / G4;
   const int k2_users = (int)std::min<int64_t>(B / 2, (B + tpb - 1) / tpb);
@@ -785,7 +830,7 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
                                    const Hyper& hp, const int32_t* tbase, int step,
                                    const StepBufs& sb, float* grads, hipStream_t s, double* loss,
                                    int64_t bstride, bool wt) {
-  const K2Grid k = k2_grid<G4, KB>(B, loss != nullptr);
+  const K2Grid k = k2_grid<G4, S, KB>(B, loss != nullptr, grads == nullptr);  // single GPU: capped
   const unsigned blocks = (unsigned)k.total();
 #define BPRMF_K2(SH_, WT_)                                                                        \
   k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,       \
@@ -829,7 +874,7 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
   if (!sb.pend_q || !sb.pend_p || !sb.pstride || !bstride) return hipErrorInvalidValue;
   if (!sb.xloss) loss = nullptr;
   BPRMF_DISPATCH4(g, ({
-    const K2Grid k = k2_grid<G4_, kBlock>(B, loss != nullptr);
+    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss != nullptr, true);
     const int k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
     k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
         bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,
@@ -845,7 +890,7 @@ hipError_t item_step_push(const Geom& g, BatchView bv, int B, Table P, Table Q, 
   if (!xloss) loss = nullptr;
   if (!gr.mark || gr.S <= 0) return hipErrorInvalidValue;
   BPRMF_DISPATCH4(g, ({
-    const K2Grid k = k2_grid<G4_, 256>(B, loss != nullptr);
+    const K2Grid k = k2_grid<G4_, S_, 256>(B, loss != nullptr);
     if (k.total() > kBoardMax) return hipErrorInvalidValue;
     k_item_step_push<G4_, S_, 256><<<(unsigned)k.total() + 1, 256, 0, s>>>(
         bv, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, loss, B, gr);

@@ -6,6 +6,56 @@
 
 #include "kernels.h"
 
+// Diagnostic build only (-DBPRMF_CALL_STAMPS, tools/ubench_call_stamps.py): per launch slot of a
+// call, the earliest workgroup start and the latest workgroup end (s_memrealtime, 100 MHz), spread
+// over 64 words per slot (blockIdx % 64) so the atomics do not serialise on one address; one table
+// per translation unit (no relocatable device code), each with its reader.  The real GPU timeline
+// of a call, kernel boundaries included, without a profiler in the loop.
+#ifdef BPRMF_CALL_STAMPS
+extern __device__ unsigned long long g_cs[64][2][64];
+#define BPRMF_CALL_STAMPS_DEF(tu)                                                                 \
+  __device__ unsigned long long g_cs[64][2][64];                                                  \
+  extern "C" int bprmf_debug_call_stamps_##tu(unsigned long long* out, int reset) {              \
+    if (reset) {                                                                                  \
+      static unsigned long long init[64][2][64];                                                  \
+      for (int a = 0; a < 64; ++a)                                                                \
+        for (int b = 0; b < 64; ++b) {                                                            \
+          init[a][0][b] = ~0ull;                                                                  \
+          init[a][1][b] = 0;                                                                      \
+        }                                                                                         \
+      return hipMemcpyToSymbol(HIP_SYMBOL(g_cs), init, sizeof init) == hipSuccess ? 0 : -3;       \
+    }                                                                                             \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cs), sizeof(g_cs)) == hipSuccess ? 0 : -3;      \
+  }
+#define CS_BEGIN(slot)                                                                            \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      atomicMin(&g_cs[(slot) & 63][0][blockIdx.x & 63], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+#define CS_END(slot)                                                                              \
+  do {                                                                                            \
+    __syncthreads();                                                                              \
+    if (threadIdx.x == 0)                                                                         \
+      atomicMax(&g_cs[(slot) & 63][1][blockIdx.x & 63], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+struct CsScope {  // CS_BEGIN at construction, CS_END when the kernel's threads leave its scope
+  int slot;
+  __device__ explicit CsScope(int s) : slot(s) { CS_BEGIN(slot); }
+  __device__ ~CsScope() { CS_END(slot); }
+};
+#else
+struct CsScope {
+  __device__ explicit CsScope(int) {}
+};
+#define BPRMF_CALL_STAMPS_DEF(tu)
+#define CS_BEGIN(slot) \
+  do {                 \
+  } while (0)
+#define CS_END(slot) \
+  do {               \
+  } while (0)
+#endif
+
 namespace bprmf {
 
 constexpr uint32_t TAG_NEG = 0x4E470000u;

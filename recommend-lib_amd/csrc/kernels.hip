@@ -19,6 +19,8 @@
 
 #include "device_common.h"
 
+BPRMF_CALL_STAMPS_DEF(ker)
+
 namespace bprmf {
 
 // ng_sample + DataLoader shuffle of one epoch (util/data_loader.py:680-690,
@@ -29,6 +31,7 @@ __global__ __launch_bounds__(kBlock) void k_sample(SamplerArgs a, uint32_t epoch
                                                    int32_t* __restrict__ oi,
                                                    int32_t* __restrict__ oj,
                                                    int32_t* __restrict__ err) {
+  CsScope cs_(1);  // diagnostic builds only (BPRMF_CALL_STAMPS)
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count;
        s += (int64_t)gridDim.x * blockDim.x) {
     int32_t u, i, j;
@@ -351,6 +354,7 @@ __global__ void k_advance_cursor(int32_t* __restrict__ c, int32_t n) {
 // stores are acknowledged: the host spins on that word instead of synchronising the stream
 __global__ void k_status_out(const uint64_t* __restrict__ src, uint64_t* dst, int n, uint64_t* seq_dst,
                              uint64_t seq) {
+  CS_BEGIN(63);  // diagnostic builds only (BPRMF_CALL_STAMPS); the end: after the stores' wait
   const int i = threadIdx.x;
   if (i < n) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (seq_dst) {
@@ -358,6 +362,7 @@ __global__ void k_status_out(const uint64_t* __restrict__ src, uint64_t* dst, in
     __syncthreads();
     if (i == 0) __hip_atomic_store(seq_dst, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  CS_END(63);
 }
 
 hipError_t set_cursor(int32_t* cursor, int32_t t, int32_t k, hipStream_t s, double* loss, int nloss) {

@@ -20,6 +20,8 @@
 
 #include "device_common.h"
 
+BPRMF_CALL_STAMPS_DEF(seg)
+
 namespace bprmf {
 
 constexpr int kBuildThreads = 1024;
@@ -735,6 +737,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   constexpr int T = kBuildThreads;
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
+  CsScope cs_(0);  // diagnostic builds only (BPRMF_CALL_STAMPS)
   using Scan = rocprim::block_scan<int, T>;
   using ScanL = rocprim::block_scan<uint64_t, T>;
   constexpr size_t kBucketBytes = 12 * (size_t)T * IPT2 + 4 * (kBuckets + 4);

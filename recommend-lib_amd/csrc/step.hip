@@ -23,6 +23,8 @@
 #include "device_common.h"
 #include "dist_body.h"
 
+BPRMF_CALL_STAMPS_DEF(step)
+
 // The in-launch hand-off below uses gfx94x/gfx950 cache-policy bits (sc1 stores and loads) and
 // the CDNA3/4 L2-per-XCD coherence model; no other target is built or supported.
 #if defined(__HIP_DEVICE_COMPILE__) && !(defined(__gfx950__) || defined(__gfx942__))
@@ -349,6 +351,7 @@ __global__ __launch_bounds__(kBlock) void k_user_step(BatchView bv, Table P, Tab
                                                       int step, StepBufs sb,
                                                       const float* __restrict__ item_rows,
                                                       PeerWait pw, int64_t bstride, int B) {
+  CsScope cs_(2);  // diagnostic builds only (BPRMF_CALL_STAMPS)
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   if (SH) wait_peer_flags(pw.flags, pw.world, pw.self, *tbase + step + 1, pw.err);
   k1_body<G4, S, SH, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, item_rows, B,
@@ -660,6 +663,7 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   StepBufs sb, int long_blocks, int item_blocks,
                                                   float* __restrict__ grads, double* __restrict__ loss,
                                                   int64_t bstride, int B) {
+  CsScope cs_(62);
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   k2_body<G4, S, SH, KB, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, long_blocks,
                                     item_blocks, grads, loss, B);
@@ -682,6 +686,7 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
                                                    int k2_blocks, double* __restrict__ loss,
                                                    int64_t bstride, int B, int32_t* err) {
   static_assert(KB == kBlock, "K1 and K2 workgroups share the launch's block size");
+  CsScope cs_(3 + step);
   const int32_t t = tbase[0] + step + 1;
   const int64_t kb = (int64_t)tbase[1] + step;
   if ((int)blockIdx.x < k2_blocks)

@@ -17,6 +17,8 @@ PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
 step tags 400 $PYT tests/test_gpu_build_tags.py tests/test_gpu_sharded.py &&
 step local 400 $PYT tests/test_gpu_hogwild.py tests/test_gpu_parity.py -k "local or atomic or hogwild" &&
 step bench20 200 python bench.py --steps 20 --warmup 5 &&
+step stamps 200 python tools/ubench_call_stamps.py 8 &&
+BPRMF_K2_ITEM_LG=0 step stamps_k2full 200 python tools/ubench_call_stamps.py 8 &&
 step bench20_sh 200 python bench.py --steps 20 --warmup 5 --sharded &&
 step bench_local20 200 python bench.py --steps 20 --warmup 5 --semantics local --no-cpu-baseline &&
 step bench_local 200 python bench.py --semantics local --no-cpu-baseline &&

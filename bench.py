@@ -196,15 +196,19 @@ def main():
                     m.train_steps(e, s, c)
                     done += c
 
+    # the timing barriers go through a gloo group (host sockets): the nccl group's barrier is a
+    # device all-reduce plus a synchronisation, ~0.1 ms that would land inside the timed region
+    bar = dist.new_group(backend="gloo") if dist and a.pg_backend == "nccl" else None
+
     def timed(first, k):
         if dist:
-            dist.barrier()
+            dist.barrier(group=bar)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(first, k)
         torch.cuda.synchronize()
         if dist:
-            dist.barrier()
+            dist.barrier(group=bar)
         el = time.perf_counter() - t0
         if dist:
             t = torch.tensor([el], dtype=torch.float64,

@@ -456,11 +456,19 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
                                                        const Table& Q, const Hyper& hp, int ld,
                                                        int32_t t, int sub,
                                                        const float* __restrict__ contrib,
-                                                       float* __restrict__ grads, const GradRoute* gr) {
+                                                       float* __restrict__ grads, const GradRoute* gr,
+                                                       int blk) {
+#ifdef BPRMF_STEP_STAMPS
+  constexpr bool kStampHere = PUB || !kFusedStampsOnly;
+#endif
+  (void)blk;
   // record {item, beg | len << 15 | long << 30, refs 0..11 as 16-bit halves} (segment.hip)
   if (r0.y >> 30) return;  // a workgroup-served hot item
   const int32_t item = r0.x;
   const int beg = r0.y & 0x7FFF, len = (r0.y >> 15) & 0x7FFF, end = beg + len;
+#ifdef BPRMF_STEP_STAMPS
+  if (kStampHere && threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
+#endif
   ItemRow<G4, S, SH> row;
   row.load(Q, item, ld, sub);
   float4 g[S];
@@ -500,7 +508,9 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
       }
     }
   }
+  SSTAMP(1, 2);
   finish_item<G4, S, SH, WT, PUB>(Q, item, item, g, row, hp, ld, t, sub, grads, gr);  // SH: item field = slot
+  SSTAMP(1, 3);
 }
 // K2 of step t, workgroup `blk` of its grid: loss workgroups, hot items (whole workgroups), item
 // segments (one lane group each), user segments spanning K1 workgroups.  PUB (fused step): every
@@ -653,7 +663,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
       r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
       r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
     }
-    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr);
+    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
   }
 }
 

@@ -1,5 +1,5 @@
-"""HR@10 / NDCG@10 of the exact and the hogwild (relaxed) step on the same data, one JSON line per
-(workload, mode).  GPU box:  python tools/hr_modes.py [--epochs E] [--users-eval N]
+"""HR@10 / NDCG@10 of the exact step and the relaxed ones (hogwild, local) on the same data, one
+JSON line per (workload, mode).  GPU box:  python tools/hr_modes.py [--epochs E] [--users-eval N]
 
 Workloads:
   f5     the reference protocol of tests/golden/hr_ndcg_ml100k.* (ml-100k fo/tfo, d=32, B=4096,
@@ -88,11 +88,12 @@ def main():
     ap.add_argument("--users-eval", type=int, default=20000)
     ap.add_argument("--seeds", default="11,12,13")
     ap.add_argument("--which", default="f5,ml20m")
+    ap.add_argument("--modes", default="exact,hogwild,local")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first)
     rl = importlib.import_module("recommend-lib_amd")
     for w in a.which.split(","):
-        for mode in ("exact", "hogwild"):
+        for mode in a.modes.split(","):
             for seed in (int(x) for x in a.seeds.split(",")):
                 r = f5(rl, mode, seed) if w == "f5" else ml20m(rl, mode, seed, a.epochs, a.users_eval)
                 print(json.dumps(r), flush=True)

@@ -83,7 +83,14 @@ KB = int(os.environ.get("BPRMF_K2_BLOCK", "256"))
 NG = KB // 32
 lb = (B + KB - 1) // KB
 k2_users = min(B // 2, B // 8)
-k2_blocks = lb + 64 + (2 * B) // NG + (k2_users + NG - 1) // NG
+# the item workgroups as step.hip k2_grid sizes them for the single-GPU step (capped: up to 6
+# segments per lane group; BPRMF_K2_ITEM_LG=0: one lane group per possible segment)
+lg = int(os.environ.get("BPRMF_K2_ITEM_LG", "384"))
+item_blocks = (2 * B + NG - 1) // NG
+if lg > 0:
+    need = (2 * B + 6 * NG - 1) // (6 * NG)
+    item_blocks = min(item_blocks, max(need, (B * lg // 1024 + NG - 1) // NG))
+k2_blocks = lb + 64 + item_blocks + (k2_users + NG - 1) // NG
 def by_len(st, k2_blocks):
     k2 = st[1, :k2_blocks]
     sel = (k2[:, 5] == 2) & (k2[:, 3] >= k2[:, 0]) & (k2[:, 2] > 0)

@@ -195,7 +195,8 @@ int bprmf_destroy(bprmf_handle* h) {
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep};
+                  h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
+                  h->d_skeys};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -295,11 +296,23 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   const std::vector<int64_t>& indptr = csr.indptr;
   const std::vector<int32_t>& indices = csr.indices;
   const int64_t n = (int64_t)pu.size();
-  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices};
+  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices, h->d_soff, h->d_skeys};
   for (void* p : olds)
     if (p) HIPCHK(hipFree(p));
-  h->d_pos_u = h->d_pos_i = h->d_indices = nullptr;
-  h->d_indptr = nullptr;
+  h->d_pos_u = h->d_pos_i = h->d_indices = h->d_skeys = nullptr;
+  h->d_indptr = h->d_soff = nullptr;
+  {  // the sampler's search trees (BPRMF_SAMPLE_TREE=0: the binary search, A/B)
+    const char* e = getenv("BPRMF_SAMPLE_TREE");
+    if (!(e && e[0] == '0')) {
+      SearchTree st;
+      build_search_tree(indptr, indices, &st);
+      if (int r = dalloc(&h->d_soff, (int64_t)st.soff.size())) return r;
+      if (int r = dalloc(&h->d_skeys, std::max<int64_t>(16, (int64_t)st.keys.size()))) return r;
+      HIPCHK(hipMemcpy(h->d_soff, st.soff.data(), 8 * st.soff.size(), hipMemcpyHostToDevice));
+      if (!st.keys.empty())
+        HIPCHK(hipMemcpy(h->d_skeys, st.keys.data(), 4 * st.keys.size(), hipMemcpyHostToDevice));
+    }
+  }
   if (int r = dalloc(&h->d_pos_u, n)) return r;
   if (int r = dalloc(&h->d_pos_i, n)) return r;
   if (int r = dalloc(&h->d_indptr, h->U + 1)) return r;
@@ -354,6 +367,8 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   a.feistel_c = h->feistel_c;
   a.k0 = h->k0;
   a.k1 = h->k1;
+  a.skeys = h->d_skeys;
+  a.soff = h->d_soff;
   return a;
 }
 

@@ -168,6 +168,31 @@ static __device__ __forceinline__ int64_t kth_nonmember(const int32_t* __restric
   return k + lo;
 }
 
+// The same count through the user's 16-ary tree (host_plan.h build_search_tree): keys b[x] =
+// a[x] - x, one 64-byte node (four 16-byte loads, one line) per level, m = #{x : b[x] <= k};
+// equal to kth_nonmember's m for every k (same value, fewer dependent loads: ceil(log16 n)
+// instead of ceil(log2 n), and ~4x fewer line requests).
+static __device__ __forceinline__ int64_t kth_nonmember_tree(const int32_t* __restrict__ keys,
+                                                             int64_t n, int64_t k) {
+  if (n <= 0) return k;
+  int L = 1;
+  for (int64_t c = 16; c < n; c *= 16) ++L;
+  int64_t node = 0;
+  for (int l = L - 1;; --l) {
+    const int4* q = reinterpret_cast<const int4*>(keys + node * 16);
+    const int4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
+    const int c = (v0.x <= k) + (v0.y <= k) + (v0.z <= k) + (v0.w <= k) + (v1.x <= k) +
+                  (v1.y <= k) + (v1.z <= k) + (v1.w <= k) + (v2.x <= k) + (v2.y <= k) +
+                  (v2.z <= k) + (v2.w <= k) + (v3.x <= k) + (v3.y <= k) + (v3.z <= k) + (v3.w <= k);
+    if (l == 0) return k + node * 16 + c;
+    if (c == 0) return k;  // k below the level's first key: no b[x] <= k
+    // the next level down: past this level's nodes (ceil(n / 16^(l+1)) of them)
+    const int sh = 4 * (l + 1);
+    keys += 16 * ((n + (1LL << sh) - 1) >> sh);
+    node = node * 16 + (c - 1);
+  }
+}
+
 // One slot of the device sampler (BPRData.ng_sample + the shuffled DataLoader,
 // util/data_loader.py:680-690, BPRMFRecommender.py:141): slot -> triplet q = perm(slot) ->
 // positive q / num_ng -> (global user u, item i) and the negative j, uniform over u's
@@ -194,7 +219,8 @@ static __device__ __forceinline__ bool sample_slot(const SamplerArgs& a, uint32_
 #if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 1)  // diagnostic: no search (timing only)
   j = (int32_t)k;
 #else
-  j = (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
+  j = a.skeys ? (int32_t)kth_nonmember_tree(a.skeys + a.soff[ul], deg, (int64_t)k)
+              : (int32_t)kth_nonmember(a.indices + beg, deg, (int64_t)k);
 #endif
   return true;
 }

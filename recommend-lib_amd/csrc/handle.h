@@ -50,6 +50,8 @@ struct bprmf_handle {
   int32_t* d_pos_i = nullptr;
   int64_t* d_indptr = nullptr;
   int32_t* d_indices = nullptr;
+  int64_t* d_soff = nullptr;    // the sampler's search trees (host_plan.h SearchTree)
+  int32_t* d_skeys = nullptr;
   uint32_t feistel_a = 1, feistel_c = 1;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0 = 0, k1 = 0;  // shard sampler key
   // triplet chunk

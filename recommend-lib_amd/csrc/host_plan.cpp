@@ -55,6 +55,48 @@ int build_shard_csr(const int32_t* users, const int32_t* items, int64_t nnz, con
   return 0;
 }
 
+void build_search_tree(const std::vector<int64_t>& indptr, const std::vector<int32_t>& indices,
+                       SearchTree* out) {
+  const int64_t U = (int64_t)indptr.size() - 1;
+  SearchTree t;
+  t.soff.assign(U + 1, 0);
+  // sizes first: level l (0 = leaves) has ceil(n / 16^(l+1)) nodes of 16 keys
+  for (int64_t u = 0; u < U; ++u) {
+    const int64_t n = indptr[u + 1] - indptr[u];
+    int64_t keys = 0;
+    for (int64_t m = n, l = 0; l < search_levels(n); ++l) {
+      m = (m + 15) / 16;  // nodes at this level
+      keys += 16 * m;
+    }
+    t.soff[u + 1] = t.soff[u] + keys;
+  }
+  t.keys.assign(t.soff[U], INT32_MAX);
+  std::vector<int32_t> cur, up;
+  for (int64_t u = 0; u < U; ++u) {
+    const int64_t n = indptr[u + 1] - indptr[u];
+    const int L = search_levels(n);
+    if (!L) continue;
+    cur.resize(n);
+    for (int64_t x = 0; x < n; ++x) cur[x] = indices[indptr[u] + x] - (int32_t)x;  // b, non-decreasing
+    // level sizes bottom-up, then write top-down: the root level first
+    std::vector<std::vector<int32_t>> lv;
+    lv.push_back(cur);
+    for (int l = 1; l < L; ++l) {
+      const std::vector<int32_t>& below = lv.back();
+      up.clear();
+      for (size_t q = 0; q < below.size(); q += 16) up.push_back(below[q]);
+      lv.push_back(up);
+    }
+    int64_t o = t.soff[u];
+    for (int l = L - 1; l >= 0; --l) {
+      const std::vector<int32_t>& v = lv[l];
+      std::copy(v.begin(), v.end(), t.keys.begin() + o);
+      o += 16 * (((int64_t)v.size() + 15) / 16);
+    }
+  }
+  *out = std::move(t);
+}
+
 int runner_geom(int64_t batch, int64_t item_num, int world, int ld, int64_t chunk_steps,
                 RunnerGeom* g) {
   if (!g || batch <= 0 || item_num <= 0 || world <= 0 || ld <= 0 || chunk_steps <= 0)

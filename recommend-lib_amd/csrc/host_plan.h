@@ -24,6 +24,25 @@ int build_shard_csr(const int32_t* users, const int32_t* items, int64_t nnz, con
                     const int32_t* ex_items, int64_t n_ex, int64_t user_num, int64_t item_num,
                     int world, int rank, int64_t local_users, ShardCsr* out);
 
+// The sampler's search structure (device_common.h sample_slot): per user with sorted positives
+// a[0..n), b[x] = a[x] - x is non-decreasing and the k-th non-member is k + #{x : b[x] <= k}.
+// Per user a 16-ary tree of 64-byte nodes (16 int32 keys, padded with INT32_MAX), levels stored
+// top-down: the leaves are b itself in 16-key nodes, a level above holds the first key of each
+// node below.  soff[u] = the user's first key (a multiple of 16), levels = ceil(log16(n)) (n >= 1;
+// n = 0: no keys).  One 64-byte load per level instead of one dependent load per halving.
+struct SearchTree {
+  std::vector<int64_t> soff;  // [users + 1]
+  std::vector<int32_t> keys;
+};
+void build_search_tree(const std::vector<int64_t>& indptr, const std::vector<int32_t>& indices,
+                       SearchTree* out);
+// levels of a user's tree with n positives (0 for n = 0)
+inline int search_levels(int64_t n) {
+  int L = 0;
+  for (int64_t c = 1; c < n; c *= 16) ++L;
+  return n > 0 ? (L > 0 ? L : 1) : 0;
+}
+
 // rows of a rank's shard of `total` rows under strided sharding (row r lives on r % world)
 inline int64_t shard_rows(int64_t total, int world, int rank) {
   return (total - rank + world - 1) / world;

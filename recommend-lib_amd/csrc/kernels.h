@@ -131,6 +131,9 @@ struct SamplerArgs {
   int32_t num_ng, world;
   uint32_t feistel_a, feistel_c;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0, k1;        // Philox key (shard seed)
+  // the k-th non-member search's 16-ary trees (host_plan.h SearchTree; null: binary search)
+  const int32_t* skeys = nullptr;
+  const int64_t* soff = nullptr;
 };
 
 // --- launches (all asynchronous on `s`) ---

@@ -74,8 +74,57 @@ static void check_csr(std::mt19937_64& g, int64_t U, int64_t I, int64_t nnz, int
   }
 }
 
+// the device search (device_common.h kth_nonmember_tree), restated on the host
+static int64_t tree_count(const int32_t* keys, int64_t n, int64_t k) {
+  if (n <= 0) return 0;
+  int L = 1;
+  for (int64_t c = 16; c < n; c *= 16) ++L;
+  int64_t node = 0;
+  for (int l = L - 1;; --l) {
+    int c = 0;
+    for (int x = 0; x < 16; ++x) c += keys[node * 16 + x] <= k;
+    if (l == 0) return node * 16 + c;
+    if (c == 0) return 0;
+    const int sh = 4 * (l + 1);
+    keys += 16 * ((n + (1LL << sh) - 1) >> sh);
+    node = node * 16 + (c - 1);
+  }
+}
+
+static void check_tree(std::mt19937_64& g, int64_t U, int64_t I, int64_t maxdeg) {
+  std::vector<int64_t> indptr(U + 1, 0);
+  std::vector<int32_t> indices;
+  for (int64_t u = 0; u < U; ++u) {
+    const int64_t want = g() % 7 == 0 ? 0 : (int64_t)(g() % (maxdeg + 1));
+    std::set<int32_t> s;
+    while ((int64_t)s.size() < std::min(want, I)) s.insert((int32_t)(g() % I));
+    indices.insert(indices.end(), s.begin(), s.end());
+    indptr[u + 1] = (int64_t)indices.size();
+  }
+  SearchTree t;
+  build_search_tree(indptr, indices, &t);
+  CHECK((int64_t)t.soff.size() == U + 1 && t.soff[U] == (int64_t)t.keys.size());
+  bool ok = true;
+  for (int64_t u = 0; u < U && ok; ++u) {
+    const int64_t n = indptr[u + 1] - indptr[u];
+    ok = t.soff[u] % 16 == 0;
+    const int32_t* a = indices.data() + indptr[u];
+    for (int rep = 0; rep < 40 && ok; ++rep) {
+      const int64_t k = rep < 4 ? rep : (int64_t)(g() % (uint64_t)std::max<int64_t>(1, I - n));
+      int64_t m = 0;  // brute force: #{x : a[x] - x <= k}
+      for (int64_t x = 0; x < n; ++x) m += a[x] - x <= k;
+      ok = tree_count(t.keys.data() + t.soff[u], n, k) == m;
+    }
+  }
+  CHECK(ok);
+}
+
 int main() {
   std::mt19937_64 g(20261017);
+  // the sampler's search trees: empty users, one node, 2-4 levels (up to 16^3 + positives)
+  check_tree(g, 50, 40, 16);
+  check_tree(g, 200, 3000, 300);
+  check_tree(g, 12, 100000, 70000);
   // shard CSR: empty input, small and skewed shapes, every world size up to one node's 16 ranks
   check_csr(g, 1, 1, 0, 0, 1);
   check_csr(g, 5, 3, 0, 4, 2);

@@ -17,6 +17,9 @@ step() {  # name, timeout, command...
 step gpu_tests 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread &&
 step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" &&
 step step_stamps 200 python tools/ubench_step_stamps.py &&
+step stamps 200 python tools/ubench_call_stamps.py 8 &&
+BPRMF_SAMPLE_TREE=0 step stamps_bsearch 200 python tools/ubench_call_stamps.py 8 &&
+step bench20 200 python bench.py --steps 20 --warmup 5 &&
 step hr 400 python tools/hr_modes.py --which f5,ml20m --modes exact,local --seeds 11,12 --epochs 10 &&
 cd /tmp && export TMPDIR=/tmp &&
 step prof 240 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline

@@ -17,7 +17,7 @@ import json
 import os
 
 STEP_KERNELS = ("k_fused_step", "k_user_step", "k_item_step", "k_gather_rows", "k_add_rows",
-                "k_apply_rows")
+                "k_apply_rows", "k_hogwild", "k_local_merge")
 
 
 def per_kernel(d, counter):
@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--factor", type=int, default=128)
+    ap.add_argument("--steps-per-launch", type=int, default=0,
+                    help="relaxed modes: steps one k_hogwild launch covers (its bytes and one merge's "
+                         "are divided by it)")
     a = ap.parse_args()
     fetch = per_kernel(a.fetch_dir, "FETCH_SIZE")
     write = per_kernel(a.write_dir, "WRITE_SIZE")
@@ -51,6 +54,9 @@ def main():
     # one launch's traffic is one step's (the chunk's lone K1 and K2 launches are its two ends)
     if "k_fused_step" in kernels:
         total = kernels["k_fused_step"]["bytes"]
+    elif "k_hogwild" in kernels and a.steps_per_launch > 0:  # relaxed: per launch (+ its merge) / steps
+        total = round((kernels["k_hogwild"]["bytes"] + kernels.get("k_local_merge", {}).get("bytes", 0))
+                      / a.steps_per_launch)
     else:
         total = sum(v["bytes"] for v in kernels.values())
     alg = a.batch * (24 * a.factor + 12)

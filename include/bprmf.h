@@ -47,7 +47,13 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
  * GPU (each XCD's waves see their own XCD's updates at once, the other XCDs' only at the next
  * merge), and every `local_steps` steps (default 16) the replicas are merged: new = decayed base +
  * sum over XCDs of each replica's change.  Staleness across XCDs is bounded by `local_steps`
- * steps; single-GPU handles only. */
+ * steps.
+ * LOCAL at world > 1 (data-parallel items): users stay sharded (u % world == rank, each rank
+ * samples only its own users' positives) but every rank holds the WHOLE item table and trains it
+ * as above; every `dp_steps` steps (default 64) and at the end of every call the ranks' item
+ * tables are merged: new = decayed base + sum over ranks of each rank's change since the last
+ * merge (one all-reduce of the table, bprmf_dist_init_rccl or _loopback; the IPC transport is
+ * not supported).  Staleness across GPUs is bounded by `dp_steps` steps. */
 
 /* How an EXACT step sums duplicate rows' gradients ("ship both").  SEGMENTED: the
  * batch is sorted by user and by item and every row is summed by one writer in a fixed order,
@@ -68,13 +74,14 @@ typedef struct {
   float init_std;       /* nn.init.normal_(std=0.01) (BPRMFRecommender.py:39-40) */
   uint64_t seed;        /* seeds init, sampler and shuffle (the reference is unseeded) */
   int32_t device;       /* HIP device ordinal */
-  int32_t rank;         /* shard of this handle: owns users u%world==rank, items i%world==rank */
+  int32_t rank;         /* shard of this handle: owns users u%world==rank, items i%world==rank
+                           (BPRMF_SEM_LOCAL: every item, see above) */
   int32_t world;        /* 1 for a single GPU */
   int32_t semantics;    /* BPRMF_SEM_EXACT (0, default): the reference's batch-synchronous step;
                            BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
   int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
   int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 16) */
-  int32_t reserved[1];
+  int32_t dp_steps;     /* BPRMF_SEM_LOCAL, world > 1: steps between the ranks' item merges (0: 64) */
 } bprmf_config;
 
 typedef struct {

@@ -193,6 +193,50 @@ def local_serial(P, Q, u, i, j, lr, wd, B, hot, period, t0=0):
     return loss, sP, sQ
 
 
+def local_dp_serial(P_parts, Q, trips, lr, wd, B, hots, period, dp_period, world):
+    """semantics "local" at world > 1 (csrc/dist.cpp dp_run / dp_merge, hogwild.hip k_dp_delta /
+    k_dp_apply), each rank run serially on one XCD (the SERIAL test build): the spec, NOT the
+    reference step.
+      rank r trains its users' rows P_parts[r] (row = u // world) and its own copy of the whole
+      item table with local_serial on trips[r] = (u, i, j) (B triplets per step, global ids; hot
+      set hots[r]);
+      every dp_period steps and at the end: each copy is brought to t1 (rows decayed from their
+      stamps), delta_r = copy - base * a^(t1 - tm) (base: the table of the last merge, current at
+      tm); every copy and the base become base * a^(t1 - tm) + sum of the deltas in rank order.
+    P_parts updated in place, rows current at the returned stamps.  Returns (loss, sPs, Q at T)."""
+    log2a = math.log2(1.0 - float(lr) * float(wd))
+
+    def dec(k):
+        return np.float32(2.0 ** np.float32(k * log2a)) if k > 0 else np.float32(1)
+
+    steps = len(trips[0][0]) // B
+    base = Q.astype(np.float32).copy()
+    sPs = [np.zeros(p.shape[0], np.int64) for p in P_parts]
+    loss = 0.0
+    tm = 0
+    while tm < steps:
+        t1 = min(steps, tm + dp_period)
+        mats = []
+        for r in range(world):
+            Pr = P_parts[r]
+            for x in range(Pr.shape[0]):  # local_serial starts every row at t0 = tm
+                Pr[x] = Pr[x] * dec(tm - sPs[r][x])
+            Qr = base.copy()
+            u, i, j = (np.asarray(v)[tm * B:t1 * B] for v in trips[r])
+            lo, sP, sQ = local_serial(Pr, Qr, u // world, i, j, lr, wd, B, hots[r], period, t0=tm)
+            loss += lo
+            sPs[r] = sP
+            mats.append(np.stack([Qr[x] * dec(t1 - sQ[x]) for x in range(Qr.shape[0])]))
+        fb = dec(t1 - tm)
+        b = (base * fb).astype(np.float64)
+        acc = np.zeros_like(b)
+        for r in range(world):
+            acc += mats[r].astype(np.float64) - b
+        base = (b + acc).astype(np.float32)
+        tm = t1
+    return loss, sPs, base
+
+
 # ----------------------------------------------------------------------------------------------
 # 2. sampler specification (bit-exact target for the HIP sampler)
 # ----------------------------------------------------------------------------------------------

@@ -99,9 +99,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   if (cfg->semantics != BPRMF_SEM_EXACT && cfg->semantics != BPRMF_SEM_HOGWILD &&
       cfg->semantics != BPRMF_SEM_LOCAL)
     return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0), _HOGWILD (1) or _LOCAL (2)");
-  if (cfg->semantics != BPRMF_SEM_EXACT && cfg->world != 1)
-    return fail(BPRMF_E_UNSUPPORTED, "relaxed semantics: single-GPU handles only");
-  if (cfg->local_steps < 0) return fail(BPRMF_E_INVALID, "local_steps must be >= 0");
+  if (cfg->semantics == BPRMF_SEM_HOGWILD && cfg->world != 1)
+    return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
+  if (cfg->local_steps < 0 || cfg->dp_steps < 0)
+    return fail(BPRMF_E_INVALID, "local_steps and dp_steps must be >= 0");
   if (cfg->step_mode != BPRMF_STEP_SEGMENTED && cfg->step_mode != BPRMF_STEP_ATOMIC)
     return fail(BPRMF_E_INVALID, "step_mode must be BPRMF_STEP_SEGMENTED (0) or BPRMF_STEP_ATOMIC (1)");
   if (cfg->step_mode == BPRMF_STEP_ATOMIC && cfg->world != 1)
@@ -110,6 +111,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   h->cfg = *cfg;
   h->semantics = cfg->semantics;
   if (cfg->local_steps > 0) h->local_steps = cfg->local_steps;
+  if (cfg->dp_steps > 0) h->dp_steps = cfg->dp_steps;
   h->geom = g;
   h->hp.lr = cfg->lr;
   h->hp.wd = cfg->weight_decay;
@@ -121,7 +123,8 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   h->hp.log2a = std::log2(h->hp.alpha);
   const int64_t W = cfg->world, R = cfg->rank;
   h->U = shard_rows(cfg->user_num, (int)W, (int)R);
-  h->I = shard_rows(cfg->item_num, (int)W, (int)R);
+  const bool dpi = dp_items(*cfg);  // LOCAL at world > 1: every item on every rank
+  h->I = dpi ? cfg->item_num : shard_rows(cfg->item_num, (int)W, (int)R);
   const uint64_t shard_seed = cfg->seed + (uint64_t)cfg->rank * 0x9E3779B97F4A7C15ull;
   h->k0 = (uint32_t)shard_seed;
   h->k1 = (uint32_t)(shard_seed >> 32);
@@ -151,6 +154,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
+  if (dpi) {
+    TRY(dalloc(&h->d_qbase, h->I * ld));
+    TRY(dalloc(&h->d_qdelta, h->I * ld));
+  }
   // {err, dist words, loss slots[kLossSlots], two call sequence numbers}
   const size_t status_bytes = kSeqCapOff + 8;
   TRY(dalloc(&h->d_status, (int64_t)status_bytes));
@@ -177,7 +184,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size
   const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
   e = init_normal(g, h->P.W, h->U, cfg->init_std, s0, s1, 0u, (int)W, (int)R, h->stream);
-  if (e == hipSuccess) e = init_normal(g, h->Q.W, h->I, cfg->init_std, s0, s1, 1u, (int)W, (int)R, h->stream);
+  if (e == hipSuccess)  // a replicated item table: every rank draws all of it
+    e = init_normal(g, h->Q.W, h->I, cfg->init_std, s0, s1, 1u, dpi ? 1 : (int)W, dpi ? 0 : (int)R, h->stream);
+  if (e == hipSuccess && dpi)
+    e = hipMemcpyAsync(h->d_qbase, h->Q.W, sizeof(float) * h->I * ld, hipMemcpyDeviceToDevice, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) {
     bprmf_destroy(h);
@@ -196,7 +206,7 @@ int bprmf_destroy(bprmf_handle* h) {
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
                   h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
-                  h->d_skeys};
+                  h->d_skeys, h->d_qbase, h->d_qdelta};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -331,7 +341,7 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   feistel_dims(N, &h->feistel_a, &h->feistel_c);
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
   // the first calls (a larger chunk later would reallocate and recapture)
-  if (seg_mode(h)) {
+  if (seg_mode(h) && h->semantics == BPRMF_SEM_EXACT) {
     const int64_t B = h->cfg.batch_size;
     const int64_t steps = h->cfg.world == 1 ? chunk_triplets(h) / B : dist_chunk_steps(h);
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(steps, ((int64_t)N + B - 1) / B));
@@ -994,6 +1004,10 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   std::vector<int32_t> st(std::max(h->U, h->I), h->t);
   if (h->U) HIPCHK(hipMemcpy(h->P.stamp, st.data(), 4 * h->U, hipMemcpyHostToDevice));
   if (h->I) HIPCHK(hipMemcpy(h->Q.stamp, st.data(), 4 * h->I, hipMemcpyHostToDevice));
+  if (h->d_qbase) {  // LOCAL at world > 1: the next merge's base (every rank sets the same Q)
+    HIPCHK(hipMemcpy(h->d_qbase, h->Q.W, sizeof(float) * h->I * ld, hipMemcpyDeviceToDevice));
+    h->dp_t = h->t;
+  }
   return local_refresh(h);  // LOCAL: the replicas start from the new rows
 }
 

@@ -67,6 +67,15 @@ struct Transport {
     HIPCHK(max_vals(vals, W, dev, h->stream));
     return 0;
   }
+  // semantics LOCAL at world > 1: the sum over ranks of every rank's buf (n floats), the same
+  // bits on every rank; *out = where it landed (buf itself, or the transport's scratch)
+  virtual int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) {
+    (void)h;
+    (void)buf;
+    (void)n;
+    (void)out;
+    return fail(BPRMF_E_UNSUPPORTED, "this transport has no all-reduce: use rccl (or loopback)");
+  }
   // exchange() only enqueues stream work (no host synchronisation): hipGraph-capturable
   virtual bool capturable() const { return false; }
   virtual bool ready() const { return true; }
@@ -116,6 +125,13 @@ struct RcclTransport final : Transport {
     (void)seq;
     if (h->cfg.world == 1) return 0;
     NCCLCHK(ncclAllReduce(dev, dev, 1, ncclInt32, ncclMax, comm, h->stream));
+    return 0;
+  }
+  // in place; ring and tree all-reduces reduce each element once and broadcast the result, so
+  // every rank holds the same bits
+  int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) override {
+    *out = buf;
+    if (h->cfg.world > 1) NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm, h->stream));
     return 0;
   }
 };
@@ -277,6 +293,7 @@ struct LoopGroup {
   int64_t gen = 0;
   std::vector<const void* const*> send;
   std::vector<int32_t> val;
+  std::vector<const float*> fbuf;  // allreduce_sum: every rank's buffer
   void barrier() {
     std::unique_lock<std::mutex> l(m);
     const int64_t g = gen;
@@ -296,7 +313,10 @@ struct LoopTransport final : Transport {
   bool shares_device() const override { return true; }  // in-process shards on one GPU
   int64_t key = 0;
   LoopGroup* g = nullptr;
+  float* scratch = nullptr;  // allreduce_sum's result (peers still read this rank's buffer)
+  int64_t scratch_n = 0;
   ~LoopTransport() override {
+    if (scratch) (void)!hipFree(scratch);
     std::lock_guard<std::mutex> l(g_loops_m);
     if (g && --g->refs == 0) {
       g_loops.erase(key);
@@ -317,6 +337,39 @@ struct LoopTransport final : Transport {
     const hipError_t e = hipStreamSynchronize(h->stream);
     if (!rc && e != hipSuccess) rc = fail(BPRMF_E_HIP, "loopback sync: %s", hipGetErrorString(e));
     g->barrier();  // every peer has read this shard's send blocks
+    return rc;
+  }
+  // every rank sums all ranks' buffers in rank order into its scratch (the same bits everywhere)
+  int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) override {
+    const int W = h->cfg.world, R = h->cfg.rank;
+    int rc = 0;
+    if (n > scratch_n) {
+      if (scratch) (void)!hipFree(scratch);
+      scratch = nullptr;
+      scratch_n = 0;
+      if (hipMalloc((void**)&scratch, sizeof(float) * n) == hipSuccess) scratch_n = n;
+      else rc = fail(BPRMF_E_HIP, "loopback all-reduce scratch");
+    }
+    hipError_t e = hipStreamSynchronize(h->stream);  // this rank's buffer is complete
+    if (!rc && e != hipSuccess) rc = fail(BPRMF_E_HIP, "loopback sync: %s", hipGetErrorString(e));
+    g->fbuf[R] = buf;
+    g->barrier();
+    bool all = true;
+    DpSrcs src{};
+    for (int p = 0; p < W; ++p) {
+      src.p[p] = g->fbuf[p];
+      all = all && src.p[p];
+    }
+    if (!rc && all) {
+      e = dp_sum(src, W, scratch, n, h->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+      if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "loopback all-reduce: %s", hipGetErrorString(e));
+    } else if (!rc) {
+      rc = fail(BPRMF_E_STATE, "loopback all-reduce: a peer failed");
+    }
+    g->barrier();  // every peer has read this rank's buffer
+    g->fbuf[R] = nullptr;
+    *out = scratch;
     return rc;
   }
   int max_i32(bprmf_handle* h, int32_t* dev, int32_t* vals, int32_t seq) override {
@@ -395,6 +448,15 @@ int64_t dist_chunk_steps(const bprmf_handle* h) {
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap);
 
 static int dist_attach(bprmf_handle* h, Transport* tr) {
+  if (dp_items(h->cfg)) {  // LOCAL at world > 1: the item merge needs only the transport
+    if (h->dist) {
+      HIPCHK(hipStreamSynchronize(h->stream));
+      dist_free(h->dist);
+    }
+    h->dist = new DistState();
+    h->dist->tr = tr;
+    return 0;
+  }
   if (!seg_mode(h)) {
     delete tr;
     return fail(BPRMF_E_UNSUPPORTED, "sharded steps need batch_size <= %d", kMaxSegBatch);
@@ -755,6 +817,63 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   return 0;
 }
 
+// ---- semantics LOCAL at world > 1: the item table replicated, merged across ranks ------------
+// (include/bprmf.h BPRMF_SEM_LOCAL.)  Every rank trains its own users' triplets
+// with the single-GPU local step (hogwild.hip, hot items in per-XCD replicas) on its own copy of
+// the whole item table; a merge brings every rank's copy to base + the sum of the ranks' changes.
+static int dp_merge(bprmf_handle* h) {
+  const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  if (la.H > 0 && h->rep_t != h->t)  // the XCD replicas into this rank's table first
+    HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
+  HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, h->geom.ld, h->hp, h->dp_t, h->t, h->stream));
+  const float* sum = nullptr;
+  if (int r = h->dist->tr->allreduce_sum(h, h->d_qdelta, h->I * (int64_t)h->geom.ld, &sum)) return r;
+  HIPCHK(dp_apply(h->Q, h->d_qbase, sum, h->geom.ld, h->hp, h->dp_t, h->t, h->stream));
+  if (la.H > 0)  // the replicas restart from the merged rows
+    HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->t, h->t, true, h->stream));
+  h->rep_t = h->dp_t = h->t;
+  return 0;
+}
+
+// steps [first_step, first_step + n_steps) of this rank's epoch (sampled; slots past the rank's
+// own epoch are empty, so every rank takes the same steps and merges) or n_steps * B replayed
+// device ids ru/ri/rj (global ids, u < 0: empty slot).  The call ends merged.
+static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
+                  const int32_t* ru, const int32_t* ri, const int32_t* rj, int64_t* triplets) {
+  const int64_t B = h->cfg.batch_size;
+  if ((int64_t)h->t + n_steps >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  int64_t N = 0;
+  bprmf_epoch_size(h, &N, nullptr);
+  if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
+  const SamplerArgs sa = sampler_args(h);
+  const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  for (int64_t s = 0; s < n_steps;) {
+    int64_t m = n_steps - s;
+    if (la.H > 0) m = std::min<int64_t>(m, std::max<int64_t>(1, h->local_steps - (h->t - h->rep_t)));
+    m = std::min<int64_t>(m, std::max<int64_t>(1, h->dp_steps - (h->t - h->dp_t)));
+    int64_t a0 = s * B, a1 = (s + m) * B;  // replay: positions in ru/ri/rj
+    if (!ru) {
+      a0 = std::min(N, (first_step + s) * B);
+      a1 = std::min(N, (first_step + s + m) * B);
+    }
+    if (a1 > a0) {
+      HIPCHK(hogwild(h->geom, ru ? nullptr : &sa, epoch, a0, ru ? ru + a0 : nullptr, ri ? ri + a0 : nullptr,
+                     rj ? rj + a0 : nullptr, a1 - a0, h->P, h->Q, h->hp, h->t, (int)B, h->d_loss, h->d_err,
+                     h->stream, la.H > 0 ? &la : nullptr, h->cfg.world));
+      if (!ru) *triplets += a1 - a0;
+    }
+    h->t += (int32_t)m;
+    s += m;
+    if (h->t - h->dp_t >= h->dp_steps || s >= n_steps) {
+      if (int r = dp_merge(h)) return r;
+    } else if (la.H > 0 && h->t - h->rep_t >= h->local_steps) {
+      HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
+      h->rep_t = h->t;
+    }
+  }
+  return 0;
+}
+
 }  // namespace bprmf
 
 using namespace bprmf;
@@ -787,6 +906,8 @@ int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id) {
 
 int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
   if (!h || !blob) return fail(BPRMF_E_INVALID, "null argument");
+  if (dp_items(h->cfg))
+    return fail(BPRMF_E_UNSUPPORTED, "local semantics at world > 1: use the rccl transport");
   if (int r = set_dev(h)) return r;
   static_assert(sizeof(hipIpcMemHandle_t) * kIpcHandles <= BPRMF_IPC_BLOB_BYTES, "blob size");
   auto* tr = new IpcTransport();
@@ -851,6 +972,7 @@ int bprmf_dist_init_loopback(bprmf_handle* h, int64_t group) {
       g->world = h->cfg.world;
       g->send.assign(h->cfg.world, nullptr);
       g->val.assign(h->cfg.world, 0);
+      g->fbuf.assign(h->cfg.world, nullptr);
     }
     if (g->world != h->cfg.world) {
       delete tr;
@@ -880,6 +1002,12 @@ int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, 
   if (!h->dist || !h->dist->tr->ready())
     return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
   if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
+  if (dp_items(h->cfg)) {  // LOCAL at world > 1
+    if (int r = begin_call(h)) return r;
+    int64_t trip = 0;
+    if (int r = dp_run(h, epoch, first_step, n_steps, nullptr, nullptr, nullptr, &trip)) return r;
+    return end_call(h, st, trip, n_steps);
+  }
   // one rank: nothing to exchange, so the single-GPU fused step runs (the same sampler stream,
   // the same step; BPRMF_DIST_W1_RUNNER=1 keeps the runner, to measure it)
   if (h->cfg.world == 1 && !h->dist->tr->self_exchange) {
@@ -926,7 +1054,12 @@ int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i,
     HIPCHK(hipMemcpyAsync(tu, u + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(ti, i + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(tj, j + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
-    if (int r = dist_chunk(h, 0, 0, m, tu, ti, tj)) return r;
+    if (dp_items(h->cfg)) {
+      int64_t unused = 0;
+      if (int r = dp_run(h, 0, 0, m, tu, ti, tj, &unused)) return r;
+    } else if (int r = dist_chunk(h, 0, 0, m, tu, ti, tj)) {
+      return r;
+    }
     HIPCHK(hipStreamSynchronize(h->stream));  // the next chunk's copies reuse d_trip
   }
   return end_call(h, st, valid, n_steps);

@@ -35,6 +35,8 @@ constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th st
 
 struct DistState;  // dist.cpp: the sharded runner's transport, plan and exchange buffers
 void dist_free(DistState* d);
+// semantics LOCAL at world > 1 (dist.cpp): the item table on every rank (not sharded)
+inline bool dp_items(const bprmf_config& c) { return c.semantics == BPRMF_SEM_LOCAL && c.world > 1; }
 
 }  // namespace bprmf
 
@@ -72,6 +74,12 @@ struct bprmf_handle {
   int64_t hot_H = 0;
   int32_t rep_t = 0;              // the step every replica row is current at (the last merge)
   int32_t local_steps = 16;       // steps per period (cfg.local_steps)
+  // BPRMF_SEM_LOCAL at world > 1 (dist.cpp dp_merge): the whole item table on every rank, merged
+  // across ranks every dp_steps steps and at the end of every call
+  float* d_qbase = nullptr;  // [I][ld] the table at the last merge (current at dp_t)
+  float* d_qdelta = nullptr; // [I][ld] this rank's change since then (the all-reduce's buffer)
+  int32_t dp_t = 0;
+  int32_t dp_steps = 64;
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
                                                     const int32_t* __restrict__ tj, int64_t n,
                                                     Table P, Table Q, Hyper hp, int ld, int32_t t0,
                                                     int B, int tpw, int fl, double* __restrict__ loss,
-                                                    int32_t* __restrict__ err, LocalArgs la = LocalArgs{}) {
+                                                    int32_t* __restrict__ err, LocalArgs la = LocalArgs{},
+                                                    int uw = 1) {
   constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round and unroll step
   constexpr int UNR = SERIAL ? 1 : kHwUnroll;
   constexpr int STEP = GPW * UNR;
@@ -273,9 +274,18 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
         mi = ti[s];
         mj = tj[s];
       }
-      // single-GPU handles only (world 1): ids are rows.  A sampler that found no negative
-      // (j = -1) has raised err bit 2; any other bad id raises bit 1.  Either way: skipped.
-      if (mu < 0 || mu >= P.rows || mi < 0 || mi >= Q.rows || mj < 0 || mj >= Q.rows) {
+      // world 1: ids are rows.  uw > 1 (semantics "local" at world uw): items are rows (every
+      // rank holds the whole item table), a user's row is u / uw, and a replayed u < 0 is an
+      // empty slot.  A sampler that found no negative (j = -1) has raised err bit 2; any other
+      // bad id raises bit 1.  Either way: skipped.
+      bool empty = false;
+      if (uw > 1) {
+        if (mu >= 0) mu /= uw;
+        else empty = !SAMPLE;
+      }
+      if (empty) {
+        mu = -1;
+      } else if (mu < 0 || mu >= P.rows || mi < 0 || mi >= Q.rows || mj < 0 || mj >= Q.rows) {
         if (mj >= 0 || !SAMPLE) atomicOr(err, 1);
         mu = -1;
       } else if (LOCAL) {  // the items' replica slots, looked up once by the sampling lane
@@ -375,6 +385,82 @@ hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_
   return hipGetLastError();
 }
 
+// semantics "local" at world > 1: a rank's change of the item table since the
+// last merge at step tm (when every row equalled `base`): delta = row brought to t1 - base decayed
+// to t1.  Flat over the table's float4s; a row's stamp read once per float4 (L2-resident).
+__global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, const float* __restrict__ base,
+                                                     float* __restrict__ delta, int64_t n4, int q4,
+                                                     Hyper hp, int32_t tm, int32_t t1) {
+  const float fb = decay_pow(hp.log2a, t1 - tm);
+  const float4* w = reinterpret_cast<const float4*>(Q.W);
+  const float4* b = reinterpret_cast<const float4*>(base);
+  float4* d = reinterpret_cast<float4*>(delta);
+  for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < n4; x += (int64_t)gridDim.x * kBlock) {
+    const float f = decay_pow(hp.log2a, t1 - Q.stamp[x / q4]);
+    const float4 v = w[x], o = b[x];
+    d[x] = make_float4(fmaf(v.x, f, -(o.x * fb)), fmaf(v.y, f, -(o.y * fb)), fmaf(v.z, f, -(o.z * fb)),
+                       fmaf(v.w, f, -(o.w * fb)));
+  }
+}
+
+// the merge: row = base = base decayed to t1 + the ranks' summed deltas, current at t1
+__global__ __launch_bounds__(kBlock) void k_dp_apply(Table Q, float* __restrict__ base,
+                                                     const float* __restrict__ sum, int64_t n4, int q4,
+                                                     Hyper hp, int32_t tm, int32_t t1) {
+  const float fb = decay_pow(hp.log2a, t1 - tm);
+  float4* w = reinterpret_cast<float4*>(Q.W);
+  float4* b = reinterpret_cast<float4*>(base);
+  const float4* s = reinterpret_cast<const float4*>(sum);
+  for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < n4; x += (int64_t)gridDim.x * kBlock) {
+    const float4 o = b[x], a = s[x];
+    const float4 nv = make_float4(fmaf(o.x, fb, a.x), fmaf(o.y, fb, a.y), fmaf(o.z, fb, a.z), fmaf(o.w, fb, a.w));
+    w[x] = nv;
+    b[x] = nv;
+    if (x % q4 == 0) Q.stamp[x / q4] = t1;
+  }
+}
+
+// the in-process transport's all-reduce: the ranks' deltas summed in rank order (the same bits on
+// every rank)
+__global__ __launch_bounds__(kBlock) void k_dp_sum(DpSrcs src, int world, float* __restrict__ out, int64_t n4) {
+  for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < n4; x += (int64_t)gridDim.x * kBlock) {
+    float4 a = reinterpret_cast<const float4*>(src.p[0])[x];
+    for (int p = 1; p < world; ++p) {
+      const float4 v = reinterpret_cast<const float4*>(src.p[p])[x];
+      a = make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+    }
+    reinterpret_cast<float4*>(out)[x] = a;
+  }
+}
+
+static unsigned dp_blocks(int64_t n4) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + kBlock - 1) / kBlock, 8192));
+}
+
+hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
+                    int32_t t1, hipStream_t s) {
+  const int64_t n4 = Q.rows * (int64_t)(ld / 4);
+  if (n4 <= 0 || ld % 4) return ld % 4 ? hipErrorInvalidValue : hipSuccess;
+  k_dp_delta<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, delta, n4, ld / 4, hp, tm, t1);
+  return hipGetLastError();
+}
+
+hipError_t dp_apply(Table Q, float* base, const float* sum, int ld, const Hyper& hp, int32_t tm,
+                    int32_t t1, hipStream_t s) {
+  const int64_t n4 = Q.rows * (int64_t)(ld / 4);
+  if (n4 <= 0 || ld % 4) return ld % 4 ? hipErrorInvalidValue : hipSuccess;
+  k_dp_apply<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, sum, n4, ld / 4, hp, tm, t1);
+  return hipGetLastError();
+}
+
+hipError_t dp_sum(const DpSrcs& src, int world, float* out, int64_t n, hipStream_t s) {
+  if (world < 1 || world > kMaxWorld || n % 4) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  if (n4 <= 0) return hipSuccess;
+  k_dp_sum<<<dp_blocks(n4), kBlock, 0, s>>>(src, world, out, n4);
+  return hipGetLastError();
+}
+
 static bool hw_serial() {
   const char* e = getenv("BPRMF_HOGWILD_SERIAL");
   return e && e[0] == '1';
@@ -395,8 +481,9 @@ static int hw_tpw(int64_t n) {
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
                    Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
-                   hipStream_t s, const LocalArgs* lap) {
+                   hipStream_t s, const LocalArgs* lap, int uw) {
   if (n <= 0) return hipSuccess;
+  if (uw < 1) return hipErrorInvalidValue;
   const bool serial = hw_serial();
   const int tpw = serial ? 64 : hw_tpw(n);
   const int64_t waves = (n + tpw - 1) / tpw;
@@ -434,32 +521,32 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
     BPRMF_DISPATCH4(g, ({
       if (serial && sa)
         k_hogwild<G4_, S_, true, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
-                                                                  hp, g.ld, t0, B, tpw, fl, loss, err, la);
+                                                                  hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
       else if (serial)
         k_hogwild<G4_, S_, false, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
-                                                                   hp, g.ld, t0, B, tpw, fl, loss, err, la);
+                                                                   hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
       else if (sa)
         k_hogwild<G4_, S_, true, false, true><<<(unsigned)blocks, threads, 0, s>>>(
-            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la);
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
       else
         k_hogwild<G4_, S_, false, false, true><<<(unsigned)blocks, threads, 0, s>>>(
-            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la);
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
     }));
     return hipGetLastError();
   }
   BPRMF_DISPATCH4(g, ({
     if (serial && sa)
       k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                          g.ld, t0, B, tpw, fl, loss, err);
+                                                          g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
     else if (serial)
       k_hogwild<G4_, S_, false, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                           g.ld, t0, B, tpw, fl, loss, err);
+                                                           g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
     else if (sa)
       k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
     else
       k_hogwild<G4_, S_, false, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
   }));
   return hipGetLastError();
 }

@@ -243,7 +243,7 @@ struct LocalArgs;
 hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
                    Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
-                   hipStream_t s, const LocalArgs* la = nullptr);
+                   hipStream_t s, const LocalArgs* la = nullptr, int user_world = 1);
 // semantics "local" (hogwild.hip): the hot items' rows in one replica per XCD
 // (rep [8][H][ld]; hot[item] = replica slot or -1), merged every period: the base row (stamp
 // t0) decayed to t1 plus every replica's change, then copied back into the replicas
@@ -255,6 +255,18 @@ struct LocalArgs {
 constexpr int kLocalXcds = 8;
 hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_t* rows,
                        const Hyper& hp, int32_t t0, int32_t t1, bool refresh, hipStream_t s);
+// semantics "local" at world > 1 (hogwild.hip): every rank holds the whole item
+// table; at a merge (steps tm -> t1) each rank's change is delta = row at t1 - base decayed to t1
+// (base: the table at the last merge, current at tm), the ranks' deltas are summed, and every
+// rank's row and base become base decayed to t1 + that sum (stamp t1).  Flat over [rows][ld].
+hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
+                    int32_t t1, hipStream_t s);
+hipError_t dp_apply(Table Q, float* base, const float* sum, int ld, const Hyper& hp, int32_t tm,
+                    int32_t t1, hipStream_t s);
+struct DpSrcs {  // the ranks' delta tables, rank order (in-process transport)
+  const float* p[kMaxWorld];
+};
+hipError_t dp_sum(const DpSrcs& src, int world, float* out, int64_t n, hipStream_t s);
 // scoring of the current weights after T steps (reads apply the pending decay)
 hipError_t score(const Geom& g, const int32_t* u, const int32_t* i, int64_t n, Table P, Table Q,
                  const Hyper& hp, int32_t T, float* out, int32_t* err, hipStream_t s);

@@ -56,13 +56,17 @@ class BPRMF:
     step; faster, nondeterministic; see DESIGN.md §5b for its HR@10 / NDCG@10 against exact).
     `semantics="local"`: hogwild for users and cold items, the hot items trained in one replica
     per XCD and merged every `local_steps` steps (default 16; bounded staleness).
+    With world > 1 and `semantics="local"` the handle keeps its users' rows but the WHOLE item
+    table, merged with the other ranks every `dp_steps` steps (default 64) and at every call's end
+    (sharded.ShardedBPRMF drives it).
     `step="atomic"` sums duplicate rows with f32 atomics instead of the sorted one-writer sums
     (any batch size; the reference step up to fp32 summation order, not bitwise reproducible).
     """
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, epochs=20, init_std=0.01, seed=0, device=0, rank=0, world=1,
-                 verbose=False, semantics="exact", step="segmented", local_steps=0):
+                 verbose=False, semantics="exact", step="segmented", local_steps=0,
+                 dp_steps=0):
         self.user_num, self.item_num = int(user_num), int(item_num)
         self.factor_num = int(factor_num)
         self.lr, self.wd = float(lr), float(wd)
@@ -84,7 +88,8 @@ class BPRMF:
                           batch_size=self.batch_size, num_ng=self.num_ng, init_std=float(init_std),
                           seed=self.seed & (2**64 - 1), device=self.device, rank=self.rank,
                           world=self.world, semantics=SEMANTICS[semantics],
-                          step_mode=STEP_MODES[step], local_steps=int(local_steps))
+                          step_mode=STEP_MODES[step], local_steps=int(local_steps),
+                          dp_steps=int(dp_steps))
         h = ctypes.c_void_p()
         _lib.check(L.bprmf_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

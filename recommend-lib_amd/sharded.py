@@ -143,11 +143,12 @@ class HipShard:
     """One shard's state in HBM and its step phases (include/bprmf.h, bprmf_dist_*)."""
 
     def __init__(self, user_num, item_num, factor_num, lr, wd, batch_size, num_ng, init_std, seed,
-                 device, rank, world):
+                 device, rank, world, semantics="exact", local_steps=0, dp_steps=0):
         from .model import BPRMF
         self.m = BPRMF(user_num, item_num, factor_num, lr=lr, wd=wd, batch_size=batch_size,
                        num_ng=num_ng, init_std=init_std, seed=seed, device=device, rank=rank,
-                       world=world)
+                       world=world, semantics=semantics, local_steps=local_steps,
+                       dp_steps=dp_steps)
         self.L, self.h = _lib.load(), self.m.handle
         ld = ctypes.c_int32()
         _lib.check(self.L.bprmf_row_stride(self.h, ctypes.byref(ld)))
@@ -267,18 +268,25 @@ class HipShard:
 # ------------------------------------------------------------------------------------------------
 class ShardedBPRMF:
     """One rank of a sharded BPR-MF run.  `comm`: TorchComm (default, one process per GPU) or a
-    ThreadComm; `backend`: the shard's compute (HipShard by default)."""
+    ThreadComm; `backend`: the shard's compute (HipShard by default).
+
+    semantics="local" (opt-in, not the reference step): users stay sharded but
+    every rank holds and trains the WHOLE item table with the single-GPU local step, and the ranks'
+    tables are merged (decayed base + the sum of the ranks' changes; one all-reduce) every
+    `dp_steps` steps and at the end of every call.  Runner only (attach_runner "rccl" or
+    "loopback"); get_weights / set_weights then take (P_local, Q_full)."""
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, init_std=0.01, seed=0, device=0, group=None, comm=None, backend=None,
-                 chunk_steps=256):
+                 chunk_steps=256, semantics="exact", local_steps=0, dp_steps=0):
         self.comm = comm if comm is not None else TorchComm(group)
         self.rank, self.world = self.comm.rank, self.comm.world
         self.user_num, self.item_num, self.factor_num = int(user_num), int(item_num), int(factor_num)
         self.batch_size = int(batch_size)
+        self.semantics = semantics
         self.b = backend if backend is not None else HipShard(
             user_num, item_num, factor_num, lr, wd, batch_size, num_ng, init_std, seed, device,
-            self.rank, self.world)
+            self.rank, self.world, semantics, local_steps, dp_steps)
         self.ld = self.b.ld
         self.device = self.b.device
         self.chunk_steps = int(chunk_steps)
@@ -346,6 +354,8 @@ class ShardedBPRMF:
             self.b.runner_rccl(uid)
         elif transport == "ipc":
             self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
+        elif transport == "auto" and self.semantics == "local":
+            return self.attach_runner("rccl")  # the item merge is an all-reduce
         elif transport == "auto":  # ipc where every rank can map its peers, else rccl
             # Every rank joins every collective whatever failed locally: a status byte travels
             # with the handles, so a rank whose export failed cannot leave its peers waiting in
@@ -442,7 +452,8 @@ class ShardedBPRMF:
 
     # -- weights / measurement --------------------------------------------------------------------
     def get_weights(self):
-        """This shard's (P_local, Q_local): global user = local*world + rank, same for items."""
+        """This shard's (P_local, Q_local): global user = local*world + rank, same for items
+        (semantics "local": Q is the whole item table, the same on every rank)."""
         return self.b.get_weights()
 
     def set_weights(self, P_local, Q_local):

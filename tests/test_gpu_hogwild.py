@@ -229,6 +229,10 @@ def test_parallel_local_trains_ml100k_protocol(rl):
         assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)
 
 
-def test_local_rejects_sharded_handles(rl):
+def test_local_sharded_handle_holds_every_item(rl):
+    """semantics "local" at world > 1 (tests/test_gpu_local_dp.py): the rank keeps
+    its users' rows and the whole item table, and trains through the runner only."""
+    m = rl.BPRMF(10, 10, 8, rank=1, world=2, semantics="local")
+    assert m.local_rows() == (5, 10)
     with pytest.raises(Exception):
-        rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="local")
+        m.train_triplets(np.array([1]), np.array([0]), np.array([2]))

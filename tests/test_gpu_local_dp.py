@@ -1,0 +1,145 @@
+"""GPU: semantics "local" at world > 1 (csrc/dist.cpp dp_run / dp_merge): users
+sharded, the whole item table on every rank, the ranks' tables merged every dp_steps steps and at
+every call's end.  Opt-in, NOT the reference step.  Several ranks share the box's one GPU through
+the in-process loopback transport (its all-reduce sums the ranks' deltas in rank order).
+
+What is pinned:
+  * the arithmetic, by the SERIAL build (BPRMF_HOGWILD_SERIAL=1: one lane group per rank, slot
+    order) against oracle/bpr_oracle.py:local_dp_serial, replayed, at worlds 2 and 3, with hot
+    items, XCD periods shorter than, equal to and longer than the merge period;
+  * every rank ends a call with the same item table, bit for bit;
+  * the sampled parallel mode trains (loss falls, weights finite) and its epoch covers each rank's
+    own positives once.
+Tolerance: the serial GPU against the float64-dot oracle, as tests/test_gpu_hogwild.py (HOG_ATOL),
+a few ulp per update; the merge's decays are exp2 of fp32 products on both sides."""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import bpr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HOG_ATOL = 2e-6
+
+
+def _threads(rl, world, fn):
+    grp = rl.sharded.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            out[r] = fn(rl.sharded.ThreadComm(grp, r), r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    assert all(not t.is_alive() for t in ts), "rank threads did not finish"
+    return out
+
+
+def _hot_set(pos, r, world, I, H):
+    """local_setup's hot items of rank r: the top H by this rank's positive count, ties by id."""
+    mine = pos[pos[:, 0] % world == r]
+    cnt = np.bincount(mine[:, 1], minlength=I)
+    return [int(x) for x in np.argsort(-cnt, kind="stable")[:H]]
+
+
+@pytest.mark.parametrize("world,period,dp", [(2, 2, 3), (3, 3, 3), (2, 5, 2)])
+def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, dp):
+    monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
+    H = 5
+    monkeypatch.setenv("BPRMF_LOCAL_HOT", str(H))
+    g = np.random.default_rng(10 * world + period + dp)
+    U, I, d, B, steps = 31, 29, 32, 16, 7
+    lr, wd = 0.05, 0.01
+    # positives with a clear popularity order per rank (hot sets differ across ranks)
+    rows = [(u, it) for u in range(U) for it in range(I) if g.random() < 0.25 / (1 + it % 7)]
+    pos = np.unique(np.array(rows, np.int64), axis=0)
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    trips = []
+    for r in range(world):
+        users = np.arange(r, U, world)
+        u = g.choice(users, steps * B)
+        i, j = g.integers(0, I, steps * B), g.integers(0, I, steps * B)
+        i[::4] = 0   # popular items often (hot on every rank)
+        j[1::6] = 1
+        j[:5] = i[:5]  # i == j
+        trips.append((u, i, j))
+    # global batches: each rank's share of step k is exactly its B triplets
+    batches = [tuple(np.concatenate([trips[r][x][k * B:(k + 1) * B] for r in range(world)])
+                     for x in range(3)) for k in range(steps)]
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, device=0, comm=comm,
+                            semantics="local", local_steps=period, dp_steps=dp)
+        m.set_train(pos)
+        m.set_weights(sh.shard_rows(P0, r, world), Q0)
+        m.attach_runner("loopback", key=7100 + 10 * world + dp)
+        st = m.train_replay(batches)
+        return m.get_weights(), st
+
+    parts = _threads(rl, world, fn)
+    for r in range(1, world):  # one item table on every rank
+        assert np.array_equal(parts[r][0][1], parts[0][0][1])
+    Pp = [sh.shard_rows(P0, r, world).copy() for r in range(world)]
+    hots = [_hot_set(pos, r, world, I, H) for r in range(world)]
+    loss, sPs, Qw = O.local_dp_serial(Pp, Q0.copy(), trips, lr, wd, B, hots, period, dp, world)
+    a = np.float32(1 - lr * wd)
+    for r in range(world):
+        Pw = Pp[r] * np.power(np.float64(a), (steps - sPs[r]))[:, None].astype(np.float32)
+        np.testing.assert_allclose(parts[r][0][0], Pw, rtol=1e-5, atol=HOG_ATOL)
+    np.testing.assert_allclose(parts[0][0][1], Qw, rtol=1e-5, atol=HOG_ATOL)
+    got = sum(p[1]["loss"] for p in parts)
+    assert got == pytest.approx(loss, rel=1e-5)
+    assert all(p[1]["steps"] == steps for p in parts)
+
+
+def test_local_dp_sampled_trains_and_ranks_agree(rl, golden):
+    """The parallel kernels, sampled, 2 ranks on one GPU: loss falls over epochs, tables finite,
+    both ranks hold the same item table after every call, each epoch's triplets = the rank's own
+    positives x num_ng."""
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    Uu, Ii = int(f["U"]), int(f["I"])
+    world, B = 2, 1024
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(Uu, Ii, 32, lr=0.05, wd=0.001, batch_size=B, seed=3, device=0,
+                            comm=comm, semantics="local", dp_steps=8)
+        S = m.set_train(pos)
+        m.attach_runner("loopback", key=7300)
+        hist, qs = [], []
+        for e in range(4):
+            st = m.train_steps(e, 0, S)
+            hist.append(st)
+            qs.append(m.get_weights()[1])
+        return hist, qs
+
+    parts = _threads(rl, world, fn)
+    for e in range(4):
+        assert np.array_equal(parts[0][1][e], parts[1][1][e])
+        assert np.isfinite(parts[0][1][e]).all()
+    for r in range(world):
+        mine = int((pos[:, 0] % world == r).sum())
+        assert parts[r][0][0]["triplets"] == 4 * mine  # num_ng = 4
+    loss = [sum(parts[r][0][e]["loss"] for r in range(world)) for e in range(4)]
+    assert loss[-1] < 0.9 * loss[0], loss
+
+
+def test_local_dp_refuses_ipc_and_hogwild_stays_single_gpu(rl):
+    sh = rl.sharded
+    m = sh.HipShard(10, 10, 8, 0.01, 0.001, 64, 4, 0.01, 0, 0, 0, 2, "local", 0, 0)
+    with pytest.raises(Exception):
+        m.ipc_export()
+    with pytest.raises(Exception):
+        rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="hogwild")

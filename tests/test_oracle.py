@@ -240,3 +240,40 @@ def test_local_serial_spec_reduces_to_hogwild_and_merges_deltas():
     T = (n + B - 1) // B
     assert sQ[5] == T
     np.testing.assert_allclose(Q3[5], Q[5] * (1 - 0.05 * 0.01) ** T, rtol=1e-6)
+
+
+def test_local_dp_spec_one_rank_is_local_serial_and_ranks_add_changes():
+    """oracle.local_dp_serial (semantics "local" at world > 1): one rank with one merge period is
+    local_serial brought to the end; two ranks whose triplets touch disjoint items each keep their
+    own change (the merge adds the other rank's zero change)."""
+    g = np.random.default_rng(5)
+    U, I, d, B, steps = 20, 24, 8, 8, 6
+    P = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    n = steps * B
+    u, i, j = g.integers(0, U, n), g.integers(0, I, n), g.integers(0, I, n)
+    P1, Q1 = P.copy(), Q.copy()
+    l1, sP1, sQ1 = O.local_serial(P1, Q1, u, i, j, 0.05, 0.01, B, [3, 4], 2)
+    a = np.float32(1 - 0.05 * 0.01)
+    Q1T = Q1 * np.power(np.float64(a), steps - sQ1)[:, None].astype(np.float32)
+    P2 = [P.copy()]
+    l2, sP2, Q2 = O.local_dp_serial(P2, Q.copy(), [(u, i, j)], 0.05, 0.01, B, [[3, 4]], 2, 100, 1)
+    assert l2 == pytest.approx(l1, rel=1e-12)
+    np.testing.assert_array_equal(sP2[0], sP1)
+    np.testing.assert_allclose(P2[0], P1, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(Q2, Q1T, rtol=1e-6, atol=1e-9)
+    # two ranks on disjoint items (rank 0: items < 12, rank 1: items >= 12), no hot items, no decay
+    tr = []
+    for r in range(2):
+        uu = g.choice(np.arange(r, U, 2), n)
+        ii, jj = g.integers(0, 12, n) + 12 * r, g.integers(0, 12, n) + 12 * r
+        tr.append((uu, ii, jj))
+    Pp = [P[r::2].copy() for r in range(2)]
+    _, _, Qm = O.local_dp_serial(Pp, Q.copy(), tr, 0.05, 0.0, B, [[], []], 3, 2, 2)
+    for r in range(2):  # each rank alone on its half of the items
+        Pr, Qr = P[r::2].copy(), Q.copy()
+        for t0 in range(0, steps, 2):
+            sl = slice(t0 * B, (t0 + 2) * B)
+            O.local_serial(Pr, Qr, tr[r][0][sl] // 2, tr[r][1][sl], tr[r][2][sl], 0.05, 0.0, B, [], 3, t0=t0)
+        half = slice(12 * r, 12 * (r + 1))
+        np.testing.assert_allclose(Qm[half], Qr[half], rtol=1e-5, atol=1e-7)

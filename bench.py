@@ -23,6 +23,9 @@ cpu_baseline: the oracle's C port of the reference step (dense grads + dense wei
   step (measured in the build container) is quoted beside it.
 --semantics hogwild: the opt-in relaxed mode (csrc/hogwild.hip; not the reference step) on the
   same workload, labelled as such in config.semantics; the default line is the exact step.
+--semantics local: hot items in per-XCD replicas; at N > 1 also the item table
+  replicated on every rank and merged by an RCCL all-reduce every --dp-steps steps (§5d).  Opt-in,
+  labelled; never the headline.
 """
 import argparse
 import importlib
@@ -126,6 +129,8 @@ def main():
                          "hogwild: opt-in relaxed synchronisation (a separate, labelled line)")
     ap.add_argument("--local-steps", type=int, default=0,
                     help="--semantics local: steps between the XCD replicas' merges (0: 16)")
+    ap.add_argument("--dp-steps", type=int, default=0,
+                    help="--semantics local, N > 1: steps between the ranks' item-table merges (0: 64)")
     ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
                     help="exact step's duplicate-row sums: segmented (sorted, one writer per row, "
                          "bitwise reproducible; the headline) or atomic (f32 atomics; a labelled line)")
@@ -147,8 +152,9 @@ def main():
     dist = None
     sharded = world > 1 or a.sharded
     hog = a.semantics in ("hogwild", "local")
-    if hog and sharded:
+    if a.semantics == "hogwild" and sharded:
         raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
+    dpi = a.semantics == "local" and sharded  # users sharded, item table replicated (§5d)
     if a.step == "atomic" and (sharded or hog):
         raise SystemExit("--step atomic is the single-GPU exact step's alternative")
     if sharded:
@@ -178,7 +184,8 @@ def main():
                 done += c
     else:
         m = rl.ShardedBPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed,
-                            device=local)
+                            device=local, semantics=a.semantics, local_steps=a.local_steps,
+                            dp_steps=a.dp_steps)
         n_steps = m.set_train(pos)
         if a.python_orchestration:
             def run(first, k):
@@ -237,6 +244,11 @@ def main():
                 # one rank: the runner dispatches to the single-GPU fused step (nothing to exchange)
                 step_us, what = us["step_graph"], ("world 1: the single-GPU fused step launches (the "
                                                    "runner has no peer to exchange with)")
+            elif "step_graph" in us and dpi:  # one pair per call: periods + merges (per rank)
+                step_us, what = us["step_graph"], ("per rank: k_hogwild<LOCAL> on the rank's users + "
+                                                   "k_local_merge every local_steps + the item-table "
+                                                   "merge (k_dp_delta, all-reduce, k_dp_apply) every "
+                                                   "dp_steps")
             elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
@@ -286,7 +298,10 @@ def main():
             xch = {k: (xs1[k] - xs0[k]) // ns for k in ("row_bytes", "grad_bytes", "id_bytes")}
             xch = {"per_rank_per_step": xch, "peer_links": world - 1, "steps": xs1["steps"] - xs0["steps"],
                    "note": ("bytes this rank sent to its peers per step as the transport moved them "
-                            "(padded to the chunk's exchange capacity; world 1 sends nothing)")}
+                            "(padded to the chunk's exchange capacity; world 1 sends nothing)"
+                            if not dpi else
+                            "grad_bytes: the item-table merges' all-reduce, 2(W-1)/W of the table per "
+                            "merge per rank (a ring's volume), averaged per step")}
         cpu = None
         if not a.no_cpu_baseline and world == 1 and not sharded:
             cpu = cpu_baseline(pos, U, I, d, B)
@@ -299,9 +314,12 @@ def main():
                        "random N(0,0.01^2) init; no dataset download",
                "config": {"workload": "BPR-MF training, ml-20m shape", "users": U, "items": I,
                           **({"local_steps": a.local_steps or 16} if a.semantics == "local" else {}),
+                          **({"dp_steps": a.dp_steps or 64} if dpi else {}),
                           "positives": int(len(pos)), "factor_num": d, "batch_size_per_gpu": B,
                           "global_batch": B * world, "num_ng": 4, "lr": 0.01, "wd": 0.001,
-                          "parallelism": (f"users+items row-sharded x{world}, "
+                          "parallelism": (f"users row-sharded x{world}, item table replicated, merged "
+                                          f"every dp_steps by {m.runner} all-reduce" if dpi else
+                                          f"users+items row-sharded x{world}, "
                                           f"{'python/torch.distributed' if a.python_orchestration else m.runner} exchange"
                                           if sharded else "single GPU"),
                           "semantics": ("relaxed (hogwild: per-triplet lock-free updates, weight decay "

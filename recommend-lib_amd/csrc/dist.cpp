@@ -822,15 +822,17 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
 // with the single-GPU local step (hogwild.hip, hot items in per-XCD replicas) on its own copy of
 // the whole item table; a merge brings every rank's copy to base + the sum of the ranks' changes.
 static int dp_merge(bprmf_handle* h) {
+  // the hot items' XCD replicas are merged inside the delta pass (k_local_merge's rule)
   const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
-  if (la.H > 0 && h->rep_t != h->t)  // the XCD replicas into this rank's table first
-    HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
-  HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, h->geom.ld, h->hp, h->dp_t, h->t, h->stream));
+  HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, h->geom.ld, h->hp, h->dp_t, h->t, la, h->rep_t, h->stream));
   const float* sum = nullptr;
-  if (int r = h->dist->tr->allreduce_sum(h, h->d_qdelta, h->I * (int64_t)h->geom.ld, &sum)) return r;
-  HIPCHK(dp_apply(h->Q, h->d_qbase, sum, h->geom.ld, h->hp, h->dp_t, h->t, h->stream));
-  if (la.H > 0)  // the replicas restart from the merged rows
-    HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->t, h->t, true, h->stream));
+  const int64_t n = h->I * (int64_t)h->geom.ld;
+  if (int r = h->dist->tr->allreduce_sum(h, h->d_qdelta, n, &sum)) return r;
+  // what a ring all-reduce moves per rank (reduce-scatter + all-gather): 2 (W-1)/W of the table
+  const int64_t W = h->cfg.world;
+  h->dist->x_grads += 2 * (W - 1) * (n * (int64_t)sizeof(float)) / W;
+  // the merged rows, and the hot items' replicas restart from them (in the same pass)
+  HIPCHK(dp_apply(h->Q, h->d_qbase, sum, h->geom.ld, h->hp, h->dp_t, h->t, la, h->stream));
   h->rep_t = h->dp_t = h->t;
   return 0;
 }
@@ -847,6 +849,9 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
   if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
   const SamplerArgs sa = sampler_args(h);
   const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;  // one pair: the periods and the merges
+  if (ea) HIPCHK(hipEventRecord(ea, h->stream));
+  h->dist->x_steps += n_steps;
   for (int64_t s = 0; s < n_steps;) {
     int64_t m = n_steps - s;
     if (la.H > 0) m = std::min<int64_t>(m, std::max<int64_t>(1, h->local_steps - (h->t - h->rep_t)));
@@ -869,6 +874,14 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
     } else if (la.H > 0 && h->t - h->rep_t >= h->local_steps) {
       HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
       h->rep_t = h->t;
+    }
+  }
+  if (ea) {
+    hipEvent_t eb = prof_event(h);
+    if (eb) {
+      HIPCHK(hipEventRecord(eb, h->stream));
+      h->prof_rec[BPRMF_KPROF_STEPS].push_back({ea, eb});
+      h->prof_weight[BPRMF_KPROF_STEPS] += n_steps - 1;
     }
   }
   return 0;

@@ -387,36 +387,69 @@ hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_
 
 // semantics "local" at world > 1: a rank's change of the item table since the
 // last merge at step tm (when every row equalled `base`): delta = row brought to t1 - base decayed
-// to t1.  Flat over the table's float4s; a row's stamp read once per float4 (L2-resident).
+// to t1.  Flat over the table's float4s (q4 per row; 32-bit index arithmetic: the launcher checks
+// the table has fewer than 2^32 float4s); a row's stamp is read once per float4 (L2-resident).
+// A hot item (la.H > 0) is first merged from its per-XCD replicas exactly as k_local_merge does
+// over the period rep_t -> t1 (the merged value is only needed here: k_dp_apply rewrites every row).
 __global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, const float* __restrict__ base,
-                                                     float* __restrict__ delta, int64_t n4, int q4,
-                                                     Hyper hp, int32_t tm, int32_t t1) {
+                                                     float* __restrict__ delta, uint32_t n4, uint32_t q4,
+                                                     Hyper hp, int32_t tm, int32_t t1, LocalArgs la,
+                                                     int32_t rep_t) {
   const float fb = decay_pow(hp.log2a, t1 - tm);
+  const float fk = decay_pow(hp.log2a, t1 - rep_t);
   const float4* w = reinterpret_cast<const float4*>(Q.W);
   const float4* b = reinterpret_cast<const float4*>(base);
   float4* d = reinterpret_cast<float4*>(delta);
-  for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < n4; x += (int64_t)gridDim.x * kBlock) {
-    const float f = decay_pow(hp.log2a, t1 - Q.stamp[x / q4]);
-    const float4 v = w[x], o = b[x];
-    d[x] = make_float4(fmaf(v.x, f, -(o.x * fb)), fmaf(v.y, f, -(o.y * fb)), fmaf(v.z, f, -(o.z * fb)),
-                       fmaf(v.w, f, -(o.w * fb)));
+  for (uint32_t x = blockIdx.x * kBlock + threadIdx.x; x < n4; x += gridDim.x * kBlock) {
+    const uint32_t row = x / q4;
+    const int32_t st = Q.stamp[row];
+    const int32_t slot = la.H > 0 ? la.hot[row] : -1;
+    float4 v = w[x];
+    if (slot >= 0) {  // k_local_merge's rule: fma(b0, fk, sum over XCDs of (replica - b0))
+      const float f0 = decay_pow(hp.log2a, rep_t - st);
+      const float4 b0 = make_float4(v.x * f0, v.y * f0, v.z * f0, v.w * f0);
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      const uint32_t col = x - row * q4;
+#pragma unroll
+      for (int r = 0; r < kLocalXcds; ++r) {
+        const float4 rv = reinterpret_cast<const float4*>(la.rep)[((int64_t)r * la.H + slot) * q4 + col];
+        acc = make_float4(acc.x + (rv.x - b0.x), acc.y + (rv.y - b0.y), acc.z + (rv.z - b0.z),
+                          acc.w + (rv.w - b0.w));
+      }
+      v = make_float4(fmaf(b0.x, fk, acc.x), fmaf(b0.y, fk, acc.y), fmaf(b0.z, fk, acc.z),
+                      fmaf(b0.w, fk, acc.w));
+    } else {
+      const float f = decay_pow(hp.log2a, t1 - st);
+      v = make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
+    }
+    const float4 o = b[x];
+    d[x] = make_float4(v.x - o.x * fb, v.y - o.y * fb, v.z - o.z * fb, v.w - o.w * fb);
   }
 }
 
-// the merge: row = base = base decayed to t1 + the ranks' summed deltas, current at t1
+// the merge: row = base = base decayed to t1 + the ranks' summed deltas, current at t1; a hot
+// item's per-XCD replicas (la.H > 0) restart from it too
 __global__ __launch_bounds__(kBlock) void k_dp_apply(Table Q, float* __restrict__ base,
-                                                     const float* __restrict__ sum, int64_t n4, int q4,
-                                                     Hyper hp, int32_t tm, int32_t t1) {
+                                                     const float* __restrict__ sum, uint32_t n4, uint32_t q4,
+                                                     Hyper hp, int32_t tm, int32_t t1, LocalArgs la) {
   const float fb = decay_pow(hp.log2a, t1 - tm);
   float4* w = reinterpret_cast<float4*>(Q.W);
   float4* b = reinterpret_cast<float4*>(base);
   const float4* s = reinterpret_cast<const float4*>(sum);
-  for (int64_t x = blockIdx.x * (int64_t)kBlock + threadIdx.x; x < n4; x += (int64_t)gridDim.x * kBlock) {
+  for (uint32_t x = blockIdx.x * kBlock + threadIdx.x; x < n4; x += gridDim.x * kBlock) {
+    const uint32_t row = x / q4, col = x - row * q4;
     const float4 o = b[x], a = s[x];
     const float4 nv = make_float4(fmaf(o.x, fb, a.x), fmaf(o.y, fb, a.y), fmaf(o.z, fb, a.z), fmaf(o.w, fb, a.w));
     w[x] = nv;
     b[x] = nv;
-    if (x % q4 == 0) Q.stamp[x / q4] = t1;
+    if (col == 0) Q.stamp[row] = t1;
+    if (la.H > 0) {
+      const int32_t slot = la.hot[row];
+      if (slot >= 0)
+#pragma unroll
+        for (int r = 0; r < kLocalXcds; ++r)
+          reinterpret_cast<float4*>(la.rep)[((int64_t)r * la.H + slot) * q4 + col] = nv;
+    }
   }
 }
 
@@ -438,18 +471,21 @@ static unsigned dp_blocks(int64_t n4) {
 }
 
 hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, hipStream_t s) {
+                    int32_t t1, const LocalArgs& la, int32_t rep_t, hipStream_t s) {
   const int64_t n4 = Q.rows * (int64_t)(ld / 4);
-  if (n4 <= 0 || ld % 4) return ld % 4 ? hipErrorInvalidValue : hipSuccess;
-  k_dp_delta<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, delta, n4, ld / 4, hp, tm, t1);
+  if (ld % 4 || n4 >= (1LL << 32)) return hipErrorInvalidValue;
+  if (n4 <= 0) return hipSuccess;
+  k_dp_delta<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, delta, (uint32_t)n4, (uint32_t)(ld / 4), hp, tm, t1,
+                                              la, rep_t);
   return hipGetLastError();
 }
 
 hipError_t dp_apply(Table Q, float* base, const float* sum, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, hipStream_t s) {
+                    int32_t t1, const LocalArgs& la, hipStream_t s) {
   const int64_t n4 = Q.rows * (int64_t)(ld / 4);
-  if (n4 <= 0 || ld % 4) return ld % 4 ? hipErrorInvalidValue : hipSuccess;
-  k_dp_apply<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, sum, n4, ld / 4, hp, tm, t1);
+  if (ld % 4 || n4 >= (1LL << 32)) return hipErrorInvalidValue;
+  if (n4 <= 0) return hipSuccess;
+  k_dp_apply<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, sum, (uint32_t)n4, (uint32_t)(ld / 4), hp, tm, t1, la);
   return hipGetLastError();
 }
 

@@ -260,9 +260,10 @@ hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_
 // (base: the table at the last merge, current at tm), the ranks' deltas are summed, and every
 // rank's row and base become base decayed to t1 + that sum (stamp t1).  Flat over [rows][ld].
 hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, hipStream_t s);
+                    int32_t t1, const LocalArgs& la, int32_t rep_t, hipStream_t s);  // la.H > 0: hot
+                                                                                     // rows from replicas
 hipError_t dp_apply(Table Q, float* base, const float* sum, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, hipStream_t s);
+                    int32_t t1, const LocalArgs& la, hipStream_t s);  // la.H > 0: replicas too
 struct DpSrcs {  // the ranks' delta tables, rank order (in-process transport)
   const float* p[kMaxWorld];
 };

@@ -10,7 +10,12 @@ Workloads:
          HR@10 / NDCG@10 over `--users-eval` users after `--epochs` epochs.  Synthetic data has no
          taste structure beyond item popularity, so this compares the two modes with each other,
          not with any published number.
-Throughput of each run (stats.seconds: host wall clock per epoch call) is printed beside it."""
+Throughput of each run (stats.seconds: host wall clock per epoch call) is printed beside it.
+
+Mode "local_dpW" (e.g. local_dp8): semantics "local" at world W: W ranks, users
+sharded, each with the whole item table, merged every --dp-steps steps; rehearsed as W in-process
+ranks sharing this one GPU (threads + the loopback transport), so its quality is what W GPUs
+would train (its throughput here is not: the ranks share one GPU)."""
 import argparse
 import importlib
 import json
@@ -24,7 +29,47 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def f5(rl, mode, seed):
+def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, **kw):
+    """W ranks of semantics "local" (threads + loopback on this GPU); returns a single-GPU model
+    holding the trained (P, Q) for scoring, the per-epoch loss, seconds and triplets."""
+    import threading
+    sh = rl.sharded
+    grp = sh.ThreadGroup(W)
+    out, errs = [None] * W, []
+
+    def run(r):
+        try:
+            m = sh.ShardedBPRMF(U, I, d, seed=seed, device=0, comm=sh.ThreadComm(grp, r),
+                                semantics="local", dp_steps=dp_steps, **kw)
+            S = m.set_train(pos)
+            m.attach_runner("loopback", key=9100 + W)
+            hist = [m.train_steps(e, 0, S) for e in range(epochs)]
+            out[r] = (m.get_weights(), hist)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(W)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    el = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    P = sh.unshard_rows([o[0][0] for o in out], U)
+    Q = out[0][0][1]
+    m = rl.BPRMF(U, I, d, **{k: v for k, v in kw.items() if k in ("lr", "wd", "batch_size", "num_ng")})
+    m.set_weights(P, Q)
+    m.history = [{"loss": sum(o[1][e]["loss"] for o in out)} for e in range(epochs)]
+    trip = sum(o[1][e]["triplets"] for o in out for e in range(epochs))
+    return m, el, trip
+
+
+def dp_world(mode):
+    return int(mode[len("local_dp"):]) if mode.startswith("local_dp") else 0
+
+
+def f5(rl, mode, seed, dp_steps=64):
     g = os.path.join(ROOT, "tests", "golden")
     with open(os.path.join(g, "hr_ndcg_ml100k.json")) as fh:
         ref = json.load(fh)
@@ -32,11 +77,16 @@ def f5(rl, mode, seed):
     p = ref["protocol"]
     gt = {int(u): set(f["gt_items"][f["gt_ptr"][k]:f["gt_ptr"][k + 1]].tolist())
           for k, u in enumerate(f["gt_users"])}
-    m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
-                 batch_size=p["batch_size"], num_ng=p["num_ng"], seed=seed, semantics=mode)
-    t0 = time.perf_counter()
-    m.fit(f["positives"].astype(np.int64), epochs=p["epochs"])
-    el = time.perf_counter() - t0
+    if dp_world(mode):
+        m, el, _ = train_local_dp(rl, dp_world(mode), int(f["U"]), int(f["I"]), p["factor_num"],
+                                  f["positives"].astype(np.int64), p["epochs"], seed, dp_steps,
+                                  lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"], num_ng=p["num_ng"])
+    else:
+        m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
+                     batch_size=p["batch_size"], num_ng=p["num_ng"], seed=seed, semantics=mode)
+        t0 = time.perf_counter()
+        m.fit(f["positives"].astype(np.int64), epochs=p["epochs"])
+        el = time.perf_counter() - t0
     kpi = rl.metrics.evaluate_topk(m, f["test_data"], gt, p["topk"])
     return dict(workload="f5 ml-100k fo/tfo d=32", mode=mode, seed=seed, epochs=p["epochs"],
                 hr10=round(kpi["hr"], 5), ndcg10=round(kpi["ndcg"], 5),
@@ -44,7 +94,7 @@ def f5(rl, mode, seed):
                 reference=dict(hr10=ref["summary"]["hr"], ndcg10=ref["summary"]["ndcg"]))
 
 
-def ml20m(rl, mode, seed, epochs, n_eval):
+def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64):
     syn = importlib.import_module("recommend-lib_amd.synthetic")
     U, I = 138493, 26744
     pos = syn.make_positives(U, I, 10_000_000, 20261015)
@@ -65,13 +115,17 @@ def ml20m(rl, mode, seed, epochs, n_eval):
                 seen.add(x)
                 cand.append(x)
         lists.append([int(test[u, 1])] + cand)  # the held-out item first
-    m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode)
-    m.set_train(train)
-    secs, trip = 0.0, 0
-    for _ in range(epochs):
-        st = m.train_epoch()
-        secs += st["seconds"]
-        trip += st["triplets"]
+    if dp_world(mode):
+        m, secs, trip = train_local_dp(rl, dp_world(mode), U, I, 128, train, epochs, seed, dp_steps,
+                                       batch_size=4096)
+    else:
+        m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode)
+        m.set_train(train)
+        secs, trip = 0.0, 0
+        for _ in range(epochs):
+            st = m.train_epoch()
+            secs += st["seconds"]
+            trip += st["triplets"]
     p, _ = m.topk_lists(users, lists, 10)
     hit = (p == 0).any(1)
     rank = np.where(p == 0, np.arange(10)[None, :], 99).min(1)
@@ -89,13 +143,17 @@ def main():
     ap.add_argument("--seeds", default="11,12,13")
     ap.add_argument("--which", default="f5,ml20m")
     ap.add_argument("--modes", default="exact,hogwild,local")
+    ap.add_argument("--dp-steps", type=int, default=64, help="local_dpW: steps between item merges")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first)
     rl = importlib.import_module("recommend-lib_amd")
     for w in a.which.split(","):
         for mode in a.modes.split(","):
             for seed in (int(x) for x in a.seeds.split(",")):
-                r = f5(rl, mode, seed) if w == "f5" else ml20m(rl, mode, seed, a.epochs, a.users_eval)
+                r = (f5(rl, mode, seed, a.dp_steps) if w == "f5"
+                     else ml20m(rl, mode, seed, a.epochs, a.users_eval, a.dp_steps))
+                if dp_world(mode):
+                    r["dp_steps"] = a.dp_steps
                 print(json.dumps(r), flush=True)
 
 

@@ -69,4 +69,14 @@ for slot in order:
                             "dur_us": round(float(en - st), 2), "gap_before_us": round(float(gap), 2)})
     prev_end = en
 out["span_us"] = round(float(prev_end), 2)
+# per call: its GPU span, the build, the mean fused body, and the wall clock (the first calls
+# after the warm-up are the bench's timed call)
+per = []
+for tab, t0, w in zip(rows, t0s, walls):
+    end = max(v[1] for v in tab.values())
+    fused = [tab[s][1] - tab[s][0] for s in range(3, 22) if s in tab]
+    per.append({"wall_us": round(w, 1), "span_us": round((end - t0) * 0.01, 2),
+                "build_us": round((tab[0][1] - tab[0][0]) * 0.01, 2) if 0 in tab else None,
+                "fused_mean_us": round(float(np.mean(fused)) * 0.01, 2) if fused else None})
+out["per_call"] = per
 print(json.dumps(out, indent=1))

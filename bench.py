@@ -131,6 +131,8 @@ def main():
                     help="--semantics local: steps between the XCD replicas' merges (0: 16)")
     ap.add_argument("--dp-steps", type=int, default=0,
                     help="--semantics local, N > 1: steps between the ranks' item-table merges (0: 64)")
+    ap.add_argument("--dp-overlap", action="store_true",
+                    help="--semantics local, N > 1: each merge's all-reduce beside the next period")
     ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
                     help="exact step's duplicate-row sums: segmented (sorted, one writer per row, "
                          "bitwise reproducible; the headline) or atomic (f32 atomics; a labelled line)")
@@ -185,7 +187,7 @@ def main():
     else:
         m = rl.ShardedBPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=a.seed,
                             device=local, semantics=a.semantics, local_steps=a.local_steps,
-                            dp_steps=a.dp_steps)
+                            dp_steps=a.dp_steps, dp_overlap=a.dp_overlap)
         n_steps = m.set_train(pos)
         if a.python_orchestration:
             def run(first, k):
@@ -314,7 +316,7 @@ def main():
                        "random N(0,0.01^2) init; no dataset download",
                "config": {"workload": "BPR-MF training, ml-20m shape", "users": U, "items": I,
                           **({"local_steps": a.local_steps or 16} if a.semantics == "local" else {}),
-                          **({"dp_steps": a.dp_steps or 64} if dpi else {}),
+                          **({"dp_steps": a.dp_steps or 64, "dp_overlap": a.dp_overlap} if dpi else {}),
                           "positives": int(len(pos)), "factor_num": d, "batch_size_per_gpu": B,
                           "global_batch": B * world, "num_ng": 4, "lr": 0.01, "wd": 0.001,
                           "parallelism": (f"users row-sharded x{world}, item table replicated, merged "

@@ -53,7 +53,10 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
  * as above; every `dp_steps` steps (default 64) and at the end of every call the ranks' item
  * tables are merged: new = decayed base + sum over ranks of each rank's change since the last
  * merge (one all-reduce of the table, bprmf_dist_init_rccl or _loopback; the IPC transport is
- * not supported).  Staleness across GPUs is bounded by `dp_steps` steps. */
+ * not supported).  Staleness across GPUs is bounded by `dp_steps` steps.
+ * dp_overlap = 1: the all-reduce of a merge runs on a side stream while the next period trains;
+ * its sum is added one period later (the other ranks' changes arrive up to 2 dp_steps late);
+ * the last merge of every call is blocking, so every rank ends a call with the same table. */
 
 /* How an EXACT step sums duplicate rows' gradients ("ship both").  SEGMENTED: the
  * batch is sorted by user and by item and every row is summed by one writer in a fixed order,
@@ -82,6 +85,8 @@ typedef struct {
   int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
   int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 16) */
   int32_t dp_steps;     /* BPRMF_SEM_LOCAL, world > 1: steps between the ranks' item merges (0: 64) */
+  int32_t dp_overlap;   /* BPRMF_SEM_LOCAL, world > 1: 1 = each merge's all-reduce runs beside the
+                           next period (its result lands one period later), 0 = blocking merges */
 } bprmf_config;
 
 typedef struct {

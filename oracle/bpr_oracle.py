@@ -193,7 +193,7 @@ def local_serial(P, Q, u, i, j, lr, wd, B, hot, period, t0=0):
     return loss, sP, sQ
 
 
-def local_dp_serial(P_parts, Q, trips, lr, wd, B, hots, period, dp_period, world):
+def local_dp_serial(P_parts, Q, trips, lr, wd, B, hots, period, dp_period, world, overlap=False):
     """semantics "local" at world > 1 (csrc/dist.cpp dp_run / dp_merge, hogwild.hip k_dp_delta /
     k_dp_apply), each rank run serially on one XCD (the SERIAL test build): the spec, NOT the
     reference step.
@@ -203,6 +203,11 @@ def local_dp_serial(P_parts, Q, trips, lr, wd, B, hots, period, dp_period, world
       every dp_period steps and at the end: each copy is brought to t1 (rows decayed from their
       stamps), delta_r = copy - base * a^(t1 - tm) (base: the table of the last merge, current at
       tm); every copy and the base become base * a^(t1 - tm) + sum of the deltas in rank order.
+      overlap (dp_overlap): at a merge other than the last, the sum is only started; each rank
+      goes on from its own copy.  At the next merge (step t1, the sum started at tp lands): the
+      base becomes base * a^(tp - tm) + sum (current at tp), the copy adds the other ranks' part
+      (sum - delta_r) * a^(t1 - tp), and the new delta is taken against the new base decayed to
+      t1.  The last merge is blocking as above.
     P_parts updated in place, rows current at the returned stamps.  Returns (loss, sPs, Q at T)."""
     log2a = math.log2(1.0 - float(lr) * float(wd))
 
@@ -211,29 +216,47 @@ def local_dp_serial(P_parts, Q, trips, lr, wd, B, hots, period, dp_period, world
 
     steps = len(trips[0][0]) // B
     base = Q.astype(np.float32).copy()
+    copies = [base.copy() for _ in range(world)]
     sPs = [np.zeros(p.shape[0], np.int64) for p in P_parts]
+    pend = None  # (tp, sum, deltas) of a started all-reduce
     loss = 0.0
     tm = 0
-    while tm < steps:
-        t1 = min(steps, tm + dp_period)
+    ts = 0  # the step every copy is current at
+    while ts < steps:
+        t1 = min(steps, ts + dp_period)
+        last = t1 == steps
         mats = []
         for r in range(world):
             Pr = P_parts[r]
-            for x in range(Pr.shape[0]):  # local_serial starts every row at t0 = tm
-                Pr[x] = Pr[x] * dec(tm - sPs[r][x])
-            Qr = base.copy()
-            u, i, j = (np.asarray(v)[tm * B:t1 * B] for v in trips[r])
-            lo, sP, sQ = local_serial(Pr, Qr, u // world, i, j, lr, wd, B, hots[r], period, t0=tm)
+            for x in range(Pr.shape[0]):  # local_serial starts every row at t0 = ts
+                Pr[x] = Pr[x] * dec(ts - sPs[r][x])
+            Qr = copies[r]
+            u, i, j = (np.asarray(v)[ts * B:t1 * B] for v in trips[r])
+            lo, sP, sQ = local_serial(Pr, Qr, u // world, i, j, lr, wd, B, hots[r], period, t0=ts)
             loss += lo
             sPs[r] = sP
-            mats.append(np.stack([Qr[x] * dec(t1 - sQ[x]) for x in range(Qr.shape[0])]))
-        fb = dec(t1 - tm)
-        b = (base * fb).astype(np.float64)
-        acc = np.zeros_like(b)
+            mats.append(np.stack([Qr[x] * dec(t1 - sQ[x]) for x in range(Qr.shape[0])]).astype(np.float64))
+        if pend is not None:
+            tp, ssum, dl = pend
+            g = base.astype(np.float64) * np.float64(dec(tp - tm)) + ssum
+            for r in range(world):
+                mats[r] = mats[r] + (ssum - dl[r]) * np.float64(dec(t1 - tp))
+            base = g.astype(np.float32)
+            tm = tp
+            pend = None
+        gd = base.astype(np.float64) * np.float64(dec(t1 - tm))
+        deltas = [mats[r] - gd for r in range(world)]
+        ssum = np.zeros_like(gd)
         for r in range(world):
-            acc += mats[r].astype(np.float64) - b
-        base = (b + acc).astype(np.float32)
-        tm = t1
+            ssum += deltas[r]
+        if overlap and not last:
+            pend = (t1, ssum, deltas)
+            copies = [mats[r].astype(np.float32) for r in range(world)]
+        else:
+            base = (gd + ssum).astype(np.float32)
+            tm = t1
+            copies = [base.copy() for _ in range(world)]
+        ts = t1
     return loss, sPs, base
 
 

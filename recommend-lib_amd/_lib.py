@@ -27,7 +27,7 @@ class Config(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("device", ctypes.c_int32), ("rank", ctypes.c_int32),
                 ("world", ctypes.c_int32), ("semantics", ctypes.c_int32),
                 ("step_mode", ctypes.c_int32), ("local_steps", ctypes.c_int32),
-                ("dp_steps", ctypes.c_int32)]
+                ("dp_steps", ctypes.c_int32), ("dp_overlap", ctypes.c_int32)]
 
 
 class NcfConfig(ctypes.Structure):  # ncf_config, include/ncf.h

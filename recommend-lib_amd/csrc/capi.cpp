@@ -103,6 +103,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
   if (cfg->local_steps < 0 || cfg->dp_steps < 0)
     return fail(BPRMF_E_INVALID, "local_steps and dp_steps must be >= 0");
+  if (cfg->dp_overlap != 0 && cfg->dp_overlap != 1) return fail(BPRMF_E_INVALID, "dp_overlap must be 0 or 1");
   if (cfg->step_mode != BPRMF_STEP_SEGMENTED && cfg->step_mode != BPRMF_STEP_ATOMIC)
     return fail(BPRMF_E_INVALID, "step_mode must be BPRMF_STEP_SEGMENTED (0) or BPRMF_STEP_ATOMIC (1)");
   if (cfg->step_mode == BPRMF_STEP_ATOMIC && cfg->world != 1)
@@ -112,6 +113,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   h->semantics = cfg->semantics;
   if (cfg->local_steps > 0) h->local_steps = cfg->local_steps;
   if (cfg->dp_steps > 0) h->dp_steps = cfg->dp_steps;
+  h->dp_overlap = cfg->dp_overlap == 1;
   h->geom = g;
   h->hp.lr = cfg->lr;
   h->hp.wd = cfg->weight_decay;
@@ -157,6 +159,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   if (dpi) {
     TRY(dalloc(&h->d_qbase, h->I * ld));
     TRY(dalloc(&h->d_qdelta, h->I * ld));
+    if (h->dp_overlap) TRY(dalloc(&h->d_qsum, h->I * ld));
   }
   // {err, dist words, loss slots[kLossSlots], two call sequence numbers}
   const size_t status_bytes = kSeqCapOff + 8;
@@ -206,7 +209,7 @@ int bprmf_destroy(bprmf_handle* h) {
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
                   h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
-                  h->d_skeys, h->d_qbase, h->d_qdelta};
+                  h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -1007,6 +1010,7 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   if (h->d_qbase) {  // LOCAL at world > 1: the next merge's base (every rank sets the same Q)
     HIPCHK(hipMemcpy(h->d_qbase, h->Q.W, sizeof(float) * h->I * ld, hipMemcpyDeviceToDevice));
     h->dp_t = h->t;
+    h->dp_pending = false;  // (calls end with a blocking merge: no all-reduce is in flight here)
   }
   return local_refresh(h);  // LOCAL: the replicas start from the new rows
 }

@@ -76,6 +76,17 @@ struct Transport {
     (void)out;
     return fail(BPRMF_E_UNSUPPORTED, "this transport has no all-reduce: use rccl (or loopback)");
   }
+  // the same sum, started beside the caller's stream (dp_overlap): into `dst` (or the transport's
+  // scratch, *out says which); allreduce_wait orders the caller's stream after it.  Default: the
+  // blocking form (its result is ready when the call returns).
+  virtual int allreduce_start(bprmf_handle* h, float* buf, float* dst, int64_t n, const float** out) {
+    (void)dst;
+    return allreduce_sum(h, buf, n, out);
+  }
+  virtual int allreduce_wait(bprmf_handle* h) {
+    (void)h;
+    return 0;
+  }
   // exchange() only enqueues stream work (no host synchronisation): hipGraph-capturable
   virtual bool capturable() const { return false; }
   virtual bool ready() const { return true; }
@@ -101,8 +112,14 @@ struct Transport {
 
 struct RcclTransport final : Transport {
   ncclComm_t comm = nullptr;
+  hipStream_t side = nullptr;  // dp_overlap: the all-reduce beside the training stream
+  hipEvent_t ev_in = nullptr, ev_done = nullptr;
   ~RcclTransport() override {
+    if (side) (void)!hipStreamSynchronize(side);
     if (comm) ncclCommDestroy(comm);
+    if (ev_in) (void)!hipEventDestroy(ev_in);
+    if (ev_done) (void)!hipEventDestroy(ev_done);
+    if (side) (void)!hipStreamDestroy(side);
   }
   bool capturable() const override { return true; }
   int exchange(bprmf_handle* h, const Xchg& x) override {
@@ -132,6 +149,23 @@ struct RcclTransport final : Transport {
   int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) override {
     *out = buf;
     if (h->cfg.world > 1) NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm, h->stream));
+    return 0;
+  }
+  int allreduce_start(bprmf_handle* h, float* buf, float* dst, int64_t n, const float** out) override {
+    if (!side) {
+      HIPCHK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(ev_in, h->stream));  // the delta pass has written buf
+    HIPCHK(hipStreamWaitEvent(side, ev_in, 0));
+    NCCLCHK(ncclAllReduce(buf, dst, (size_t)n, ncclFloat, ncclSum, comm, side));
+    HIPCHK(hipEventRecord(ev_done, side));
+    *out = dst;
+    return 0;
+  }
+  int allreduce_wait(bprmf_handle* h) override {
+    if (side) HIPCHK(hipStreamWaitEvent(h->stream, ev_done, 0));
     return 0;
   }
 };
@@ -821,16 +855,34 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
 // (include/bprmf.h BPRMF_SEM_LOCAL.)  Every rank trains its own users' triplets
 // with the single-GPU local step (hogwild.hip, hot items in per-XCD replicas) on its own copy of
 // the whole item table; a merge brings every rank's copy to base + the sum of the ranks' changes.
-static int dp_merge(bprmf_handle* h) {
+// dp_overlap and not the call's last merge: the all-reduce is only started (beside the next
+// period), and lands at the next merge.  Otherwise blocking: every rank leaves with base + sum.
+static int dp_merge(bprmf_handle* h, bool last) {
+  Transport* tr = h->dist->tr;
+  const bool pend = h->dp_pending;
+  if (pend)
+    if (int r = tr->allreduce_wait(h)) return r;
+  const int32_t tp = pend ? h->dp_tp : h->dp_t;
+  const bool start = h->dp_overlap && !last;
   // the hot items' XCD replicas are merged inside the delta pass (k_local_merge's rule)
   const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
-  HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, h->geom.ld, h->hp, h->dp_t, h->t, la, h->rep_t, h->stream));
-  const float* sum = nullptr;
+  HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, pend ? h->dp_sum : nullptr, h->geom.ld, h->hp, h->dp_t, tp,
+                  h->t, la, h->rep_t, start, h->stream));
+  h->dp_t = tp;  // the base is current at tp now
+  h->dp_pending = false;
   const int64_t n = h->I * (int64_t)h->geom.ld;
-  if (int r = h->dist->tr->allreduce_sum(h, h->d_qdelta, n, &sum)) return r;
   // what a ring all-reduce moves per rank (reduce-scatter + all-gather): 2 (W-1)/W of the table
   const int64_t W = h->cfg.world;
   h->dist->x_grads += 2 * (W - 1) * (n * (int64_t)sizeof(float)) / W;
+  if (start) {
+    if (int r = tr->allreduce_start(h, h->d_qdelta, h->d_qsum, n, &h->dp_sum)) return r;
+    h->dp_pending = true;
+    h->dp_tp = h->t;
+    h->rep_t = h->t;  // the rows and replicas went on from this rank's own result
+    return 0;
+  }
+  const float* sum = nullptr;
+  if (int r = tr->allreduce_sum(h, h->d_qdelta, n, &sum)) return r;
   // the merged rows, and the hot items' replicas restart from them (in the same pass)
   HIPCHK(dp_apply(h->Q, h->d_qbase, sum, h->geom.ld, h->hp, h->dp_t, h->t, la, h->stream));
   h->rep_t = h->dp_t = h->t;
@@ -855,7 +907,7 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
   for (int64_t s = 0; s < n_steps;) {
     int64_t m = n_steps - s;
     if (la.H > 0) m = std::min<int64_t>(m, std::max<int64_t>(1, h->local_steps - (h->t - h->rep_t)));
-    m = std::min<int64_t>(m, std::max<int64_t>(1, h->dp_steps - (h->t - h->dp_t)));
+    m = std::min<int64_t>(m, std::max<int64_t>(1, h->dp_steps - (h->t - (h->dp_pending ? h->dp_tp : h->dp_t))));
     int64_t a0 = s * B, a1 = (s + m) * B;  // replay: positions in ru/ri/rj
     if (!ru) {
       a0 = std::min(N, (first_step + s) * B);
@@ -869,8 +921,9 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
     }
     h->t += (int32_t)m;
     s += m;
-    if (h->t - h->dp_t >= h->dp_steps || s >= n_steps) {
-      if (int r = dp_merge(h)) return r;
+    const int32_t since = h->t - (h->dp_pending ? h->dp_tp : h->dp_t);  // steps since the last merge
+    if (since >= h->dp_steps || s >= n_steps) {
+      if (int r = dp_merge(h, s >= n_steps)) return r;
     } else if (la.H > 0 && h->t - h->rep_t >= h->local_steps) {
       HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
       h->rep_t = h->t;

@@ -78,8 +78,15 @@ struct bprmf_handle {
   // across ranks every dp_steps steps and at the end of every call
   float* d_qbase = nullptr;  // [I][ld] the table at the last merge (current at dp_t)
   float* d_qdelta = nullptr; // [I][ld] this rank's change since then (the all-reduce's buffer)
-  int32_t dp_t = 0;
+  int32_t dp_t = 0;             // the step qbase is current at
   int32_t dp_steps = 64;
+  // cfg.dp_overlap: a merge's all-reduce runs beside the next period; its sum (dp_sum, in d_qsum
+  // or the transport's scratch) is added at the next merge, and d_qdelta keeps this rank's part
+  bool dp_overlap = false;
+  bool dp_pending = false;      // an all-reduce was started at step dp_tp and not applied yet
+  int32_t dp_tp = 0;
+  const float* dp_sum = nullptr;
+  float* d_qsum = nullptr;      // [I][ld] the overlapped all-reduce's result (RCCL, out of place)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
   int64_t plan_steps = 0;      // batches of the current sharded plan

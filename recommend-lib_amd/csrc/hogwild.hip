@@ -390,18 +390,23 @@ hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_
 // to t1.  Flat over the table's float4s (q4 per row; 32-bit index arithmetic: the launcher checks
 // the table has fewer than 2^32 float4s); a row's stamp is read once per float4 (L2-resident).
 // A hot item (la.H > 0) is first merged from its per-XCD replicas exactly as k_local_merge does
-// over the period rep_t -> t1 (the merged value is only needed here: k_dp_apply rewrites every row).
-__global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, const float* __restrict__ base,
-                                                     float* __restrict__ delta, uint32_t n4, uint32_t q4,
-                                                     Hyper hp, int32_t tm, int32_t t1, LocalArgs la,
-                                                     int32_t rep_t) {
-  const float fb = decay_pow(hp.log2a, t1 - tm);
+// over the period rep_t -> t1.  pend_sum (dp_overlap, kernels.h dp_delta): the sum started at
+// step tp lands here.  keep: the row and its replicas take the result (the next period starts from
+// it); otherwise k_dp_apply rewrites every row.
+__global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, float* __restrict__ base,
+                                                     float* __restrict__ delta,
+                                                     const float* __restrict__ pend_sum, uint32_t n4,
+                                                     uint32_t q4, Hyper hp, int32_t tm, int32_t tp,
+                                                     int32_t t1, LocalArgs la, int32_t rep_t, int keep) {
+  const float fb = decay_pow(hp.log2a, tp - tm);  // base -> tp
+  const float fc = decay_pow(hp.log2a, t1 - tp);  // tp -> t1
   const float fk = decay_pow(hp.log2a, t1 - rep_t);
-  const float4* w = reinterpret_cast<const float4*>(Q.W);
-  const float4* b = reinterpret_cast<const float4*>(base);
+  float4* w = reinterpret_cast<float4*>(Q.W);
+  float4* b = reinterpret_cast<float4*>(base);
   float4* d = reinterpret_cast<float4*>(delta);
+  const float4* ps = reinterpret_cast<const float4*>(pend_sum);
   for (uint32_t x = blockIdx.x * kBlock + threadIdx.x; x < n4; x += gridDim.x * kBlock) {
-    const uint32_t row = x / q4;
+    const uint32_t row = x / q4, col = x - row * q4;
     const int32_t st = Q.stamp[row];
     const int32_t slot = la.H > 0 ? la.hot[row] : -1;
     float4 v = w[x];
@@ -409,7 +414,6 @@ __global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, const float* __res
       const float f0 = decay_pow(hp.log2a, rep_t - st);
       const float4 b0 = make_float4(v.x * f0, v.y * f0, v.z * f0, v.w * f0);
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      const uint32_t col = x - row * q4;
 #pragma unroll
       for (int r = 0; r < kLocalXcds; ++r) {
         const float4 rv = reinterpret_cast<const float4*>(la.rep)[((int64_t)r * la.H + slot) * q4 + col];
@@ -423,7 +427,23 @@ __global__ __launch_bounds__(kBlock) void k_dp_delta(Table Q, const float* __res
       v = make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
     }
     const float4 o = b[x];
-    d[x] = make_float4(v.x - o.x * fb, v.y - o.y * fb, v.z - o.z * fb, v.w - o.w * fb);
+    float4 g = make_float4(o.x * fb, o.y * fb, o.z * fb, o.w * fb);
+    if (ps) {  // the landed sum: the common table at tp, and the other ranks' part of it
+      const float4 sm = ps[x], od = d[x];
+      g = make_float4(fmaf(o.x, fb, sm.x), fmaf(o.y, fb, sm.y), fmaf(o.z, fb, sm.z), fmaf(o.w, fb, sm.w));
+      v = make_float4(fmaf(sm.x - od.x, fc, v.x), fmaf(sm.y - od.y, fc, v.y), fmaf(sm.z - od.z, fc, v.z),
+                      fmaf(sm.w - od.w, fc, v.w));
+      b[x] = g;
+    }
+    d[x] = make_float4(v.x - g.x * fc, v.y - g.y * fc, v.z - g.z * fc, v.w - g.w * fc);
+    if (keep) {
+      w[x] = v;
+      if (col == 0) Q.stamp[row] = t1;
+      if (slot >= 0)
+#pragma unroll
+        for (int r = 0; r < kLocalXcds; ++r)
+          reinterpret_cast<float4*>(la.rep)[((int64_t)r * la.H + slot) * q4 + col] = v;
+    }
   }
 }
 
@@ -470,13 +490,14 @@ static unsigned dp_blocks(int64_t n4) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + kBlock - 1) / kBlock, 8192));
 }
 
-hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, const LocalArgs& la, int32_t rep_t, hipStream_t s) {
+hipError_t dp_delta(Table Q, float* base, float* delta, const float* pend_sum, int ld, const Hyper& hp,
+                    int32_t tm, int32_t tp, int32_t t1, const LocalArgs& la, int32_t rep_t, bool keep,
+                    hipStream_t s) {
   const int64_t n4 = Q.rows * (int64_t)(ld / 4);
-  if (ld % 4 || n4 >= (1LL << 32)) return hipErrorInvalidValue;
+  if (ld % 4 || n4 >= (1LL << 32) || tp < tm || t1 < tp || (!pend_sum && tp != tm)) return hipErrorInvalidValue;
   if (n4 <= 0) return hipSuccess;
-  k_dp_delta<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, delta, (uint32_t)n4, (uint32_t)(ld / 4), hp, tm, t1,
-                                              la, rep_t);
+  k_dp_delta<<<dp_blocks(n4), kBlock, 0, s>>>(Q, base, delta, pend_sum, (uint32_t)n4, (uint32_t)(ld / 4), hp,
+                                              tm, tp, t1, la, rep_t, keep ? 1 : 0);
   return hipGetLastError();
 }
 

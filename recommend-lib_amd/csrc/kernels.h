@@ -259,9 +259,14 @@ hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_
 // table; at a merge (steps tm -> t1) each rank's change is delta = row at t1 - base decayed to t1
 // (base: the table at the last merge, current at tm), the ranks' deltas are summed, and every
 // rank's row and base become base decayed to t1 + that sum (stamp t1).  Flat over [rows][ld].
-hipError_t dp_delta(Table Q, const float* base, float* delta, int ld, const Hyper& hp, int32_t tm,
-                    int32_t t1, const LocalArgs& la, int32_t rep_t, hipStream_t s);  // la.H > 0: hot
-                                                                                     // rows from replicas
+// dp_delta also brings a hot row from its XCD replicas (la.H > 0, k_local_merge's rule over
+// rep_t -> t1).  pend_sum (dp_overlap): the all-reduce started at the last merge (step tp) has
+// landed: base becomes base decayed to tp + pend_sum, the row takes the other ranks' part
+// (pend_sum - delta, decayed to t1), and delta is taken against the new base.  keep: the row
+// (and a hot row's replicas) keep the result, current at t1 (the next period starts from it).
+hipError_t dp_delta(Table Q, float* base, float* delta, const float* pend_sum, int ld, const Hyper& hp,
+                    int32_t tm, int32_t tp, int32_t t1, const LocalArgs& la, int32_t rep_t, bool keep,
+                    hipStream_t s);
 hipError_t dp_apply(Table Q, float* base, const float* sum, int ld, const Hyper& hp, int32_t tm,
                     int32_t t1, const LocalArgs& la, hipStream_t s);  // la.H > 0: replicas too
 struct DpSrcs {  // the ranks' delta tables, rank order (in-process transport)

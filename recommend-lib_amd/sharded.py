@@ -143,12 +143,13 @@ class HipShard:
     """One shard's state in HBM and its step phases (include/bprmf.h, bprmf_dist_*)."""
 
     def __init__(self, user_num, item_num, factor_num, lr, wd, batch_size, num_ng, init_std, seed,
-                 device, rank, world, semantics="exact", local_steps=0, dp_steps=0):
+                 device, rank, world, semantics="exact", local_steps=0, dp_steps=0,
+                 dp_overlap=False):
         from .model import BPRMF
         self.m = BPRMF(user_num, item_num, factor_num, lr=lr, wd=wd, batch_size=batch_size,
                        num_ng=num_ng, init_std=init_std, seed=seed, device=device, rank=rank,
                        world=world, semantics=semantics, local_steps=local_steps,
-                       dp_steps=dp_steps)
+                       dp_steps=dp_steps, dp_overlap=dp_overlap)
         self.L, self.h = _lib.load(), self.m.handle
         ld = ctypes.c_int32()
         _lib.check(self.L.bprmf_row_stride(self.h, ctypes.byref(ld)))
@@ -273,12 +274,13 @@ class ShardedBPRMF:
     semantics="local" (opt-in, not the reference step): users stay sharded but
     every rank holds and trains the WHOLE item table with the single-GPU local step, and the ranks'
     tables are merged (decayed base + the sum of the ranks' changes; one all-reduce) every
-    `dp_steps` steps and at the end of every call.  Runner only (attach_runner "rccl" or
+    `dp_steps` steps and at the end of every call (`dp_overlap`: each merge's all-reduce runs
+    beside the next period, its sum added one period later).  Runner only (attach_runner "rccl" or
     "loopback"); get_weights / set_weights then take (P_local, Q_full)."""
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, init_std=0.01, seed=0, device=0, group=None, comm=None, backend=None,
-                 chunk_steps=256, semantics="exact", local_steps=0, dp_steps=0):
+                 chunk_steps=256, semantics="exact", local_steps=0, dp_steps=0, dp_overlap=False):
         self.comm = comm if comm is not None else TorchComm(group)
         self.rank, self.world = self.comm.rank, self.comm.world
         self.user_num, self.item_num, self.factor_num = int(user_num), int(item_num), int(factor_num)
@@ -286,7 +288,7 @@ class ShardedBPRMF:
         self.semantics = semantics
         self.b = backend if backend is not None else HipShard(
             user_num, item_num, factor_num, lr, wd, batch_size, num_ng, init_std, seed, device,
-            self.rank, self.world, semantics, local_steps, dp_steps)
+            self.rank, self.world, semantics, local_steps, dp_steps, dp_overlap)
         self.ld = self.b.ld
         self.device = self.b.device
         self.chunk_steps = int(chunk_steps)

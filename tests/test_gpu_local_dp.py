@@ -7,6 +7,7 @@ What is pinned:
   * the arithmetic, by the SERIAL build (BPRMF_HOGWILD_SERIAL=1: one lane group per rank, slot
     order) against oracle/bpr_oracle.py:local_dp_serial, replayed, at worlds 2 and 3, with hot
     items, XCD periods shorter than, equal to and longer than the merge period;
+  * the overlapped schedule (dp_overlap: each merge's sum lands one period later) the same way;
   * every rank ends a call with the same item table, bit for bit;
   * the sampled parallel mode trains (loss falls, weights finite) and its epoch covers each rank's
     own positives once.
@@ -51,8 +52,9 @@ def _hot_set(pos, r, world, I, H):
     return [int(x) for x in np.argsort(-cnt, kind="stable")[:H]]
 
 
-@pytest.mark.parametrize("world,period,dp", [(2, 2, 3), (3, 3, 3), (2, 5, 2)])
-def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, dp):
+@pytest.mark.parametrize("world,period,dp,overlap", [(2, 2, 3, False), (3, 3, 3, False), (2, 5, 2, False),
+                                                     (2, 2, 3, True), (3, 5, 2, True)])
+def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, dp, overlap):
     monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
     H = 5
     monkeypatch.setenv("BPRMF_LOCAL_HOT", str(H))
@@ -80,10 +82,10 @@ def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, d
 
     def fn(comm, r):
         m = sh.ShardedBPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, device=0, comm=comm,
-                            semantics="local", local_steps=period, dp_steps=dp)
+                            semantics="local", local_steps=period, dp_steps=dp, dp_overlap=overlap)
         m.set_train(pos)
         m.set_weights(sh.shard_rows(P0, r, world), Q0)
-        m.attach_runner("loopback", key=7100 + 10 * world + dp)
+        m.attach_runner("loopback", key=7100 + 10 * world + dp + 1000 * overlap)
         st = m.train_replay(batches)
         return m.get_weights(), st
 
@@ -92,7 +94,8 @@ def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, d
         assert np.array_equal(parts[r][0][1], parts[0][0][1])
     Pp = [sh.shard_rows(P0, r, world).copy() for r in range(world)]
     hots = [_hot_set(pos, r, world, I, H) for r in range(world)]
-    loss, sPs, Qw = O.local_dp_serial(Pp, Q0.copy(), trips, lr, wd, B, hots, period, dp, world)
+    loss, sPs, Qw = O.local_dp_serial(Pp, Q0.copy(), trips, lr, wd, B, hots, period, dp, world,
+                                      overlap=overlap)
     a = np.float32(1 - lr * wd)
     for r in range(world):
         Pw = Pp[r] * np.power(np.float64(a), (steps - sPs[r]))[:, None].astype(np.float32)
@@ -103,7 +106,8 @@ def test_local_dp_serial_replay_matches_oracle(rl, monkeypatch, world, period, d
     assert all(p[1]["steps"] == steps for p in parts)
 
 
-def test_local_dp_sampled_trains_and_ranks_agree(rl, golden):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_local_dp_sampled_trains_and_ranks_agree(rl, golden, overlap):
     """The parallel kernels, sampled, 2 ranks on one GPU: loss falls over epochs, tables finite,
     both ranks hold the same item table after every call, each epoch's triplets = the rank's own
     positives x num_ng."""
@@ -115,9 +119,9 @@ def test_local_dp_sampled_trains_and_ranks_agree(rl, golden):
 
     def fn(comm, r):
         m = sh.ShardedBPRMF(Uu, Ii, 32, lr=0.05, wd=0.001, batch_size=B, seed=3, device=0,
-                            comm=comm, semantics="local", dp_steps=8)
+                            comm=comm, semantics="local", dp_steps=8, dp_overlap=overlap)
         S = m.set_train(pos)
-        m.attach_runner("loopback", key=7300)
+        m.attach_runner("loopback", key=7300 + overlap)
         hist, qs = [], []
         for e in range(4):
             st = m.train_steps(e, 0, S)

@@ -268,8 +268,17 @@ def test_local_dp_spec_one_rank_is_local_serial_and_ranks_add_changes():
         uu = g.choice(np.arange(r, U, 2), n)
         ii, jj = g.integers(0, 12, n) + 12 * r, g.integers(0, 12, n) + 12 * r
         tr.append((uu, ii, jj))
+    # the overlapped schedule: one rank, or ranks on disjoint items, see no one else's change
+    P3 = [P.copy()]
+    _, _, Q3 = O.local_dp_serial(P3, Q.copy(), [(u, i, j)], 0.05, 0.01, B, [[3, 4]], 2, 2, 1, overlap=True)
+    P4 = [P.copy()]
+    _, _, Q4 = O.local_dp_serial(P4, Q.copy(), [(u, i, j)], 0.05, 0.01, B, [[3, 4]], 2, 2, 1)
+    np.testing.assert_allclose(Q3, Q4, rtol=1e-5, atol=1e-7)
+    Po = [P[r::2].copy() for r in range(2)]
+    _, _, Qo = O.local_dp_serial(Po, Q.copy(), tr, 0.05, 0.0, B, [[], []], 3, 2, 2, overlap=True)
     Pp = [P[r::2].copy() for r in range(2)]
     _, _, Qm = O.local_dp_serial(Pp, Q.copy(), tr, 0.05, 0.0, B, [[], []], 3, 2, 2)
+    np.testing.assert_allclose(Qo, Qm, rtol=1e-5, atol=1e-7)
     for r in range(2):  # each rank alone on its half of the items
         Pr, Qr = P[r::2].copy(), Q.copy()
         for t0 in range(0, steps, 2):

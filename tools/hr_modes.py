@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, **kw):
+def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, dp_overlap=False, **kw):
     """W ranks of semantics "local" (threads + loopback on this GPU); returns a single-GPU model
     holding the trained (P, Q) for scoring, the per-epoch loss, seconds and triplets."""
     import threading
@@ -40,7 +40,7 @@ def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, **kw):
     def run(r):
         try:
             m = sh.ShardedBPRMF(U, I, d, seed=seed, device=0, comm=sh.ThreadComm(grp, r),
-                                semantics="local", dp_steps=dp_steps, **kw)
+                                semantics="local", dp_steps=dp_steps, dp_overlap=dp_overlap, **kw)
             S = m.set_train(pos)
             m.attach_runner("loopback", key=9100 + W)
             hist = [m.train_steps(e, 0, S) for e in range(epochs)]
@@ -69,7 +69,7 @@ def dp_world(mode):
     return int(mode[len("local_dp"):]) if mode.startswith("local_dp") else 0
 
 
-def f5(rl, mode, seed, dp_steps=64):
+def f5(rl, mode, seed, dp_steps=64, dp_overlap=False):
     g = os.path.join(ROOT, "tests", "golden")
     with open(os.path.join(g, "hr_ndcg_ml100k.json")) as fh:
         ref = json.load(fh)
@@ -80,7 +80,7 @@ def f5(rl, mode, seed, dp_steps=64):
     if dp_world(mode):
         m, el, _ = train_local_dp(rl, dp_world(mode), int(f["U"]), int(f["I"]), p["factor_num"],
                                   f["positives"].astype(np.int64), p["epochs"], seed, dp_steps,
-                                  lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"], num_ng=p["num_ng"])
+                                  dp_overlap, lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"], num_ng=p["num_ng"])
     else:
         m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
                      batch_size=p["batch_size"], num_ng=p["num_ng"], seed=seed, semantics=mode)
@@ -94,7 +94,7 @@ def f5(rl, mode, seed, dp_steps=64):
                 reference=dict(hr10=ref["summary"]["hr"], ndcg10=ref["summary"]["ndcg"]))
 
 
-def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64):
+def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64, dp_overlap=False):
     syn = importlib.import_module("recommend-lib_amd.synthetic")
     U, I = 138493, 26744
     pos = syn.make_positives(U, I, 10_000_000, 20261015)
@@ -117,7 +117,7 @@ def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64):
         lists.append([int(test[u, 1])] + cand)  # the held-out item first
     if dp_world(mode):
         m, secs, trip = train_local_dp(rl, dp_world(mode), U, I, 128, train, epochs, seed, dp_steps,
-                                       batch_size=4096)
+                                       dp_overlap, batch_size=4096)
     else:
         m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode)
         m.set_train(train)
@@ -144,16 +144,18 @@ def main():
     ap.add_argument("--which", default="f5,ml20m")
     ap.add_argument("--modes", default="exact,hogwild,local")
     ap.add_argument("--dp-steps", type=int, default=64, help="local_dpW: steps between item merges")
+    ap.add_argument("--dp-overlap", action="store_true", help="local_dpW: all-reduce beside the next period")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first)
     rl = importlib.import_module("recommend-lib_amd")
     for w in a.which.split(","):
         for mode in a.modes.split(","):
             for seed in (int(x) for x in a.seeds.split(",")):
-                r = (f5(rl, mode, seed, a.dp_steps) if w == "f5"
-                     else ml20m(rl, mode, seed, a.epochs, a.users_eval, a.dp_steps))
+                r = (f5(rl, mode, seed, a.dp_steps, a.dp_overlap) if w == "f5"
+                     else ml20m(rl, mode, seed, a.epochs, a.users_eval, a.dp_steps, a.dp_overlap))
                 if dp_world(mode):
                     r["dp_steps"] = a.dp_steps
+                    r["dp_overlap"] = a.dp_overlap
                 print(json.dumps(r), flush=True)
 
 

@@ -20,6 +20,7 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     dp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    ov = len(sys.argv) > 4 and sys.argv[4] == "overlap"
     import torch  # noqa: F401  (HIP runtime first)
     rl = importlib.import_module("recommend-lib_amd")
     syn = importlib.import_module("recommend-lib_amd.synthetic")
@@ -32,7 +33,8 @@ def main():
     def run(r):
         try:
             m = sh.ShardedBPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, seed=5, device=0,
-                                comm=sh.ThreadComm(grp, r), semantics="local", dp_steps=dp)
+                                comm=sh.ThreadComm(grp, r), semantics="local", dp_steps=dp,
+                                dp_overlap=ov)
             m.set_train(pos)
             m.attach_runner("loopback", key=9300 + W)
             m.train_steps(0, 0, dp)  # warm-up: one merge period
@@ -53,7 +55,7 @@ def main():
     if errs:
         raise errs[0]
     walls = [max(o[0][c] for o in out) for c in range(3)]
-    print(json.dumps({"world": W, "steps_per_call": steps, "dp_steps": dp, "batch_per_rank": B,
+    print(json.dumps({"world": W, "steps_per_call": steps, "dp_steps": dp, "dp_overlap": ov, "batch_per_rank": B,
                       "wall_s_per_call": [round(w, 5) for w in walls],
                       "us_per_step_all_ranks_on_one_gpu": round(min(walls) / steps * 1e6, 2),
                       "note": "W ranks share one GPU: not the W-GPU time"}), flush=True)

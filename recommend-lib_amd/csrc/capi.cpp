@@ -209,7 +209,7 @@ int bprmf_destroy(bprmf_handle* h) {
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
                   h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
-                  h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum};
+                  h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -309,11 +309,15 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   const std::vector<int64_t>& indptr = csr.indptr;
   const std::vector<int32_t>& indices = csr.indices;
   const int64_t n = (int64_t)pu.size();
-  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices, h->d_soff, h->d_skeys};
+  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices, h->d_soff, h->d_skeys, h->d_pos2, h->d_urec};
   for (void* p : olds)
     if (p) HIPCHK(hipFree(p));
   h->d_pos_u = h->d_pos_i = h->d_indices = h->d_skeys = nullptr;
   h->d_indptr = h->d_soff = nullptr;
+  h->d_pos2 = h->d_urec = nullptr;
+  // packed sampler reads (BPRMF_SAMPLE_PACKED=0: the separate arrays, A/B)
+  const char* pk = getenv("BPRMF_SAMPLE_PACKED");
+  const bool packed = !(pk && pk[0] == '0');
   {  // the sampler's search trees (BPRMF_SAMPLE_TREE=0: the binary search, A/B)
     const char* e = getenv("BPRMF_SAMPLE_TREE");
     if (!(e && e[0] == '0')) {
@@ -324,7 +328,20 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
       HIPCHK(hipMemcpy(h->d_soff, st.soff.data(), 8 * st.soff.size(), hipMemcpyHostToDevice));
       if (!st.keys.empty())
         HIPCHK(hipMemcpy(h->d_skeys, st.keys.data(), 4 * st.keys.size(), hipMemcpyHostToDevice));
+      if (packed && st.soff.back() < INT32_MAX) {
+        std::vector<int2> ur(h->U);
+        for (int64_t lu = 0; lu < h->U; ++lu)
+          ur[lu] = make_int2((int32_t)st.soff[lu], (int32_t)(indptr[lu + 1] - indptr[lu]));
+        if (int r = dalloc(&h->d_urec, std::max<int64_t>(1, h->U))) return r;
+        if (h->U) HIPCHK(hipMemcpy(h->d_urec, ur.data(), 8 * ur.size(), hipMemcpyHostToDevice));
+      }
     }
+  }
+  if (packed && !pu.empty()) {
+    std::vector<int2> p2(pu.size());
+    for (size_t k = 0; k < pu.size(); ++k) p2[k] = make_int2(pu[k], pi[k]);
+    if (int r = dalloc(&h->d_pos2, (int64_t)p2.size())) return r;
+    HIPCHK(hipMemcpy(h->d_pos2, p2.data(), 8 * p2.size(), hipMemcpyHostToDevice));
   }
   if (int r = dalloc(&h->d_pos_u, n)) return r;
   if (int r = dalloc(&h->d_pos_i, n)) return r;
@@ -382,6 +399,8 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   a.k1 = h->k1;
   a.skeys = h->d_skeys;
   a.soff = h->d_soff;
+  a.pos2 = h->d_pos2;
+  a.urec = h->d_urec;
   return a;
 }
 

@@ -207,10 +207,29 @@ static __device__ __forceinline__ bool sample_slot(const SamplerArgs& a, uint32_
   const uint64_t q = permute(slot, N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
 #endif
   const int64_t p = div_small(q, (uint32_t)a.num_ng);
-  u = a.pos_u[p];
-  i = a.pos_i[p];
+  if (a.pos2) {  // one 8-byte load: one line per positive instead of two
+    const int2 pr = a.pos2[p];
+    u = pr.x;
+    i = pr.y;
+  } else {
+    u = a.pos_u[p];
+    i = a.pos_i[p];
+  }
   const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
   const int64_t ul = u / a.world;
+  if (a.urec) {  // {first tree key, positive count}: one line per user instead of indptr + soff
+    const int2 ur = a.urec[ul];
+    const int64_t free_u = a.item_num - ur.y;
+    j = -1;
+    if (free_u <= 0) return false;
+    const uint32_t k = bounded_from(d0, q, epoch, (uint32_t)free_u, a.k0, a.k1);
+#if defined(BPRMF_SAMPLE_DIAG) && (BPRMF_SAMPLE_DIAG & 1)  // diagnostic: no search (timing only)
+    j = (int32_t)k;
+#else
+    j = (int32_t)kth_nonmember_tree(a.skeys + ur.x, ur.y, (int64_t)k);
+#endif
+    return true;
+  }
   const int64_t beg = a.indptr[ul], deg = a.indptr[ul + 1] - beg;
   const int64_t free_items = a.item_num - deg;
   j = -1;

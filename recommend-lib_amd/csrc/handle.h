@@ -54,6 +54,8 @@ struct bprmf_handle {
   int32_t* d_indices = nullptr;
   int64_t* d_soff = nullptr;    // the sampler's search trees (host_plan.h SearchTree)
   int32_t* d_skeys = nullptr;
+  int2* d_pos2 = nullptr;       // {pos_u, pos_i} interleaved (the sampler's packed reads)
+  int2* d_urec = nullptr;       // per local user {first tree key, positive count}
   uint32_t feistel_a = 1, feistel_c = 1;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0 = 0, k1 = 0;  // shard sampler key
   // triplet chunk

@@ -134,6 +134,10 @@ struct SamplerArgs {
   // the k-th non-member search's 16-ary trees (host_plan.h SearchTree; null: binary search)
   const int32_t* skeys = nullptr;
   const int64_t* soff = nullptr;
+  // the same data packed so each dependent level is one line (null: the arrays above):
+  // pos2[p] = {pos_u[p], pos_i[p]}; urec[local user] = {its first tree key, its positive count}
+  const int2* pos2 = nullptr;
+  const int2* urec = nullptr;
 };
 
 // --- launches (all asynchronous on `s`) ---

@@ -45,7 +45,7 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
 /* LOCAL (bounded staleness, opt-in): HOGWILD for users and for all but the most popular items;
  * the hot items (the top min(I, 4096) by positive count) are trained in one replica per XCD of the
  * GPU (each XCD's waves see their own XCD's updates at once, the other XCDs' only at the next
- * merge), and every `local_steps` steps (default 16) the replicas are merged: new = decayed base +
+ * merge), and every `local_steps` steps (default 128) the replicas are merged: new = decayed base +
  * sum over XCDs of each replica's change.  Staleness across XCDs is bounded by `local_steps`
  * steps.
  * LOCAL at world > 1 (data-parallel items): users stay sharded (u % world == rank, each rank
@@ -83,7 +83,7 @@ typedef struct {
   int32_t semantics;    /* BPRMF_SEM_EXACT (0, default): the reference's batch-synchronous step;
                            BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
   int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
-  int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 16) */
+  int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 128) */
   int32_t dp_steps;     /* BPRMF_SEM_LOCAL, world > 1: steps between the ranks' item merges (0: 64) */
   int32_t dp_overlap;   /* BPRMF_SEM_LOCAL, world > 1: 1 = each merge's all-reduce runs beside the
                            next period (its result lands one period later), 0 = blocking merges */

@@ -75,7 +75,7 @@ struct bprmf_handle {
   float* d_qrep = nullptr;        // [kLocalXcds][H][ld]
   int64_t hot_H = 0;
   int32_t rep_t = 0;              // the step every replica row is current at (the last merge)
-  int32_t local_steps = 16;       // steps per period (cfg.local_steps)
+  int32_t local_steps = 128;      // steps per period (cfg.local_steps)
   // BPRMF_SEM_LOCAL at world > 1 (dist.cpp dp_merge): the whole item table on every rank, merged
   // across ranks every dp_steps steps and at the end of every call
   float* d_qbase = nullptr;  // [I][ld] the table at the last merge (current at dp_t)

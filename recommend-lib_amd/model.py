@@ -55,7 +55,7 @@ class BPRMF:
     unseeded).  `semantics="hogwild"` opts into relaxed synchronisation (not the reference's
     step; faster, nondeterministic; see DESIGN.md §5b for its HR@10 / NDCG@10 against exact).
     `semantics="local"`: hogwild for users and cold items, the hot items trained in one replica
-    per XCD and merged every `local_steps` steps (default 16; bounded staleness).
+    per XCD and merged every `local_steps` steps (default 128; bounded staleness).
     With world > 1 and `semantics="local"` the handle keeps its users' rows but the WHOLE item
     table, merged with the other ranks every `dp_steps` steps (default 64) and at every call's end
     (sharded.ShardedBPRMF drives it); `dp_overlap=True` runs each merge's

@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, dp_overlap=False, **kw):
+def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, dp_overlap=False, local_steps=0, **kw):
     """W ranks of semantics "local" (threads + loopback on this GPU); returns a single-GPU model
     holding the trained (P, Q) for scoring, the per-epoch loss, seconds and triplets."""
     import threading
@@ -40,7 +40,8 @@ def train_local_dp(rl, W, U, I, d, pos, epochs, seed, dp_steps, dp_overlap=False
     def run(r):
         try:
             m = sh.ShardedBPRMF(U, I, d, seed=seed, device=0, comm=sh.ThreadComm(grp, r),
-                                semantics="local", dp_steps=dp_steps, dp_overlap=dp_overlap, **kw)
+                                semantics="local", dp_steps=dp_steps, dp_overlap=dp_overlap,
+                                local_steps=local_steps, **kw)
             S = m.set_train(pos)
             m.attach_runner("loopback", key=9100 + W)
             hist = [m.train_steps(e, 0, S) for e in range(epochs)]
@@ -69,7 +70,7 @@ def dp_world(mode):
     return int(mode[len("local_dp"):]) if mode.startswith("local_dp") else 0
 
 
-def f5(rl, mode, seed, dp_steps=64, dp_overlap=False):
+def f5(rl, mode, seed, dp_steps=64, dp_overlap=False, local_steps=0):
     g = os.path.join(ROOT, "tests", "golden")
     with open(os.path.join(g, "hr_ndcg_ml100k.json")) as fh:
         ref = json.load(fh)
@@ -80,10 +81,11 @@ def f5(rl, mode, seed, dp_steps=64, dp_overlap=False):
     if dp_world(mode):
         m, el, _ = train_local_dp(rl, dp_world(mode), int(f["U"]), int(f["I"]), p["factor_num"],
                                   f["positives"].astype(np.int64), p["epochs"], seed, dp_steps,
-                                  dp_overlap, lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"], num_ng=p["num_ng"])
+                                  dp_overlap, local_steps, lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"], num_ng=p["num_ng"])
     else:
         m = rl.BPRMF(int(f["U"]), int(f["I"]), p["factor_num"], lr=p["lr"], wd=p["wd"],
-                     batch_size=p["batch_size"], num_ng=p["num_ng"], seed=seed, semantics=mode)
+                     batch_size=p["batch_size"], num_ng=p["num_ng"], seed=seed, semantics=mode,
+                     local_steps=local_steps)
         t0 = time.perf_counter()
         m.fit(f["positives"].astype(np.int64), epochs=p["epochs"])
         el = time.perf_counter() - t0
@@ -94,7 +96,7 @@ def f5(rl, mode, seed, dp_steps=64, dp_overlap=False):
                 reference=dict(hr10=ref["summary"]["hr"], ndcg10=ref["summary"]["ndcg"]))
 
 
-def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64, dp_overlap=False):
+def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64, dp_overlap=False, local_steps=0):
     syn = importlib.import_module("recommend-lib_amd.synthetic")
     U, I = 138493, 26744
     pos = syn.make_positives(U, I, 10_000_000, 20261015)
@@ -117,9 +119,9 @@ def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64, dp_overlap=False):
         lists.append([int(test[u, 1])] + cand)  # the held-out item first
     if dp_world(mode):
         m, secs, trip = train_local_dp(rl, dp_world(mode), U, I, 128, train, epochs, seed, dp_steps,
-                                       dp_overlap, batch_size=4096)
+                                       dp_overlap, local_steps, batch_size=4096)
     else:
-        m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode)
+        m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode, local_steps=local_steps)
         m.set_train(train)
         secs, trip = 0.0, 0
         for _ in range(epochs):
@@ -145,14 +147,18 @@ def main():
     ap.add_argument("--modes", default="exact,hogwild,local")
     ap.add_argument("--dp-steps", type=int, default=64, help="local_dpW: steps between item merges")
     ap.add_argument("--dp-overlap", action="store_true", help="local_dpW: all-reduce beside the next period")
+    ap.add_argument("--local-steps", type=int, default=0, help="local: steps between XCD merges (0: 128)")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first)
     rl = importlib.import_module("recommend-lib_amd")
     for w in a.which.split(","):
         for mode in a.modes.split(","):
             for seed in (int(x) for x in a.seeds.split(",")):
-                r = (f5(rl, mode, seed, a.dp_steps, a.dp_overlap) if w == "f5"
-                     else ml20m(rl, mode, seed, a.epochs, a.users_eval, a.dp_steps, a.dp_overlap))
+                r = (f5(rl, mode, seed, a.dp_steps, a.dp_overlap, a.local_steps) if w == "f5"
+                     else ml20m(rl, mode, seed, a.epochs, a.users_eval, a.dp_steps, a.dp_overlap,
+                                a.local_steps))
+                if mode == "local" or dp_world(mode):
+                    r["local_steps"] = a.local_steps or 128
                 if dp_world(mode):
                     r["dp_steps"] = a.dp_steps
                     r["dp_overlap"] = a.dp_overlap

@@ -1017,6 +1017,7 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   if (!h || !P || !Q) return fail(BPRMF_E_INVALID, "null argument");
   if (int r = set_dev(h)) return r;
   const size_t D = h->geom.D, ld = h->geom.ld;
+  if (int r = dp_quiesce(h)) return r;
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemset(h->P.W, 0, sizeof(float) * h->U * ld));
   HIPCHK(hipMemset(h->Q.W, 0, sizeof(float) * h->I * ld));
@@ -1029,7 +1030,6 @@ int bprmf_set_weights(bprmf_handle* h, const float* P, const float* Q) {
   if (h->d_qbase) {  // LOCAL at world > 1: the next merge's base (every rank sets the same Q)
     HIPCHK(hipMemcpy(h->d_qbase, h->Q.W, sizeof(float) * h->I * ld, hipMemcpyDeviceToDevice));
     h->dp_t = h->t;
-    h->dp_pending = false;  // (calls end with a blocking merge: no all-reduce is in flight here)
   }
   return local_refresh(h);  // LOCAL: the replicas start from the new rows
 }

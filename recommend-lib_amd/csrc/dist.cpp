@@ -855,6 +855,15 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
 // (include/bprmf.h BPRMF_SEM_LOCAL.)  Every rank trains its own users' triplets
 // with the single-GPU local step (hogwild.hip, hot items in per-XCD replicas) on its own copy of
 // the whole item table; a merge brings every rank's copy to base + the sum of the ranks' changes.
+int dp_quiesce(bprmf_handle* h) {
+  if (!h->dp_pending) return 0;
+  h->dp_pending = false;
+  if (h->dist)
+    if (int r = h->dist->tr->allreduce_wait(h)) return r;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 // dp_overlap and not the call's last merge: the all-reduce is only started (beside the next
 // period), and lands at the next merge.  Otherwise blocking: every rank leaves with base + sum.
 static int dp_merge(bprmf_handle* h, bool last) {

@@ -37,6 +37,8 @@ struct DistState;  // dist.cpp: the sharded runner's transport, plan and exchang
 void dist_free(DistState* d);
 // semantics LOCAL at world > 1 (dist.cpp): the item table on every rank (not sharded)
 inline bool dp_items(const bprmf_config& c) { return c.semantics == BPRMF_SEM_LOCAL && c.world > 1; }
+// an all-reduce a failed call left in flight (dp_overlap) is waited for and dropped
+int dp_quiesce(bprmf_handle* h);
 
 }  // namespace bprmf
 

@@ -518,6 +518,27 @@ hipError_t dp_sum(const DpSrcs& src, int world, float* out, int64_t n, hipStream
   return hipGetLastError();
 }
 
+// the geometries of the hogwild launch: by default half the rows' lanes per triplet and twice the
+// stripes for 32- and 64-lane rows (d = 65..256: twice the triplets, so twice the rows, in flight
+// per wave; local mode 1.56 -> 1.61e9 triplets/s at the ml-20m shape); BPRMF_HOGWILD_NARROW=0:
+// the rows' own (G4, S) (A/B)
+#define HW_DISPATCH(geom, BODY)                                     \
+  switch ((geom).G4 * 10 + (geom).S) {                             \
+    case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
+    case 21: { constexpr int G4_ = 2, S_ = 1; BODY; } break;       \
+    case 41: { constexpr int G4_ = 4, S_ = 1; BODY; } break;       \
+    case 81: { constexpr int G4_ = 8, S_ = 1; BODY; } break;       \
+    case 161: { constexpr int G4_ = 16, S_ = 1; BODY; } break;     \
+    case 162: { constexpr int G4_ = 16, S_ = 2; BODY; } break;     \
+    case 321: { constexpr int G4_ = 32, S_ = 1; BODY; } break;     \
+    case 322: { constexpr int G4_ = 32, S_ = 2; BODY; } break;     \
+    case 641: { constexpr int G4_ = 64, S_ = 1; BODY; } break;     \
+    case 642: { constexpr int G4_ = 64, S_ = 2; BODY; } break;     \
+    case 643: { constexpr int G4_ = 64, S_ = 3; BODY; } break;     \
+    case 644: { constexpr int G4_ = 64, S_ = 4; BODY; } break;     \
+    default: return hipErrorInvalidValue;                          \
+  }
+
 static bool hw_serial() {
   const char* e = getenv("BPRMF_HOGWILD_SERIAL");
   return e && e[0] == '1';
@@ -535,12 +556,18 @@ static int hw_tpw(int64_t n) {
   return 16;
 }
 
-hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
+hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_t slot0,
                    const int32_t* tu, const int32_t* ti, const int32_t* tj, int64_t n, Table P,
                    Table Q, const Hyper& hp, int32_t t0, int B, double* loss, int32_t* err,
                    hipStream_t s, const LocalArgs* lap, int uw) {
   if (n <= 0) return hipSuccess;
   if (uw < 1) return hipErrorInvalidValue;
+  Geom g = g0;
+  const char* nw = getenv("BPRMF_HOGWILD_NARROW");
+  if (!(nw && nw[0] == '0') && (g.G4 == 32 || g.G4 == 64) && g.S == 1) {
+    g.G4 /= 2;
+    g.S = 2;
+  }
   const bool serial = hw_serial();
   const int tpw = serial ? 64 : hw_tpw(n);
   const int64_t waves = (n + tpw - 1) / tpw;
@@ -575,7 +602,7 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
   if (sa) a = *sa;
   if (lap) {  // semantics "local": the hot items in per-XCD replicas
     const LocalArgs la = *lap;
-    BPRMF_DISPATCH4(g, ({
+    HW_DISPATCH(g, ({
       if (serial && sa)
         k_hogwild<G4_, S_, true, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
                                                                   hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
@@ -591,7 +618,7 @@ hipError_t hogwild(const Geom& g, const SamplerArgs* sa, uint32_t epoch, int64_t
     }));
     return hipGetLastError();
   }
-  BPRMF_DISPATCH4(g, ({
+  HW_DISPATCH(g, ({
     if (serial && sa)
       k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
                                                           g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);

@@ -57,3 +57,33 @@ def test_config_layout_matches_header(rl):
     assert ctypes.sizeof(mf.MfConfig) == 112 and mf.MfConfig.lr.offset == 32
     assert mf.MfConfig.lr_yj.offset == 96 and mf.MfConfig.reg_yj.offset == 104
     assert ctypes.sizeof(mf.MfStats) == 24
+
+
+def test_config_offsets_match_the_c_header(rl, tmp_path):
+    """Every bprmf_config / bprmf_stats field at the offset a C compiler gives it (include/bprmf.h
+    compiled with gcc here), so a field added on one side only cannot go unnoticed."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = [f for f, _ in rl._lib.Config._fields_]
+    st = [f for f, _ in rl._lib.Stats._fields_]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "bprmf.h"', "int main(void) {",
+             '  printf("config %zu\\n", sizeof(bprmf_config));', '  printf("stats %zu\\n", sizeof(bprmf_stats));']
+    lines += [f'  printf("c.{f} %zu\\n", offsetof(bprmf_config, {f}));' for f in cfg]
+    lines += [f'  printf("s.{f} %zu\\n", offsetof(bprmf_stats, {f}));' for f in st]
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)],
+                   check=True, capture_output=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                 text=True).stdout.splitlines())
+    assert int(got["config"]) == ctypes.sizeof(rl._lib.Config)
+    assert int(got["stats"]) == ctypes.sizeof(rl._lib.Stats)
+    for f in cfg:
+        assert int(got[f"c.{f}"]) == getattr(rl._lib.Config, f).offset, f
+    for f in st:
+        assert int(got[f"s.{f}"]) == getattr(rl._lib.Stats, f).offset, f

@@ -70,6 +70,12 @@ def dp_world(mode):
     return int(mode[len("local_dp"):]) if mode.startswith("local_dp") else 0
 
 
+def big_batch(mode):
+    """"exact_bN": the exact step with per-step batch N (the union batch of N / 4096 ranks of the
+    exact sharded runner; B > 8192 takes the f32-atomic sums)."""
+    return int(mode[len("exact_b"):]) if mode.startswith("exact_b") else 0
+
+
 def f5(rl, mode, seed, dp_steps=64, dp_overlap=False, local_steps=0):
     g = os.path.join(ROOT, "tests", "golden")
     with open(os.path.join(g, "hr_ndcg_ml100k.json")) as fh:
@@ -121,7 +127,10 @@ def ml20m(rl, mode, seed, epochs, n_eval, dp_steps=64, dp_overlap=False, local_s
         m, secs, trip = train_local_dp(rl, dp_world(mode), U, I, 128, train, epochs, seed, dp_steps,
                                        dp_overlap, local_steps, batch_size=4096)
     else:
-        m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode, local_steps=local_steps)
+        if big_batch(mode):
+            m = rl.BPRMF(U, I, 128, batch_size=big_batch(mode), seed=seed)
+        else:
+            m = rl.BPRMF(U, I, 128, batch_size=4096, seed=seed, semantics=mode, local_steps=local_steps)
         m.set_train(train)
         secs, trip = 0.0, 0
         for _ in range(epochs):

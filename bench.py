@@ -130,7 +130,7 @@ def main():
     ap.add_argument("--local-steps", type=int, default=0,
                     help="--semantics local: steps between the XCD replicas' merges (0: 128)")
     ap.add_argument("--dp-steps", type=int, default=0,
-                    help="--semantics local, N > 1: steps between the ranks' item-table merges (0: 64)")
+                    help="--semantics local, N > 1: steps between the ranks' item-table merges (0: 256)")
     ap.add_argument("--dp-overlap", action="store_true",
                     help="--semantics local, N > 1: each merge's all-reduce beside the next period")
     ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
@@ -316,7 +316,7 @@ def main():
                        "random N(0,0.01^2) init; no dataset download",
                "config": {"workload": "BPR-MF training, ml-20m shape", "users": U, "items": I,
                           **({"local_steps": a.local_steps or 128} if a.semantics == "local" else {}),
-                          **({"dp_steps": a.dp_steps or 64, "dp_overlap": a.dp_overlap} if dpi else {}),
+                          **({"dp_steps": a.dp_steps or 256, "dp_overlap": a.dp_overlap} if dpi else {}),
                           "positives": int(len(pos)), "factor_num": d, "batch_size_per_gpu": B,
                           "global_batch": B * world, "num_ng": 4, "lr": 0.01, "wd": 0.001,
                           "parallelism": (f"users row-sharded x{world}, item table replicated, merged "

@@ -50,7 +50,7 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
  * steps.
  * LOCAL at world > 1 (data-parallel items): users stay sharded (u % world == rank, each rank
  * samples only its own users' positives) but every rank holds the WHOLE item table and trains it
- * as above; every `dp_steps` steps (default 64) and at the end of every call the ranks' item
+ * as above; every `dp_steps` steps (default 256) and at the end of every call the ranks' item
  * tables are merged: new = decayed base + sum over ranks of each rank's change since the last
  * merge (one all-reduce of the table, bprmf_dist_init_rccl or _loopback; the IPC transport is
  * not supported).  Staleness across GPUs is bounded by `dp_steps` steps.
@@ -84,7 +84,7 @@ typedef struct {
                            BPRMF_SEM_HOGWILD (1): opt-in relaxed synchronisation, see below */
   int32_t step_mode;    /* BPRMF_STEP_SEGMENTED (0, default) or BPRMF_STEP_ATOMIC (1), single GPU */
   int32_t local_steps;  /* BPRMF_SEM_LOCAL: steps between replica merges (0: 128) */
-  int32_t dp_steps;     /* BPRMF_SEM_LOCAL, world > 1: steps between the ranks' item merges (0: 64) */
+  int32_t dp_steps;     /* BPRMF_SEM_LOCAL, world > 1: steps between the ranks' item merges (0: 256) */
   int32_t dp_overlap;   /* BPRMF_SEM_LOCAL, world > 1: 1 = each merge's all-reduce runs beside the
                            next period (its result lands one period later), 0 = blocking merges */
 } bprmf_config;

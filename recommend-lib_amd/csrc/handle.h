@@ -83,7 +83,7 @@ struct bprmf_handle {
   float* d_qbase = nullptr;  // [I][ld] the table at the last merge (current at dp_t)
   float* d_qdelta = nullptr; // [I][ld] this rank's change since then (the all-reduce's buffer)
   int32_t dp_t = 0;             // the step qbase is current at
-  int32_t dp_steps = 64;
+  int32_t dp_steps = 256;
   // cfg.dp_overlap: a merge's all-reduce runs beside the next period; its sum (dp_sum, in d_qsum
   // or the transport's scratch) is added at the next merge, and d_qdelta keeps this rank's part
   bool dp_overlap = false;

@@ -57,7 +57,7 @@ class BPRMF:
     `semantics="local"`: hogwild for users and cold items, the hot items trained in one replica
     per XCD and merged every `local_steps` steps (default 128; bounded staleness).
     With world > 1 and `semantics="local"` the handle keeps its users' rows but the WHOLE item
-    table, merged with the other ranks every `dp_steps` steps (default 64) and at every call's end
+    table, merged with the other ranks every `dp_steps` steps (default 256) and at every call's end
     (sharded.ShardedBPRMF drives it); `dp_overlap=True` runs each merge's
     all-reduce beside the next period and adds its sum one period later.
     `step="atomic"` sums duplicate rows with f32 atomics instead of the sorted one-writer sums

@@ -205,19 +205,36 @@ def main():
                     m.train_steps(e, s, c)
                     done += c
 
-    # the timing barriers go through a gloo group (host sockets): the nccl group's barrier is a
-    # device all-reduce plus a synchronisation, ~0.1 ms that would land inside the timed region
+    # the timing barriers: the ranks of one node meet on shared memory (bprmf_node_barrier_*,
+    # ~1 us); a process group's barrier (gloo sockets, or the nccl group's device all-reduce plus a
+    # synchronisation) costs ~0.1 ms that would land inside the timed region.  Ranks on several
+    # nodes: a gloo group's barrier.
     bar = dist.new_group(backend="gloo") if dist and a.pg_backend == "nccl" else None
+    nb, nb_path = None, None
+    if dist and world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world:
+        tok = [f"/dev/shm/bprmf_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
+        dist.broadcast_object_list(tok, src=0, group=bar)
+        nb_path = tok[0]
+        if rank == 0:
+            nb = rl.sharded.NodeBarrier(nb_path, world, rank, create=True)
+        dist.barrier(group=bar)
+        if rank != 0:
+            nb = rl.sharded.NodeBarrier(nb_path, world, rank, create=False)
+        dist.barrier(group=bar)
+
+    def barrier():
+        if nb is not None:
+            nb.wait()
+        elif dist:
+            dist.barrier(group=bar)
 
     def timed(first, k):
-        if dist:
-            dist.barrier(group=bar)
+        barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(first, k)
         torch.cuda.synchronize()
-        if dist:
-            dist.barrier(group=bar)
+        barrier()
         el = time.perf_counter() - t0
         if dist:
             t = torch.tensor([el], dtype=torch.float64,
@@ -340,6 +357,13 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
+        if nb is not None:
+            nb.close()
+            if rank == 0:
+                try:
+                    os.unlink(nb_path)
+                except OSError:
+                    pass
         dist.destroy_process_group()
     return out
 

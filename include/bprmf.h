@@ -264,6 +264,16 @@ int bprmf_dist_exchange_stats(bprmf_handle* h, int64_t* steps, int64_t* row_byte
 int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
                             int64_t n_steps, bprmf_stats* stats);
 
+/* ---- a barrier for the ranks of one node (host only; no reference counterpart) -------------
+ * bench.py brackets its timed region with a barrier on every rank (the measurement contract); a
+ * process group's barrier costs ~0.1 ms, the ranks of one node meet on two shared words of a
+ * /dev/shm file instead (~1 us).  One rank opens it with create = 1, the others after it with 0
+ * (same path and world); wait returns once every rank has called it, or BPRMF_E_STATE after
+ * timeout_s seconds (<= 0: no limit). */
+int bprmf_node_barrier_open(const char* path, int32_t world, int32_t rank, int32_t create, void** out);
+int bprmf_node_barrier_wait(void* barrier, double timeout_s);
+int bprmf_node_barrier_close(void* barrier);
+
 /* ---- test hooks (no reference counterpart) ------------------------------------------------ */
 /* The launch tag the next split batch build of this process will carry (segment.hip): the tests
  * use it to plant stale words that an unsafe tag scheme would mistake for this launch's. */

@@ -112,6 +112,10 @@ SIGNATURES = {
     "bprmf_dataset_candidates": [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                  ctypes.POINTER(_I64), _P, _P],
     "bprmf_dataset_free": [_P],
+    "bprmf_node_barrier_open": [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.POINTER(ctypes.c_void_p)],
+    "bprmf_node_barrier_wait": [_P, ctypes.c_double],
+    "bprmf_node_barrier_close": [_P],
     "bprmf_debug_next_build_tag": [ctypes.POINTER(ctypes.c_uint32)],
     "bprmf_debug_fill_batches": [_P, ctypes.c_int32],
     "bprmf_profile": [_P, ctypes.c_int32],

@@ -468,6 +468,27 @@ class ShardedBPRMF:
         return self.b.profile_read()
 
 
+class NodeBarrier:
+    """The ranks of one node meeting on two shared words of a /dev/shm file (include/bprmf.h
+    bprmf_node_barrier_*; ~1 us instead of a process group's ~0.1 ms).  One rank constructs it
+    with create=True before the others open the same path."""
+
+    def __init__(self, path, world, rank, create):
+        self.L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self.L.bprmf_node_barrier_open(str(path).encode(), int(world), int(rank),
+                                                  int(bool(create)), ctypes.byref(h)))
+        self.h = h
+
+    def wait(self, timeout=120.0):
+        _lib.check(self.L.bprmf_node_barrier_wait(self.h, float(timeout)))
+
+    def close(self):
+        if self.h:
+            self.L.bprmf_node_barrier_close(self.h)
+            self.h = None
+
+
 def shard_rows(global_table, rank, world):
     """Rows of a global table owned by `rank` (strided sharding)."""
     return np.ascontiguousarray(global_table[rank::world])

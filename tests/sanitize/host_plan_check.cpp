@@ -7,6 +7,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <map>
 #include <random>
 #include <set>
@@ -196,6 +199,37 @@ int main() {
     CHECK(!ipc_shares_device(blobs.data(), 8, 0, bb, off, bus));
     CHECK(!ipc_shares_device(blobs.data(), 1, 0, bb, off, bus));
     CHECK(!ipc_shares_device(blobs.data(), 8, 0, bb, bb - 8, bus));  // field past the blob
+  }
+  {  // the node barrier (node_barrier.cpp): one rank, a wrong world, then forked ranks
+    char path[64];
+    snprintf(path, sizeof path, "/tmp/bprmf_nb_check_%d", (int)getpid());
+    void* b = nullptr;
+    CHECK(bprmf_node_barrier_open(path, 1, 0, 1, &b) == 0);
+    for (int k = 0; k < 1000; ++k) CHECK(bprmf_node_barrier_wait(b, 5.0) == 0);
+    void* w = nullptr;
+    CHECK(bprmf_node_barrier_open(path, 3, 1, 0, &w) == BPRMF_E_STATE && w == nullptr);
+    CHECK(bprmf_node_barrier_close(b) == 0);
+    const int W = 3, iters = 300;
+    CHECK(bprmf_node_barrier_open(path, W, 0, 1, &b) == 0);
+    for (int r = 1; r < W; ++r) {
+      if (fork() == 0) {  // a rank: meets the others iters times, then exits with its status
+        void* c = nullptr;
+        int bad = bprmf_node_barrier_open(path, W, r, 0, &c) != 0;
+        for (int k = 0; k < iters && !bad; ++k) bad = bprmf_node_barrier_wait(c, 30.0) != 0;
+        bprmf_node_barrier_close(c);
+        _exit(bad);
+      }
+    }
+    bool ok = true;
+    for (int k = 0; k < iters && ok; ++k) ok = bprmf_node_barrier_wait(b, 30.0) == 0;
+    CHECK(ok);
+    for (int r = 1; r < W; ++r) {
+      int st = 0;
+      wait(&st);
+      CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+    }
+    CHECK(bprmf_node_barrier_close(b) == 0);
+    unlink(path);
   }
   printf("host_plan_check: %s, %d cases\n", g_fail ? "FAILED" : "ok", g_cases);
   return g_fail ? 1 : 0;

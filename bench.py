@@ -225,7 +225,7 @@ def main():
     def barrier():
         if nb is not None:
             nb.wait()
-        elif dist:
+        elif dist and world > 1:  # (one rank: nothing to wait for)
             dist.barrier(group=bar)
 
     def timed(first, k):

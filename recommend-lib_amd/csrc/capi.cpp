@@ -126,6 +126,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   const int64_t W = cfg->world, R = cfg->rank;
   h->U = shard_rows(cfg->user_num, (int)W, (int)R);
   const bool dpi = dp_items(*cfg);  // LOCAL at world > 1: every item on every rank
+  h->dp_mode = dpi;
   h->I = dpi ? cfg->item_num : shard_rows(cfg->item_num, (int)W, (int)R);
   const uint64_t shard_seed = cfg->seed + (uint64_t)cfg->rank * 0x9E3779B97F4A7C15ull;
   h->k0 = (uint32_t)shard_seed;

@@ -148,7 +148,7 @@ struct RcclTransport final : Transport {
   // every rank holds the same bits
   int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) override {
     *out = buf;
-    if (h->cfg.world > 1) NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm, h->stream));
+    NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, ncclSum, comm, h->stream));
     return 0;
   }
   int allreduce_start(bprmf_handle* h, float* buf, float* dst, int64_t n, const float** out) override {
@@ -482,7 +482,7 @@ int64_t dist_chunk_steps(const bprmf_handle* h) {
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap);
 
 static int dist_attach(bprmf_handle* h, Transport* tr) {
-  if (dp_items(h->cfg)) {  // LOCAL at world > 1: the item merge needs only the transport
+  if (h->dp_mode) {  // LOCAL at world > 1: the item merge needs only the transport
     if (h->dist) {
       HIPCHK(hipStreamSynchronize(h->stream));
       dist_free(h->dist);
@@ -981,7 +981,7 @@ int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id) {
 
 int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
   if (!h || !blob) return fail(BPRMF_E_INVALID, "null argument");
-  if (dp_items(h->cfg))
+  if (h->dp_mode)
     return fail(BPRMF_E_UNSUPPORTED, "local semantics at world > 1: use the rccl transport");
   if (int r = set_dev(h)) return r;
   static_assert(sizeof(hipIpcMemHandle_t) * kIpcHandles <= BPRMF_IPC_BLOB_BYTES, "blob size");
@@ -1077,7 +1077,7 @@ int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, 
   if (!h->dist || !h->dist->tr->ready())
     return fail(BPRMF_E_STATE, "attach a transport first (bprmf_dist_init_*)");
   if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
-  if (dp_items(h->cfg)) {  // LOCAL at world > 1
+  if (h->dp_mode) {  // LOCAL at world > 1
     if (int r = begin_call(h)) return r;
     int64_t trip = 0;
     if (int r = dp_run(h, epoch, first_step, n_steps, nullptr, nullptr, nullptr, &trip)) return r;
@@ -1129,7 +1129,7 @@ int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i,
     HIPCHK(hipMemcpyAsync(tu, u + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(ti, i + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(tj, j + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
-    if (dp_items(h->cfg)) {
+    if (h->dp_mode) {
       int64_t unused = 0;
       if (int r = dp_run(h, 0, 0, m, tu, ti, tj, &unused)) return r;
     } else if (int r = dist_chunk(h, 0, 0, m, tu, ti, tj)) {

@@ -2,6 +2,7 @@
 // (single-GPU training, weights, scoring) and dist.cpp (the sharded multi-GPU runner).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include <string>
 #include <utility>
@@ -36,7 +37,14 @@ constexpr int kProfStride = 16;  // profiling: time the kernels of every 16th st
 struct DistState;  // dist.cpp: the sharded runner's transport, plan and exchange buffers
 void dist_free(DistState* d);
 // semantics LOCAL at world > 1 (dist.cpp): the item table on every rank (not sharded)
-inline bool dp_items(const bprmf_config& c) { return c.semantics == BPRMF_SEM_LOCAL && c.world > 1; }
+// (BPRMF_DP_ONE_RANK=1, a test hook: a one-rank world of LOCAL handles also merges through the
+// transport, so the one-GPU test box runs the RCCL all-reduce path: tests/test_gpu_local_dp.py)
+inline bool dp_items(const bprmf_config& c) {
+  if (c.semantics != BPRMF_SEM_LOCAL) return false;
+  if (c.world > 1) return true;
+  const char* e = getenv("BPRMF_DP_ONE_RANK");
+  return e && e[0] == '1';
+}
 // an all-reduce a failed call left in flight (dp_overlap) is waited for and dropped
 int dp_quiesce(bprmf_handle* h);
 
@@ -87,6 +95,7 @@ struct bprmf_handle {
   // cfg.dp_overlap: a merge's all-reduce runs beside the next period; its sum (dp_sum, in d_qsum
   // or the transport's scratch) is added at the next merge, and d_qdelta keeps this rank's part
   bool dp_overlap = false;
+  bool dp_mode = false;         // dp_items(cfg) at create: the item merges run (dist.cpp)
   bool dp_pending = false;      // an all-reduce was started at step dp_tp and not applied yet
   int32_t dp_tp = 0;
   const float* dp_sum = nullptr;

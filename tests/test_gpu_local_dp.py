@@ -147,3 +147,42 @@ def test_local_dp_refuses_ipc_and_hogwild_stays_single_gpu(rl):
         m.ipc_export()
     with pytest.raises(Exception):
         rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="hogwild")
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_local_dp_rccl_transport_one_rank_matches_oracle(rl, monkeypatch, overlap):
+    """The RCCL all-reduce path (in place; overlapped: out of place on the transport's own stream,
+    ordered by events) on a one-rank communicator (BPRMF_DP_ONE_RANK=1 runs the item merges at
+    world 1): the SERIAL build against local_dp_serial at world 1."""
+    import ctypes
+    monkeypatch.setenv("BPRMF_DP_ONE_RANK", "1")
+    monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
+    H = 4
+    monkeypatch.setenv("BPRMF_LOCAL_HOT", str(H))
+    g = np.random.default_rng(41 + overlap)
+    U, I, d, B, steps, period, dp = 19, 23, 32, 16, 7, 2, 3
+    lr, wd = 0.05, 0.01
+    rows = [(u, it) for u in range(U) for it in range(I) if g.random() < 0.3 / (1 + it % 5)]
+    pos = np.unique(np.array(rows, np.int64), axis=0)
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    u, i, j = g.integers(0, U, steps * B), g.integers(0, I, steps * B), g.integers(0, I, steps * B)
+    i[::3] = 0
+    j[:4] = i[:4]
+    m = rl.sharded.HipShard(U, I, d, lr, wd, B, 4, 0.01, 0, 0, 0, 1, "local", period, dp, overlap)
+    m.set_train(pos)
+    m.set_weights(P0, Q0)
+    L = rl._lib.load()
+    uid = (ctypes.c_uint8 * 128)()
+    rl._lib.check(L.bprmf_dist_unique_id(ctypes.addressof(uid)))
+    m.runner_rccl(bytes(uid))
+    st = m.runner_train_replay(u, i, j, steps)
+    Pg, Qg = m.get_weights()
+    Pp = [P0.copy()]
+    loss, sPs, Qw = O.local_dp_serial(Pp, Q0.copy(), [(u, i, j)], lr, wd, B, [_hot_set(pos, 0, 1, I, H)],
+                                      period, dp, 1, overlap=overlap)
+    a = np.float32(1 - lr * wd)
+    Pw = Pp[0] * np.power(np.float64(a), (steps - sPs[0]))[:, None].astype(np.float32)
+    np.testing.assert_allclose(Pg, Pw, rtol=1e-5, atol=HOG_ATOL)
+    np.testing.assert_allclose(Qg, Qw, rtol=1e-5, atol=HOG_ATOL)
+    assert st["loss"] == pytest.approx(loss, rel=1e-5)

@@ -85,7 +85,11 @@ static __device__ __forceinline__ void hw_sample(const SamplerArgs& a, uint32_t 
   if (!sample_slot(a, epoch, slot, u, i, j)) atomicOr(err, 2);
 }
 
-constexpr int kHwUnroll = 2;  // triplets per lane group per round (rows in flight per buffer)
+#ifndef BPRMF_HW_UNROLL
+#define BPRMF_HW_UNROLL 2
+#endif
+constexpr int kHwUnroll = BPRMF_HW_UNROLL;  // triplets per lane group per round (rows in flight
+                                            // per buffer; -DBPRMF_HW_UNROLL: A/B builds)
 
 // One round of a wave: kHwUnroll triplets per lane group, their ids, stamps and rows.
 template <int S, int UNR>

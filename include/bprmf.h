@@ -52,8 +52,8 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
  * samples only its own users' positives) but every rank holds the WHOLE item table and trains it
  * as above; every `dp_steps` steps (default 256) and at the end of every call the ranks' item
  * tables are merged: new = decayed base + sum over ranks of each rank's change since the last
- * merge (one all-reduce of the table, bprmf_dist_init_rccl or _loopback; the IPC transport is
- * not supported).  Staleness across GPUs is bounded by `dp_steps` steps.
+ * merge (one all-reduce of the table: RCCL's, the IPC transport's reduce-scatter + all-gather
+ * pushes, or the loopback's).  Staleness across GPUs is bounded by `dp_steps` steps (§5d).
  * dp_overlap = 1: the all-reduce of a merge runs on a side stream while the next period trains;
  * its sum is added one period later (the other ranks' changes arrive up to 2 dp_steps late);
  * the last merge of every call is blocking, so every rank ends a call with the same table. */

@@ -159,7 +159,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->Q.stamp, h->I));
   if (dpi) {
     TRY(dalloc(&h->d_qbase, h->I * ld));
-    TRY(dalloc(&h->d_qdelta, h->I * ld));
+    // the delta table padded to world slices of ceil(I / world) rows (the IPC all-reduce pushes
+    // whole slices; the padding stays zero)
+    const int64_t pad_rows = W * ((h->I + W - 1) / W);
+    TRY(dalloc(&h->d_qdelta, pad_rows * ld));
     if (h->dp_overlap) TRY(dalloc(&h->d_qsum, h->I * ld));
   }
   // {err, dist words, loss slots[kLossSlots], two call sequence numbers}
@@ -183,6 +186,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     return 0;
   };
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
+  if (h->d_qdelta) TRY(memz(h->d_qdelta, sizeof(float) * (size_t)(W * ((h->I + W - 1) / W) * ld)));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
   TRY(memz(h->d_status, status_bytes));
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size

@@ -283,6 +283,45 @@ struct IpcTransport final : Transport {
     HIPCHK(ipc_push(a, world, (int64_t)x.bytes, x.tbase, x.k, x.seq, board(x.kind), h->d_err, h->stream));
     return 0;
   }
+  // semantics LOCAL at world > 1 (dist.cpp dp_merge): the item tables' all-reduce as a
+  // reduce-scatter and an all-gather of pushes over the full mesh (each rank owns a slice of
+  // ceil(I / W) rows): every rank pushes its slice p of buf into rank p's landing buffer (kind
+  // X_ROWS, block = the sender), waits for the W blocks of its own slice, sums them in rank order
+  // into its sum buffer (kind X_GRADS), pushes that slice into every peer's sum buffer and waits
+  // for theirs.  The sums are the loopback transport's, bit for bit.  A slice's landing blocks
+  // are reused by the next all-reduce only after every peer has pushed (so read) this one's.
+  int64_t dp_seq = 0;
+  int allreduce_sum(bprmf_handle* h, float* buf, int64_t n, const float** out) override {
+    const int W = world, R = rank;
+    const int64_t ld = h->geom.ld, slice = (h->I + W - 1) / W * ld;  // floats per slice
+    if (n != h->I * ld || !local[X_ROWS] || !local[X_GRADS])
+      return fail(BPRMF_E_STATE, "ipc all-reduce: the item-table buffers are not attached");
+    const int32_t seq = (int32_t)++dp_seq;
+    float* land = static_cast<float*>(local[X_ROWS]);
+    float* sum = static_cast<float*>(local[X_GRADS]);
+    PushArgs a{};
+    for (int p = 0; p < W; ++p) {
+      a.src[p] = buf + (int64_t)p * slice;
+      a.dst[p] = (p == R ? land : static_cast<float*>(remote[X_ROWS][p])) + (int64_t)R * slice;
+      if (p != R) a.flag[p] = static_cast<int32_t*>(remote[X_KINDS][p]) + X_ROWS * kMaxWorld + R;
+    }
+    HIPCHK(ipc_push(a, W, slice * (int64_t)sizeof(float), nullptr, 0, seq, board(X_ROWS), h->d_err, h->stream));
+    HIPCHK(ipc_wait(flags() + X_ROWS * kMaxWorld, W, R, nullptr, 0, seq, h->d_err, h->stream));
+    DpSrcs src{};
+    for (int p = 0; p < W; ++p) src.p[p] = land + (int64_t)p * slice;
+    HIPCHK(dp_sum(src, W, sum + (int64_t)R * slice, slice, h->stream));
+    PushArgs c{};
+    for (int p = 0; p < W; ++p) {
+      if (p == R) continue;
+      c.src[p] = sum + (int64_t)R * slice;
+      c.dst[p] = static_cast<float*>(remote[X_GRADS][p]) + (int64_t)R * slice;
+      c.flag[p] = static_cast<int32_t*>(remote[X_KINDS][p]) + X_GRADS * kMaxWorld + R;
+    }
+    HIPCHK(ipc_push(c, W, slice * (int64_t)sizeof(float), nullptr, 0, seq, board(X_GRADS), h->d_err, h->stream));
+    HIPCHK(ipc_wait(flags() + X_GRADS * kMaxWorld, W, R, nullptr, 0, seq, h->d_err, h->stream));
+    *out = sum;
+    return 0;
+  }
   int exchange(bprmf_handle* h, const Xchg& x) override {
     if (!x.bytes) return 0;
     if (world == 1) {  // no peers: only a self block, if the caller did not place it
@@ -489,6 +528,16 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
     }
     h->dist = new DistState();
     h->dist->tr = tr;
+    if (dynamic_cast<IpcTransport*>(tr)) {  // its all-reduce's landing and sum buffers (exported)
+      const int64_t W = h->cfg.world;
+      const size_t bytes = sizeof(float) * (size_t)(W * ((h->I + W - 1) / W) * h->geom.ld);
+      void* p = nullptr;
+      if (int r = tr->alloc_shared(h, X_ROWS, bytes, &p)) return r;
+      if (int r = tr->alloc_shared(h, X_GRADS, bytes, &p)) return r;
+      // (the other kinds are unused here, but every exported handle needs a buffer)
+      if (int r = tr->alloc_shared(h, X_IDS, 256, &p)) return r;
+      if (int r = tr->alloc_shared(h, X_MAX, 256, &p)) return r;
+    }
     return 0;
   }
   if (!seg_mode(h)) {
@@ -981,8 +1030,6 @@ int bprmf_dist_init_rccl(bprmf_handle* h, const uint8_t* id) {
 
 int bprmf_dist_ipc_export(bprmf_handle* h, uint8_t* blob) {
   if (!h || !blob) return fail(BPRMF_E_INVALID, "null argument");
-  if (h->dp_mode)
-    return fail(BPRMF_E_UNSUPPORTED, "local semantics at world > 1: use the rccl transport");
   if (int r = set_dev(h)) return r;
   static_assert(sizeof(hipIpcMemHandle_t) * kIpcHandles <= BPRMF_IPC_BLOB_BYTES, "blob size");
   auto* tr = new IpcTransport();

@@ -21,9 +21,19 @@ def main():
     sh = rl.sharded
     spec = np.load(os.environ["IPC_SPEC"])
     U, I, D, B = (int(spec[k]) for k in ("U", "I", "D", "B"))
+    local = mode == "local"  # semantics "local": the item table replicated, merged by all-reduce
+    kw = dict(semantics="local", local_steps=int(spec["period"]), dp_steps=int(spec["dp"]),
+              dp_overlap=bool(spec["overlap"])) if local else {}
     m = sh.ShardedBPRMF(U, I, D, lr=float(spec["lr"]), wd=float(spec["wd"]), batch_size=B,
-                        seed=int(spec["seed"]), device=0)
-    if mode == "replay":
+                        seed=int(spec["seed"]), device=0, **kw)
+    if local:
+        m.set_train(spec["pos"])
+        m.set_weights(sh.shard_rows(spec["P0"], rank, world), spec["Q0"])
+        m.attach_runner("ipc")
+        batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]
+        st = m.train_replay(batches)
+        st2 = m.train_replay(batches)
+    elif mode == "replay":
         m.set_weights(sh.shard_rows(spec["P0"], rank, world), sh.shard_rows(spec["Q0"], rank, world))
         m.attach_runner("ipc")
         batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]

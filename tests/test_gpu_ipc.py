@@ -154,3 +154,59 @@ def test_ipc_sampler_training_equals_loopback(rl, golden, tmp_path):
     lb = _loopback(rl, 2, spec, "sampler", key=4010)
     for r in range(2):
         assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])
+
+
+@pytest.mark.parametrize("world,overlap", [(2, False), (3, True)])
+def test_ipc_local_semantics_all_reduce_equals_loopback(rl, tmp_path, monkeypatch, world, overlap):
+    """semantics "local" across processes: the IPC transport's all-reduce
+    (reduce-scatter + all-gather pushes over the full mesh) against the in-process loopback
+    transport's rank-order sum, the SERIAL build on both sides: bit for bit, and every rank ends
+    with the same item table."""
+    U, I, D, B, steps = 61, 47, 32, 64, 7
+    g = np.random.default_rng(23 + world)
+    rows = [(uu, it) for uu in range(U) for it in range(I) if g.random() < 0.2 / (1 + it % 5)]
+    pos = np.unique(np.array(rows, np.int64), axis=0).astype(np.int32)
+    us, is_, js = [], [], []
+    for k in range(steps):  # each rank's share of a step: exactly B triplets
+        parts = [g.choice(np.arange(r, U, world), B) for r in range(world)]
+        us.append(np.concatenate(parts))
+        is_.append(g.integers(0, I, world * B))
+        js.append(g.integers(0, I, world * B))
+    spec = dict(U=U, I=I, D=D, B=B, lr=0.05, wd=0.01, seed=5, pos=pos, period=2, dp=3,
+                overlap=int(overlap), u=np.array(us, np.int32), i=np.array(is_, np.int32),
+                j=np.array(js, np.int32),
+                P0=(0.1 * g.standard_normal((U, D))).astype(np.float32),
+                Q0=(0.1 * g.standard_normal((I, D))).astype(np.float32))
+    env = {"BPRMF_HOGWILD_SERIAL": "1", "BPRMF_LOCAL_HOT": "4"}
+    res = _run_workers(tmp_path, spec, "local", world, extra_env=env)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sh = rl.sharded
+    grp = sh.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=B, seed=5, device=0,
+                                comm=sh.ThreadComm(grp, r), semantics="local", local_steps=2,
+                                dp_steps=3, dp_overlap=overlap)
+            m.set_train(pos)
+            m.set_weights(sh.shard_rows(spec["P0"], r, world), spec["Q0"])
+            m.attach_runner("loopback", key=8800 + world)
+            batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(steps)]
+            m.train_replay(batches)
+            m.train_replay(batches)
+            out[r] = m.get_weights()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    for r in range(world):
+        assert np.array_equal(res[r]["Q"], res[0]["Q"])
+        assert np.array_equal(res[r]["P"], out[r][0]), r
+        assert np.array_equal(res[r]["Q"], out[r][1]), r

@@ -8,7 +8,8 @@ What is pinned:
     order) against oracle/bpr_oracle.py:local_dp_serial, replayed, at worlds 2 and 3, with hot
     items, XCD periods shorter than, equal to and longer than the merge period;
   * the overlapped schedule (dp_overlap: each merge's sum lands one period later) the same way;
-  * every rank ends a call with the same item table, bit for bit;
+  * every rank ends a call with the same item table, bit for bit (across processes with the IPC
+    transport's all-reduce: tests/test_gpu_ipc.py);
   * the sampled parallel mode trains (loss falls, weights finite) and its epoch covers each rank's
     own positives once.
 Tolerance: the serial GPU against the float64-dot oracle, as tests/test_gpu_hogwild.py (HOG_ATOL),
@@ -140,11 +141,12 @@ def test_local_dp_sampled_trains_and_ranks_agree(rl, golden, overlap):
     assert loss[-1] < 0.9 * loss[0], loss
 
 
-def test_local_dp_refuses_ipc_and_hogwild_stays_single_gpu(rl):
+def test_local_dp_exports_ipc_handles_and_hogwild_stays_single_gpu(rl):
+    """The IPC transport carries this mode too (its all-reduce: tests/test_gpu_ipc.py); the
+    hogwild semantics stays single-GPU."""
     sh = rl.sharded
     m = sh.HipShard(10, 10, 8, 0.01, 0.001, 64, 4, 0.01, 0, 0, 0, 2, "local", 0, 0)
-    with pytest.raises(Exception):
-        m.ipc_export()
+    assert len(m.ipc_export()) == rl._lib.IPC_BLOB_BYTES
     with pytest.raises(Exception):
         rl.BPRMF(10, 10, 8, rank=0, world=2, semantics="hogwild")
 

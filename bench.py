@@ -28,7 +28,6 @@ cpu_baseline: the oracle's C port of the reference step (dense grads + dense wei
   labelled; never the headline.
 """
 import argparse
-import gc
 import importlib
 import json
 import os
@@ -230,17 +229,12 @@ def main():
             dist.barrier(group=bar)
 
     def timed(first, k):
-        # Python's garbage collector: collected before, paused inside the timed region (a
-        # collection there is interpreter noise, not the workload)
-        gc.collect()
-        gc.disable()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(first, k)
         torch.cuda.synchronize()
         barrier()
-        gc.enable()
         el = time.perf_counter() - t0
         if dist:
             t = torch.tensor([el], dtype=torch.float64,

@@ -13,7 +13,14 @@
 // of a call, kernel boundaries included, without a profiler in the loop.
 #ifdef BPRMF_CALL_STAMPS
 extern __device__ unsigned long long g_cs[64][2][64];
+// and, per slot, workgroup 0's shader-clock counter (s_memtime) and 100 MHz clock
+// (s_memrealtime) at its start and end: their ratio is the shader clock during the launch
+extern __device__ unsigned long long g_clk[64][4];
 #define BPRMF_CALL_STAMPS_DEF(tu)                                                                 \
+  __device__ unsigned long long g_clk[64][4];                                                     \
+  extern "C" int bprmf_debug_clk_##tu(unsigned long long* out) {                                  \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(g_clk)) == hipSuccess ? 0 : -3;    \
+  }                                                                                               \
   __device__ unsigned long long g_cs[64][2][64];                                                  \
   extern "C" int bprmf_debug_call_stamps_##tu(unsigned long long* out, int reset) {              \
     if (reset) {                                                                                  \
@@ -31,12 +38,20 @@ extern __device__ unsigned long long g_cs[64][2][64];
   do {                                                                                            \
     if (threadIdx.x == 0)                                                                         \
       atomicMin(&g_cs[(slot) & 63][0][blockIdx.x & 63], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                                    \
+      g_clk[(slot) & 63][0] = __builtin_amdgcn_s_memtime();                                      \
+      g_clk[(slot) & 63][1] = __builtin_amdgcn_s_memrealtime();                                  \
+    }                                                                                             \
   } while (0)
 #define CS_END(slot)                                                                              \
   do {                                                                                            \
     __syncthreads();                                                                              \
     if (threadIdx.x == 0)                                                                         \
       atomicMax(&g_cs[(slot) & 63][1][blockIdx.x & 63], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                                    \
+      g_clk[(slot) & 63][2] = __builtin_amdgcn_s_memtime();                                      \
+      g_clk[(slot) & 63][3] = __builtin_amdgcn_s_memrealtime();                                  \
+    }                                                                                             \
   } while (0)
 struct CsScope {  // CS_BEGIN at construction, CS_END when the kernel's threads leave its scope
   int slot;

@@ -40,7 +40,11 @@ pos = syn.make_positives(138493, 26744, 10_000_000, 20261015)
 m = rl.BPRMF(138493, 26744, 128, lr=0.01, wd=0.001, batch_size=4096, num_ng=4, seed=20261015)
 m.set_train(pos)
 m.train_steps(0, 0, 5)  # the bench's warm-up call
-rows, walls = [], []
+clk_step = L.bprmf_debug_clk_step
+clk_step.argtypes = [ctypes.c_void_p]
+clk_seg = L.bprmf_debug_clk_seg
+clk_seg.argtypes = [ctypes.c_void_p]
+rows, walls, mhz = [], [], []
 import time  # noqa: E402
 for c in range(calls):
     for f in readers:
@@ -57,6 +61,16 @@ for c in range(calls):
             if st != np.iinfo(np.uint64).max and en:
                 tab[slot] = (int(st), int(en))
     rows.append(tab)
+    # shader clock during each fused launch (workgroup 0: s_memtime ticks per 10 ns of s_memrealtime)
+    ck = np.zeros((64, 4), np.uint64)
+    assert clk_step(ck.ctypes.data) == 0
+    fs = [(int(ck[s, 2]) - int(ck[s, 0])) / max(1, int(ck[s, 3]) - int(ck[s, 1])) * 100.0
+          for s in range(3, 22) if int(ck[s, 3]) > int(ck[s, 1])]
+    cb = np.zeros((64, 4), np.uint64)
+    assert clk_seg(cb.ctypes.data) == 0
+    b = (int(cb[0, 2]) - int(cb[0, 0])) / max(1, int(cb[0, 3]) - int(cb[0, 1])) * 100.0 if int(cb[0, 3]) > int(cb[0, 1]) else None
+    mhz.append({"fused_mhz_mean": round(float(np.mean(fs)), 1) if fs else None,
+                "fused_mhz_first": round(fs[0], 1) if fs else None, "build_mhz": round(b, 1) if b else None})
 t0s = [min(v[0] for v in tab.values()) for tab in rows]
 out = {"wall_us_per_call": [round(w, 1) for w in walls], "launches": []}
 order = sorted(rows[-1], key=lambda s: rows[-1][s][0])
@@ -79,4 +93,6 @@ for tab, t0, w in zip(rows, t0s, walls):
                 "build_us": round((tab[0][1] - tab[0][0]) * 0.01, 2) if 0 in tab else None,
                 "fused_mean_us": round(float(np.mean(fused)) * 0.01, 2) if fused else None})
 out["per_call"] = per
+for p_, m_ in zip(per, mhz):
+    p_.update(m_)
 print(json.dumps(out, indent=1))

@@ -188,3 +188,43 @@ def test_local_dp_rccl_transport_one_rank_matches_oracle(rl, monkeypatch, overla
     np.testing.assert_allclose(Pg, Pw, rtol=1e-5, atol=HOG_ATOL)
     np.testing.assert_allclose(Qg, Qw, rtol=1e-5, atol=HOG_ATOL)
     assert st["loss"] == pytest.approx(loss, rel=1e-5)
+
+
+def test_local_dp_trains_ml100k_protocol(rl, golden):
+    """F5 protocol (ml-100k fo/tfo, d=32, B=4096 per rank, 20 epochs) with 4 ranks, overlapped
+    merges: HR@10 / NDCG@10 of the merged model inside the reference's spread over seeds (mean
+    +- 4 std, as the single-GPU tests), loss falling."""
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        ref = json.load(fh)
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    p = ref["protocol"]
+    gt = {int(u): set(f["gt_items"][f["gt_ptr"][k]:f["gt_ptr"][k + 1]].tolist())
+          for k, u in enumerate(f["gt_users"])}
+    Uu, Ii, world = int(f["U"]), int(f["I"]), 4
+    pos = f["positives"].astype(np.int64)
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(Uu, Ii, p["factor_num"], lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"],
+                            num_ng=p["num_ng"], seed=11, device=0, comm=comm, semantics="local",
+                            dp_steps=64, dp_overlap=True)
+        S = m.set_train(pos)
+        m.attach_runner("loopback", key=7500)
+        losses = [m.train_steps(e, 0, S)["loss"] for e in range(p["epochs"])]
+        return m.get_weights(), losses
+
+    parts = _threads(rl, world, fn)
+    P = sh.unshard_rows([x[0][0] for x in parts], Uu)
+    Q = parts[0][0][1]
+    losses = [sum(x[1][e] for x in parts) for e in range(p["epochs"])]
+    assert losses[-1] < 0.8 * losses[0]
+    m = rl.BPRMF(Uu, Ii, p["factor_num"], lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"])
+    m.set_weights(P, Q)
+    kpi = rl.metrics.evaluate_topk(m, f["test_data"], gt, p["topk"])
+    print("local x4 F5:", kpi, "reference:", ref["summary"])
+    for k in ("hr", "ndcg"):
+        mu, sd = ref["summary"][k]["mean"], ref["summary"][k]["std"]
+        assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)

@@ -855,7 +855,9 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
                                    const Hyper& hp, const int32_t* tbase, int step,
                                    const StepBufs& sb, float* grads, hipStream_t s, double* loss,
                                    int64_t bstride, bool wt) {
-  const K2Grid k = k2_grid<G4, S, KB>(B, loss != nullptr, grads == nullptr);  // single GPU: capped
+  // single GPU: capped, when the items are many against the batch's 2B references (few items, as
+  // at the ml-1m shape, send most of their segments to K2, which the capped grid serialises)
+  const K2Grid k = k2_grid<G4, S, KB>(B, loss != nullptr, grads == nullptr && Q.rows >= 2LL * B);
   const unsigned blocks = (unsigned)k.total();
 #define BPRMF_K2(SH_, WT_)                                                                        \
   k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,       \
@@ -899,7 +901,7 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
   if (!sb.pend_q || !sb.pend_p || !sb.pstride || !bstride) return hipErrorInvalidValue;
   if (!sb.xloss) loss = nullptr;
   BPRMF_DISPATCH4(g, ({
-    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss != nullptr, true);
+    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss != nullptr, Q.rows >= 2LL * B);
     const int k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
     k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
         bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,

@@ -101,6 +101,60 @@ def load_traffic(cfg_key):
     return e.get("hbm_bytes_per_step"), src
 
 
+def relaxed_local(rl, pos, U, I, d, B, seed, local_steps, steps, warmup):
+    """The opt-in relaxed mode (semantics="local") on the same workload, as a
+    labelled sub-object of the exact line: its own model, warm-up and timed
+    region (whole merge periods: `steps` >= 1024), live HIP-event roofline, its own PMC key.  NOT
+    the reference step, never the headline `value`."""
+    import torch
+    m = rl.BPRMF(U, I, d, lr=0.01, wd=0.001, batch_size=B, num_ng=4, seed=seed, device=0,
+                 semantics="local", local_steps=local_steps)
+    m.set_train(pos)
+    n_steps = m.epoch_size()[1]
+
+    def run(first, k):
+        done = 0
+        while done < k:
+            e, s = divmod(first + done, n_steps)
+            c = min(k - done, n_steps - s)
+            m.train_steps(e, s, c)
+            done += c
+
+    run(0, warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(warmup, steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    m.profile(True)
+    run(warmup + steps, steps)
+    torch.cuda.synchronize()
+    kp = m.profile_read()
+    m.profile(False)
+    roof = None
+    if kp and kp["step_graph"]["count"]:
+        step_us = kp["step_graph"]["ms"] / kp["step_graph"]["count"] * 1e3
+        ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9
+        traffic, tsrc = (load_traffic(f"ml20m_d{d}_B{B}_local") if (U, I) == (U_ML20M, I_ML20M)
+                         else (None, None))
+        roof = dict(bound="hbm", kernel=("k_hogwild<LOCAL> (in-kernel sampling + gather + dots + "
+                                         "sigmoid + SGD scatter, hot items in per-XCD replicas) + "
+                                         "k_local_merge every period"),
+                    achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
+                    algorithmic_bytes_per_step=B * bytes_per_triplet(d),
+                    avg_us_per_step=round(step_us, 3))
+    del m
+    return {"semantics": ("relaxed (local: hogwild for users and cold items, the hot items in one "
+                          "replica per XCD merged every local_steps steps; NOT the reference step; "
+                          "opt-in, never the headline)"),
+            "value": round(steps * B / el, 1), "unit": "triplets/s", "steps": steps,
+            "warmup": warmup, "ms_per_step": round(el / steps * 1e3, 5), "local_steps": local_steps,
+            "timed_region": "one train_steps call per epoch segment, synchronised on both sides",
+            "roofline": roof,
+            "quality": "HR@10 / NDCG@10 against the exact step: DESIGN.md §5c, tools/hr_modes.py"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,6 +190,10 @@ def main():
     ap.add_argument("--step", default="segmented", choices=["segmented", "atomic"],
                     help="exact step's duplicate-row sums: segmented (sorted, one writer per row, "
                          "bitwise reproducible; the headline) or atomic (f32 atomics; a labelled line)")
+    ap.add_argument("--no-relaxed", action="store_true",
+                    help="N=1 exact line: skip its relaxed_local sub-object")
+    ap.add_argument("--relaxed-steps", type=int, default=2048,
+                    help="timed steps of the relaxed_local sub-object (whole 128-step periods)")
     ap.add_argument("--pg-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend (gloo: rehearse several ranks on one GPU, IPC "
                          "transport; RCCL refuses two ranks on one device)")
@@ -156,7 +214,12 @@ def main():
     hog = a.semantics in ("hogwild", "local")
     if a.semantics == "hogwild" and sharded:
         raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
-    dpi = a.semantics == "local" and sharded  # users sharded, item table replicated (§5d)
+    # users sharded, item table replicated and merged (§5d): only with peers to merge with (a
+    # one-rank --sharded handle runs the single-GPU local path unless BPRMF_DP_ONE_RANK is set)
+    dpi = a.semantics == "local" and sharded and (world > 1 or os.environ.get("BPRMF_DP_ONE_RANK") == "1")
+    if a.semantics == "local" and a.python_orchestration:
+        raise SystemExit("--semantics local runs through the library runner only (per-step Python "
+                         "orchestration addresses items by owner)")
     if a.step == "atomic" and (sharded or hog):
         raise SystemExit("--step atomic is the single-GPU exact step's alternative")
     if sharded:
@@ -259,7 +322,7 @@ def main():
         roof = None
         if kp and (kp["step_graph"]["count"] or kp["user_step"]["count"]):
             us = {k: v["ms"] / v["count"] * 1e3 for k, v in kp.items() if v["count"]}
-            if "step_graph" in us and sharded and world == 1 and not a.python_orchestration:
+            if "step_graph" in us and sharded and world == 1 and not a.python_orchestration and not hog:
                 # one rank: the runner dispatches to the single-GPU fused step (nothing to exchange)
                 step_us, what = us["step_graph"], ("world 1: the single-GPU fused step launches (the "
                                                    "runner has no peer to exchange with)")
@@ -268,13 +331,13 @@ def main():
                                                    "k_local_merge every local_steps + the item-table "
                                                    "merge (k_dp_delta, all-reduce, k_dp_apply) every "
                                                    "dp_steps")
-            elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
-                step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
-                                                   "user_step + item_step + grad exchange + owner apply")
             elif "step_graph" in us and a.semantics == "local":  # periods: k_hogwild + k_local_merge
                 step_us, what = us["step_graph"], ("k_hogwild<LOCAL> (in-kernel sampling + gather + dots "
                                                    "+ sigmoid + SGD scatter, hot items in per-XCD replicas) "
                                                    "+ k_local_merge every period")
+            elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
+                step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
+                                                   "user_step + item_step + grad exchange + owner apply")
             elif "step_graph" in us and hog:  # one k_hogwild launch per chunk
                 step_us, what = us["step_graph"], ("k_hogwild (in-kernel sampling + gather + dots + "
                                                    "sigmoid + SGD scatter, one launch per chunk)")
@@ -321,6 +384,12 @@ def main():
                             if not dpi else
                             "grad_bytes: the item-table merges' all-reduce, 2(W-1)/W of the table per "
                             "merge per rank (a ring's volume), averaged per step")}
+        rlx = None
+        if (world == 1 and not sharded and a.semantics == "exact" and a.step == "segmented"
+                and not a.no_relaxed):
+            del m  # the exact model's tables and buffers are not needed any more
+            rlx = relaxed_local(rl, pos, U, I, d, B, a.seed, a.local_steps or 128,
+                                max(1024, a.relaxed_steps), 256)
         cpu = None
         if not a.no_cpu_baseline and world == 1 and not sharded:
             cpu = cpu_baseline(pos, U, I, d, B)
@@ -352,6 +421,8 @@ def main():
                                         if a.step == "atomic" else
                                         "exact batch-synchronous SGD (reference step), lazy weight decay")},
                "roofline": roof, "cpu_baseline": cpu}
+        if rlx is not None:
+            out["relaxed_local"] = rlx
         if sharded:
             out["exchange"] = xch
         print(json.dumps(out), flush=True)

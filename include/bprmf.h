@@ -56,7 +56,12 @@ enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2 };
  * pushes, or the loopback's).  Staleness across GPUs is bounded by `dp_steps` steps (§5d).
  * dp_overlap = 1: the all-reduce of a merge runs on a side stream while the next period trains;
  * its sum is added one period later (the other ranks' changes arrive up to 2 dp_steps late);
- * the last merge of every call is blocking, so every rank ends a call with the same table. */
+ * the last merge of every call is blocking, so every rank ends a call with the same table.
+ * Footprint per rank at world > 1: the item table 5-6 times (Q, merge base, delta, the overlap's
+ * sum, the IPC transport's two exported buffers) plus the hot items' XCD replicas; bprmf_create
+ * refuses with BPRMF_E_UNSUPPORTED when that exceeds the device's free memory.  The per-step
+ * sharded calls (bprmf_dist_plan*, _gather_items, _apply_items, _user_step, _item_grads) address
+ * items by owner and refuse this mode; the runner (bprmf_dist_train_*) runs it. */
 
 /* How an EXACT step sums duplicate rows' gradients ("ship both").  SEGMENTED: the
  * batch is sorted by user and by item and every row is summed by one writer in a fixed order,
@@ -280,6 +285,9 @@ int bprmf_node_barrier_close(void* barrier);
 int bprmf_debug_next_build_tag(uint32_t* tag);
 /* Fill every int32 of the handle's batch buffer with `value` (stale memory, deliberately). */
 int bprmf_debug_fill_batches(bprmf_handle* h, int32_t value);
+/* Leave the batch buffer as a timed-out split build would (every batch marked dead, err bit 16):
+ * the next call's steps must skip every batch, leave the tables untouched and fail. */
+int bprmf_debug_fail_build(bprmf_handle* h);
 
 /* ---- ingestion: ratings files -> dense-coded rows (util/data_loader.py:27-146, :410-548) ---- */
 /* Host-only (no GPU).  Lines "<user> <sep> <item> <sep> <rating> <sep> <timestamp>" with any

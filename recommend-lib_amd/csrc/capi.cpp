@@ -61,12 +61,21 @@ int bprmf::ensure_trip(bprmf_handle* h, int64_t n) {
   return 0;
 }
 
+// after a timed-out build (err bit 16): the batch buffer back to zeros, as allocated, so no
+// batch keeps its dead mark (kernels.h kMetaDead) or the unfinished build's exchange words
+static hipError_t clear_batches(bprmf_handle* h) {
+  if (!h->d_batch || !h->batch_cap) return hipSuccess;
+  return hipMemsetAsync(h->d_batch, 0,
+                        sizeof(int32_t) * h->batch_cap * BatchBuf::stride_for(h->cfg.batch_size), h->stream);
+}
+
 int bprmf::check_err_flag(bprmf_handle* h) {
   int32_t e = 0;
   HIPCHK(hipMemcpyAsync(&e, h->d_err, sizeof e, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
+    if (e & 16) HIPCHK(clear_batches(h));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
@@ -153,6 +162,22 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
     h->fused = !(f && f[0] == '0') && !(w && w[0] == '0');
   }
   const int64_t ld = g.ld;
+  if (dpi) {  // every rank holds the whole item table several times over: fail early and clearly
+    // Q, its merge base, the delta table (padded to world slices), the overlap's sum buffer, and
+    // the IPC transport's two exported [W * ceil(I / W)][ld] buffers (dist_attach); the hot
+    // items' XCD replicas are at most 8 x 4096 rows on top
+    const int64_t pad = W * ((h->I + W - 1) / W);
+    const int64_t rows = h->U + h->I * 2 + pad * 3 + (h->dp_overlap ? h->I : 0) + 8 * 4096;
+    const size_t need = sizeof(float) * (size_t)(rows * ld);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && need > fr) {
+      bprmf_destroy(h);
+      return fail(BPRMF_E_UNSUPPORTED,
+                  "semantics local at world %lld replicates the %lld-row item table on every rank "
+                  "(~%.1f GB with its merge buffers) but the device has %.1f GB free",
+                  (long long)W, (long long)cfg->item_num, need / 1e9, fr / 1e9);
+    }
+  }
   TRY(dalloc(&h->P.W, h->U * ld));
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
@@ -492,6 +517,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   const int32_t e = *reinterpret_cast<const volatile int32_t*>(h->h_status);
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
+    if (e & 16) HIPCHK(clear_batches(h));
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 8) return fail(BPRMF_E_HIP, "fused step: a row's owner never published it (wait timed out)");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
@@ -553,6 +579,20 @@ int bprmf::ensure_seg(bprmf_handle* h, int64_t n_batches) {
   return 0;
 }
 
+extern "C" int bprmf_debug_fail_build(bprmf_handle* h) {
+  if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (!h->d_batch) return fail(BPRMF_E_STATE, "no batch buffer yet");
+  if (int r = set_dev(h)) return r;
+  // what a build whose wait timed out leaves (segment.hip): the dead mark in every batch's meta
+  // word and err bit 16 (the builders never clear either: the host does, when it reports the error)
+  const BatchBuf bb{h->d_batch, h->cfg.batch_size};
+  for (int64_t k = 0; k < h->batch_cap; ++k)
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(bb.view(k).meta + kMetaDead), kDeadMark, 1, h->stream));
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_err, kErrBuild, 1, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 extern "C" int bprmf_debug_fill_batches(bprmf_handle* h, int32_t value) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
   if (!h->d_batch) return fail(BPRMF_E_STATE, "no batch buffer yet");
@@ -596,7 +636,6 @@ StepBufs bprmf::step_bufs(const bprmf_handle* h) {
   b.pend_p = h->fused ? h->d_pend_p : nullptr;
   b.qrows = h->I;
   b.prows = h->U;
-  b.build_err = h->d_err;
   return b;
 }
 
@@ -1234,9 +1273,22 @@ static int dist_counts(bprmf_handle* h, int64_t n_steps, int32_t* owner_counts) 
   return check_err_flag(h);
 }
 
+// semantics LOCAL at world > 1 keeps the WHOLE item table on every rank (Q indexed by global id):
+// the per-step sharded calls address items by owner (i % world, local row i / world) and would
+// read and update the wrong rows of it.  Only the runner (bprmf_dist_train_*) runs
+// that mode.
+static int dist_per_step_ok(bprmf_handle* h) {
+  if (h && h->dp_mode)
+    return fail(BPRMF_E_UNSUPPORTED,
+                "the per-step sharded calls address items by owner; semantics local at world > 1 "
+                "replicates the item table: use bprmf_dist_train_steps / bprmf_dist_train_replay");
+  return 0;
+}
+
 int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
                     int32_t* owner_counts) {
   if (!h || first_step < 0 || n_steps <= 0 || !owner_counts) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = dist_per_step_ok(h)) return r;
   if (!seg_mode(h)) return fail(BPRMF_E_UNSUPPORTED, "sharded steps need batch_size <= %d", kMaxSegBatch);
   if (!h->d_pos_u) return fail(BPRMF_E_STATE, "call bprmf_set_train first");
   if (int r = set_dev(h)) return r;
@@ -1259,6 +1311,7 @@ int bprmf_dist_plan(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t
 int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, const int32_t* j,
                            int64_t n_steps, int32_t* owner_counts) {
   if (!h || n_steps <= 0 || !u || !i || !j || !owner_counts) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = dist_per_step_ok(h)) return r;
   if (!seg_mode(h)) return fail(BPRMF_E_UNSUPPORTED, "sharded steps need batch_size <= %d", kMaxSegBatch);
   const int64_t B = h->cfg.batch_size, n = n_steps * B, W = h->cfg.world, R = h->cfg.rank;
   for (int64_t k = 0; k < n; ++k) {
@@ -1285,6 +1338,7 @@ int bprmf_dist_plan_replay(bprmf_handle* h, const int32_t* u, const int32_t* i, 
 
 static int dist_step_ok(bprmf_handle* h, int64_t k) {
   if (!h) return fail(BPRMF_E_INVALID, "null handle");
+  if (int r = dist_per_step_ok(h)) return r;
   if (k < 0 || k >= h->plan_steps) return fail(BPRMF_E_STATE, "step %lld is not in the current plan", (long long)k);
   return set_dev(h);
 }
@@ -1299,6 +1353,7 @@ int bprmf_dist_request_ids(bprmf_handle* h, int64_t k, int32_t* ids, int64_t n) 
 
 int bprmf_dist_gather_items(bprmf_handle* h, const int32_t* rows, int64_t n, float* out) {
   if (!h || n < 0 || (n > 0 && (!rows || !out))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = dist_per_step_ok(h)) return r;
   if (int r = set_dev(h)) return r;
   HIPCHK(gather_rows(h->geom, h->Q, rows, n, h->hp, h->t + 1, out, h->d_err, h->stream));
   return 0;
@@ -1327,6 +1382,7 @@ int bprmf_dist_item_grads(bprmf_handle* h, int64_t k, float* grads) {
 
 int bprmf_dist_apply_items(bprmf_handle* h, const int32_t* rows, const float* grads, int64_t n) {
   if (!h || n < 0 || (n > 0 && (!rows || !grads))) return fail(BPRMF_E_INVALID, "bad arguments");
+  if (int r = dist_per_step_ok(h)) return r;
   if (int r = set_dev(h)) return r;
   if (int r = ensure_grad(h)) return r;
   ProfScope ps(h, BPRMF_KPROF_OWNER);

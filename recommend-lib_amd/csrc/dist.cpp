@@ -515,6 +515,10 @@ void dist_free(DistState* d) {
 }
 
 int64_t dist_chunk_steps(const bprmf_handle* h) {
+  // BPRMF_DIST_CHUNK: a shorter chunk, so tests reach chunk boundaries with small replays
+  // (read per call: a test sets it for one handle)
+  if (const char* e = getenv("BPRMF_DIST_CHUNK"))
+    if (*e) return std::max<int64_t>(1, atoll(e));
   return std::max<int64_t>(1, (int64_t(1) << 20) / h->cfg.batch_size);
 }
 
@@ -950,8 +954,12 @@ static int dp_merge(bprmf_handle* h, bool last) {
 // steps [first_step, first_step + n_steps) of this rank's epoch (sampled; slots past the rank's
 // own epoch are empty, so every rank takes the same steps and merges) or n_steps * B replayed
 // device ids ru/ri/rj (global ids, u < 0: empty slot).  The call ends merged.
+// final: this is the call's last run of steps, which ends with a blocking merge (the host then
+// sees the same table on every rank).  A replay call runs its chunks with final = false but for
+// the last, so its merges follow dp_steps like a sampled call's do.
 static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n_steps,
-                  const int32_t* ru, const int32_t* ri, const int32_t* rj, int64_t* triplets) {
+                  const int32_t* ru, const int32_t* ri, const int32_t* rj, int64_t* triplets,
+                  bool final = true) {
   const int64_t B = h->cfg.batch_size;
   if ((int64_t)h->t + n_steps >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   int64_t N = 0;
@@ -980,8 +988,8 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
     h->t += (int32_t)m;
     s += m;
     const int32_t since = h->t - (h->dp_pending ? h->dp_tp : h->dp_t);  // steps since the last merge
-    if (since >= h->dp_steps || s >= n_steps) {
-      if (int r = dp_merge(h, s >= n_steps)) return r;
+    if (since >= h->dp_steps || (final && s >= n_steps)) {
+      if (int r = dp_merge(h, final && s >= n_steps)) return r;
     } else if (la.H > 0 && h->t - h->rep_t >= h->local_steps) {
       HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->rep_t, h->t, false, h->stream));
       h->rep_t = h->t;
@@ -1178,7 +1186,7 @@ int bprmf_dist_train_replay(bprmf_handle* h, const int32_t* u, const int32_t* i,
     HIPCHK(hipMemcpyAsync(tj, j + s * B, 4 * m * B, hipMemcpyHostToDevice, h->stream));
     if (h->dp_mode) {
       int64_t unused = 0;
-      if (int r = dp_run(h, 0, 0, m, tu, ti, tj, &unused)) return r;
+      if (int r = dp_run(h, 0, 0, m, tu, ti, tj, &unused, s + m >= n_steps)) return r;
     } else if (int r = dist_chunk(h, 0, 0, m, tu, ti, tj)) {
       return r;
     }

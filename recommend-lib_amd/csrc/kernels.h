@@ -204,11 +204,17 @@ struct StepBufs {
   int32_t* pend_q = nullptr;
   int32_t* pend_p = nullptr;
   int64_t qrows = 0, prows = 0;
-  // single GPU: the call's error word; a batch build that timed out (bit 16, segment.hip) leaves
-  // its batches unfinished, so every step workgroup then returns without touching a row
-  const int32_t* build_err = nullptr;
 };
 constexpr int32_t kErrBuild = 16;
+// A batch whose build timed out (err bit 16, segment.hip) is left unfinished; the workgroup that
+// gave up also stores kDeadMark into the batch's meta[kMetaDead], and every step workgroup of that
+// batch returns without touching a row.  The word sits beside meta[0..4], which the step kernels
+// load anyway (one line: no extra load level, where a check of the call's error word cost
+// ~0.2 us per fused step, profiles/r05_ab_round4_additions.txt).  The batch buffer is zeroed when
+// allocated and again by the host when it reports err bit 16 (capi.cpp), so the mark never
+// outlives the failed call; no builder ever stores this value elsewhere in the buffer.
+constexpr int kMetaDead = 7;
+constexpr int32_t kDeadMark = (int32_t)0xDEADB175u;
 // sharded K1 over the IPC transport: wait for the peers' row flags first (flags == null: none)
 struct PeerWait {
   const int32_t* flags = nullptr;

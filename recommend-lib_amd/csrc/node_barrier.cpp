@@ -25,6 +25,8 @@ struct Shared {
   std::atomic<int32_t> count;  // ranks arrived in the current generation
   std::atomic<int32_t> gen;    // generation: bumped by the last rank to arrive
   int32_t world;
+  std::atomic<int32_t> broken;  // a rank timed out: its arrival stays counted, so the barrier is
+                                // poisoned and every later wait fails at once (close and reopen)
 };
 static_assert(std::atomic<int32_t>::is_always_lock_free, "lock-free int32 atomics");
 
@@ -64,6 +66,7 @@ int bprmf_node_barrier_open(const char* path, int32_t world, int32_t rank, int32
   if (create) {
     new (&s->count) std::atomic<int32_t>(0);
     new (&s->gen) std::atomic<int32_t>(0);
+    new (&s->broken) std::atomic<int32_t>(0);
     s->world = world;
   } else if (s->world != world) {
     const int made = s->world;  // read before the unmap
@@ -79,11 +82,16 @@ int bprmf_node_barrier_open(const char* path, int32_t world, int32_t rank, int32
 }
 
 // Every rank returns once all `world` ranks have called it (for this generation); a rank that
-// waits longer than timeout_s seconds (a peer died) gets BPRMF_E_STATE.
+// waits longer than timeout_s seconds (a peer died) gets BPRMF_E_STATE and poisons the barrier:
+// its arrival is still in `count`, so a later generation could release one rank early.  Every
+// wait on a poisoned barrier (this rank's or a peer's, also one already spinning) fails at once;
+// recreate the mapping to go on.
 int bprmf_node_barrier_wait(void* h, double timeout_s) {
   auto* b = static_cast<NodeBarrier*>(h);
   if (!b || !b->s) return fail(BPRMF_E_INVALID, "null barrier");
   Shared* s = b->s;
+  if (s->broken.load(std::memory_order_acquire))
+    return fail(BPRMF_E_STATE, "node barrier: poisoned by an earlier timeout (recreate it)");
   const int32_t g = s->gen.load(std::memory_order_acquire);
   if (s->count.fetch_add(1, std::memory_order_acq_rel) + 1 == b->world) {
     s->count.store(0, std::memory_order_relaxed);  // before the release below: the next
@@ -93,8 +101,14 @@ int bprmf_node_barrier_wait(void* h, double timeout_s) {
   const double t0 = now_s();
   for (uint32_t spin = 1; s->gen.load(std::memory_order_acquire) == g; ++spin) {
     __builtin_ia32_pause();
-    if ((spin & 4095) == 0 && timeout_s > 0 && now_s() - t0 > timeout_s)
-      return fail(BPRMF_E_STATE, "node barrier: a rank did not arrive within %g s", timeout_s);
+    if ((spin & 4095) == 0) {
+      if (s->broken.load(std::memory_order_acquire))
+        return fail(BPRMF_E_STATE, "node barrier: poisoned by a peer's timeout");
+      if (timeout_s > 0 && now_s() - t0 > timeout_s) {
+        s->broken.store(1, std::memory_order_release);
+        return fail(BPRMF_E_STATE, "node barrier: a rank did not arrive within %g s", timeout_s);
+      }
+    }
   }
   return 0;
 }

@@ -801,6 +801,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
         __builtin_amdgcn_s_sleep(1);
         if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
           atomicOr(err, 16);
+          __hip_atomic_store(v.meta + kMetaDead, kDeadMark, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -1046,6 +1047,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       __builtin_amdgcn_s_sleep(1);
       if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
         atomicOr(err, 16);
+        __hip_atomic_store(v.meta + kMetaDead, kDeadMark, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int m = 0; m < kXchWords; ++m) w[m] = 0;
         break;

@@ -159,13 +159,13 @@ static __device__ __forceinline__ void put_stamp(int32_t* stamp, int32_t t, bool
   }
 }
 
-// the call's batch build failed (err bit 16): the step leaves the tables alone
-static __device__ __forceinline__ bool build_failed(const StepBufs& sb) {
+// this batch's build timed out (kernels.h kMetaDead): the step leaves the tables alone
+static __device__ __forceinline__ bool build_failed(const BatchView& bv) {
 #ifdef BPRMF_NO_DEAD_CHECK  // diagnostic A/B only
-  (void)sb;
+  (void)bv;
   return false;
 #else
-  return sb.build_err && (*sb.build_err & kErrBuild);
+  return bv.meta[kMetaDead] == kDeadMark;
 #endif
 }
 
@@ -192,7 +192,7 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
   // blocks: the index is clamped into the batch's B records (never read past them)
   const int4 r = reinterpret_cast<const int4*>(bv.trec)[min(p, B - 1)];
   const int n = bv.meta[0];
-  const bool dead = build_failed(sb);  // the batch build failed
+  const bool dead = build_failed(bv);  // the batch build failed
   const int64_t par = sb.pstride ? (int64_t)(t & 1) : 0;  // this step's half of the buffers
   float* contrib = sb.contrib + par * sb.pstride;
   float* ugrad = sb.ugrad + par * sb.pstride;
@@ -544,7 +544,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const float* __restrict__ ugrad = sb.ugrad + par * sb.pstride;
   const float* __restrict__ xloss = sb.xloss ? sb.xloss + par * B : nullptr;
   if (!xloss) loss = nullptr;
-  const bool dead = build_failed(sb);  // the batch build failed
+  const bool dead = build_failed(bv);  // the batch build failed
   // the step's loss: the first loss_blocks(B, KB) workgroups (dispatched first, off the tail) each
   // sum log(1 + e^-x) over KB triplets, one per thread, in a fixed tree, and add it to their own
   // slot loss[b] (one writer per slot per launch; the host adds the slots once per call)

@@ -238,6 +238,10 @@ class BPRMF:
         v = int(value) & 0xFFFFFFFF
         _lib.check(self._L.bprmf_debug_fill_batches(self._h, v - (1 << 32) if v >> 31 else v))
 
+    def debug_fail_build(self):
+        """Leave the batches as a timed-out build would (tests only): the next call fails."""
+        _lib.check(self._L.bprmf_debug_fail_build(self._h))
+
     # -- weights -------------------------------------------------------------------------------
     def local_rows(self):
         u, i = ctypes.c_int64(), ctypes.c_int64()

@@ -305,7 +305,15 @@ class ShardedBPRMF:
         self._plan = None
         return self.steps_per_epoch
 
+    def _per_step_ok(self):
+        # semantics "local" keeps the whole item table on every rank; the per-step calls address
+        # items by owner (i % world), so only the runner (train_steps / train_replay) runs it
+        if self.semantics == "local":
+            raise ValueError('semantics="local" runs through the library runner only '
+                             '(attach_runner + train_steps / train_replay), not per-step orchestration')
+
     def _ensure_plan(self, epoch, step):
+        self._per_step_ok()
         p = self._plan
         if p is not None and p[0] == epoch and p[1] <= step < p[1] + p[2]:
             return
@@ -335,6 +343,7 @@ class ShardedBPRMF:
 
     def plan_replay(self, batches):
         """Replay plan (per-step Python orchestration) from GLOBAL batches, see _local_batches."""
+        self._per_step_ok()
         U, I, J, n = self._local_batches(batches)
         send = self.b.plan_replay(U, I, J, n)
         recv = self.comm.exchange_counts(send, self.device)
@@ -411,6 +420,7 @@ class ShardedBPRMF:
         return self._run(step - self._plan[1], want_loss)
 
     def step_replay(self, k, want_loss=False):
+        self._per_step_ok()
         return self._run(k, want_loss)
 
     def _run(self, k, want_loss):

@@ -134,3 +134,31 @@ def test_sharded_plan_build_ignores_planted_tags(rl, world):
                 assert not bad.any(), (f"step {k}, rank {r}: {name} differs from the dense oracle in "
                                        f"{int(bad.sum())} of {bad.size} elements "
                                        f"(max {np.abs(got - want).max():.3g})")
+
+
+def test_timed_out_build_leaves_tables_untouched(rl):
+    """A batch whose split build timed out carries a dead mark (kernels.h kMetaDead) that every
+    step workgroup of that batch reads beside meta[0]: the steps skip it and the call fails with
+    the builder's error.  The step counter still advances (rows decay lazily as over steps with no
+    triplets), so the tables equal the earlier ones times the decay of those steps; the host clears
+    the buffer, and the next call trains normally."""
+    syn = importlib.import_module("recommend-lib_amd.synthetic")
+    U, I, d, B, seed = 900, 700, 32, 512, 5
+    lr, wd = 0.05, 0.001
+    pos = syn.make_positives(U, I, 20_000, seed)
+    m = rl.BPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, seed=seed, device=0)
+    m.set_train(pos)
+    m.train_steps(0, 0, 4)
+    P0, Q0 = m.get_weights()
+    m.debug_fail_build()
+    with pytest.raises(rl.BprmfError, match="batch builder"):
+        # a short chunk: the split builder (the one with the timed waits), then fused steps
+        m.train_steps(0, 4, 6)
+    P1, Q1 = m.get_weights()
+    dec = (1 - lr * wd) ** 6  # a real step moves rows by ~1e-2 relative: far outside rtol
+    np.testing.assert_allclose(P1, P0 * dec, rtol=2e-6, atol=1e-9)
+    np.testing.assert_allclose(Q1, Q0 * dec, rtol=2e-6, atol=1e-9)
+    st = m.train_steps(0, 10, 6)
+    assert np.isfinite(st["loss"]) and st["loss"] > 0
+    P2, _ = m.get_weights()
+    assert not np.allclose(P2, P1 * dec, rtol=1e-4)

@@ -228,3 +228,66 @@ def test_local_dp_trains_ml100k_protocol(rl, golden):
     for k in ("hr", "ndcg"):
         mu, sd = ref["summary"][k]["mean"], ref["summary"][k]["std"]
         assert abs(kpi[k] - mu) <= 4 * sd + 1e-9, (k, kpi[k], mu, sd)
+
+
+def test_local_dp_replay_merges_follow_dp_steps_across_chunks(rl, monkeypatch):
+    """A replay longer than the runner's chunk (BPRMF_DIST_CHUNK=2 here; 2^20 / B steps by
+    default) merges every dp_steps steps and at the call's end, like a sampled call, not at every
+    chunk boundary: the SERIAL build against local_dp_serial with dp_steps 5."""
+    monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
+    monkeypatch.setenv("BPRMF_DIST_CHUNK", "2")
+    H, world, period, dp = 4, 2, 3, 5
+    monkeypatch.setenv("BPRMF_LOCAL_HOT", str(H))
+    g = np.random.default_rng(77)
+    U, I, d, B, steps = 23, 19, 32, 8, 7
+    lr, wd = 0.05, 0.01
+    rows = [(u, it) for u in range(U) for it in range(I) if g.random() < 0.3 / (1 + it % 5)]
+    pos = np.unique(np.array(rows, np.int64), axis=0)
+    P0 = (0.1 * g.standard_normal((U, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I, d))).astype(np.float32)
+    trips = []
+    for r in range(world):
+        u = g.choice(np.arange(r, U, world), steps * B)
+        i, j = g.integers(0, I, steps * B), g.integers(0, I, steps * B)
+        i[::3] = 0
+        trips.append((u, i, j))
+    batches = [tuple(np.concatenate([trips[r][x][k * B:(k + 1) * B] for r in range(world)])
+                     for x in range(3)) for k in range(steps)]
+    sh = rl.sharded
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(U, I, d, lr=lr, wd=wd, batch_size=B, device=0, comm=comm,
+                            semantics="local", local_steps=period, dp_steps=dp)
+        m.set_train(pos)
+        m.set_weights(sh.shard_rows(P0, r, world), Q0)
+        m.attach_runner("loopback", key=7700)
+        return m.train_replay(batches), m.get_weights()
+
+    parts = _threads(rl, world, fn)
+    Pp = [sh.shard_rows(P0, r, world).copy() for r in range(world)]
+    hots = [_hot_set(pos, r, world, I, H) for r in range(world)]
+    loss, _, Qw = O.local_dp_serial(Pp, Q0.copy(), trips, lr, wd, B, hots, period, dp, world)
+    np.testing.assert_allclose(parts[0][1][1], Qw, rtol=1e-5, atol=HOG_ATOL)
+    assert np.array_equal(parts[1][1][1], parts[0][1][1])
+    assert sum(p[0]["loss"] for p in parts) == pytest.approx(loss, rel=1e-5)
+
+
+def test_local_dp_refuses_per_step_calls(rl):
+    """The per-step sharded API addresses items by owner (i % world); with the item table
+    replicated (semantics "local", world > 1) it is refused instead of updating wrong rows."""
+    sh = rl.sharded
+    pos = np.array([[u, (u * 7 + k) % 13] for u in range(10) for k in range(3)], np.int64)
+
+    def fn(comm, r):
+        m = sh.ShardedBPRMF(10, 13, 32, batch_size=8, device=0, comm=comm, semantics="local")
+        m.set_train(pos)
+        with pytest.raises(ValueError, match="runner"):
+            m.step(0, 0)
+        with pytest.raises(ValueError, match="runner"):
+            m.plan_replay([(np.array([0, 1]), np.array([1, 2]), np.array([3, 4]))])
+        # and the C ABI itself refuses (a caller that bypasses the Python check)
+        with pytest.raises(Exception, match="replicates the item table"):
+            m.b.plan(0, 0, 1)
+        return True
+
+    assert all(_threads(rl, 2, fn))

@@ -53,6 +53,17 @@ def test_missing_rank_times_out(rl, tmp_path):
     with pytest.raises(Exception):
         b.wait(0.2)
     assert time.monotonic() - t0 < 10
+    # the timed-out arrival is still counted: the barrier is poisoned, so a peer arriving now
+    # (which would otherwise complete the generation with one rank short) and every later wait
+    # of this rank fail at once
+    peer = rl.sharded.NodeBarrier(path, 2, 1, create=False)
+    t0 = time.monotonic()
+    with pytest.raises(Exception, match="poisoned"):
+        peer.wait(30.0)
+    with pytest.raises(Exception, match="poisoned"):
+        b.wait(30.0)
+    assert time.monotonic() - t0 < 5
+    peer.close()
     with pytest.raises(Exception):  # a different world size on the same file is refused
         rl.sharded.NodeBarrier(path, 3, 1, create=False)
     b.close()

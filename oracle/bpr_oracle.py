@@ -74,6 +74,57 @@ def train_replay(P, Q, triplets, bounds, lr, wd):
     return np.array(losses)
 
 
+def bpr_step_stale(P, Q, Qs, u, i, j, lr, wd):
+    """One step of the reference (bpr_step_dense) whose forward and gradients read the item rows
+    Qs instead of Q (the rows a stale-1 sharded step receives, see sharded_stale1_serial); the
+    update is applied to the current P and Q (their weight decay included), exactly torch's SGD
+    given those gradients.  In place; returns the loss."""
+    f32 = np.float32
+    lr = f32(lr)
+    wd = f32(wd)
+    u = np.asarray(u, dtype=np.int64)
+    i = np.asarray(i, dtype=np.int64)
+    j = np.asarray(j, dtype=np.int64)
+    pu, qi, qj = P[u], Qs[i], Qs[j]
+    x = (pu * qi).sum(-1, dtype=f32) - (pu * qj).sum(-1, dtype=f32)
+    s = (f32(1) / (f32(1) + np.exp(-x, dtype=f32))).astype(f32)
+    with np.errstate(divide="ignore"):
+        loss = float(-np.log(s.astype(np.float64)).sum())
+    c = (f32(1) - s).astype(f32)
+    gP = np.zeros_like(P)
+    gQ = np.zeros_like(Q)
+    np.add.at(gP, u, (-c)[:, None] * qi + c[:, None] * qj)
+    np.add.at(gQ, i, (-c)[:, None] * pu)
+    np.add.at(gQ, j, c[:, None] * pu)
+    for W, G in ((P, gP), (Q, gQ)):
+        W -= lr * (G + wd * W)
+    return loss
+
+
+def sharded_stale1_serial(P, Q, batches, lr, wd, chunk):
+    """The opt-in stale-1 sharded step (semantics "stale1", csrc/dist.cpp enqueue_stale1), as one
+    table: the spec, NOT the reference step.  The runner overlaps step k's gradient exchange and
+    the owners' apply with step k+1's compute, so the item rows a step reads miss the previous
+    step's gradients: step t reads Q_{t-2} (the table after step t-2) brought to step t-1 by the
+    weight decay alone, i.e. a * Q_{t-2} (a = 1 - lr wd; the owners' gather decays rows to the
+    consuming step, dist_body.h owner_gather_body).  Users are owned by their rank and stay exact:
+    P is current.  The first step of every runner chunk (`chunk` steps; the plans change there)
+    reads the current table.  The update is the reference's SGD on the current P and Q with the
+    gradients taken at those rows (bpr_step_stale).  With chunk = 1 every step is the reference
+    step.  batches: the union batch of every step (u, i, j).  In place; returns per-step losses."""
+    a = np.float32(1) - np.float32(lr) * np.float32(wd)
+    losses = []
+    prev = None  # the table before the previous step's update (a step that was not a chunk start)
+    for k, (u, i, j) in enumerate(batches):
+        if k % chunk == 0:
+            Qs = Q.copy()
+        else:
+            Qs = (prev * a).astype(np.float32)
+        prev = Q.copy()
+        losses.append(bpr_step_stale(P, Q, Qs, u, i, j, lr, wd))
+    return np.array(losses)
+
+
 def hogwild_serial(P, Q, u, i, j, lr, wd, B, t0=0, sP=None, sQ=None):
     """The opt-in relaxed mode (semantics "hogwild", csrc/hogwild.hip) run serially: the spec its
     SERIAL test build (BPRMF_HOGWILD_SERIAL=1: one lane group, slot order) must reproduce.

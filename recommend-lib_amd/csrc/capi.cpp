@@ -106,8 +106,13 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   Geom g;
   if (!make_geom(cfg->factor_num, &g)) return fail(BPRMF_E_UNSUPPORTED, "factor_num must be in [1, 1024]");
   if (cfg->semantics != BPRMF_SEM_EXACT && cfg->semantics != BPRMF_SEM_HOGWILD &&
-      cfg->semantics != BPRMF_SEM_LOCAL)
-    return fail(BPRMF_E_INVALID, "semantics must be BPRMF_SEM_EXACT (0), _HOGWILD (1) or _LOCAL (2)");
+      cfg->semantics != BPRMF_SEM_LOCAL && cfg->semantics != BPRMF_SEM_STALE1)
+    return fail(BPRMF_E_INVALID,
+                "semantics must be BPRMF_SEM_EXACT (0), _HOGWILD (1), _LOCAL (2) or _STALE1 (3)");
+  if (cfg->semantics == BPRMF_SEM_STALE1 &&
+      (cfg->step_mode != BPRMF_STEP_SEGMENTED || cfg->batch_size > kMaxSegBatch))
+    return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics: the segmented sharded step (batch_size <= %d)",
+                kMaxSegBatch);
   if (cfg->semantics == BPRMF_SEM_HOGWILD && cfg->world != 1)
     return fail(BPRMF_E_UNSUPPORTED, "hogwild semantics: single-GPU handles only");
   if (cfg->local_steps < 0 || cfg->dp_steps < 0)
@@ -391,13 +396,14 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   feistel_dims(N, &h->feistel_a, &h->feistel_c);
   // single GPU: the step buffers of a whole chunk and the step graphs, now rather than inside
   // the first calls (a larger chunk later would reallocate and recapture)
-  if (seg_mode(h) && h->semantics == BPRMF_SEM_EXACT) {
+  if (seg_mode(h) && (h->semantics == BPRMF_SEM_EXACT || h->semantics == BPRMF_SEM_STALE1)) {
     const int64_t B = h->cfg.batch_size;
-    const int64_t steps = h->cfg.world == 1 ? chunk_triplets(h) / B : dist_chunk_steps(h);
+    const bool one = h->cfg.world == 1 && h->semantics == BPRMF_SEM_EXACT;  // the single-GPU step
+    const int64_t steps = one ? chunk_triplets(h) / B : dist_chunk_steps(h);
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(steps, ((int64_t)N + B - 1) / B));
     if (int r = ensure_seg(h, nb)) return r;
     if (int r = ensure_trip(h, nb * B)) return r;
-    if (h->cfg.world == 1 && h->use_graphs)
+    if (one && h->use_graphs)
       if (int r = ensure_step_graphs(h)) return r;
   }
   return 0;
@@ -776,6 +782,9 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
   const int64_t B = h->cfg.batch_size;
   const int64_t nb = (n + B - 1) / B;
   if ((int64_t)h->t + nb >= INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
+  if (h->semantics == BPRMF_SEM_STALE1)
+    return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics run through the sharded runner "
+                                     "(bprmf_dist_init_* + bprmf_dist_train_*)");
   if (h->semantics == BPRMF_SEM_LOCAL) {
     // periods of local_steps steps: one hogwild launch (hot items in the XCD replicas), then the
     // merge; the call's last period is merged too, so the base table is current when it returns

@@ -494,6 +494,13 @@ struct DistState {
   float* rows_recv = nullptr;   // shared, requester: [W][S][ld] (slot order)
   float* grads_send = nullptr;  // requester: [W][S][ld]
   float* grads_recv = nullptr;  // shared, owner: [W][cap][ld] (cap <= S)
+  // semantics STALE1 (enqueue_stale1): the second parity of rows_recv and grads_send, the owner
+  // stream (gradient exchange, apply, gather, row exchange) and the events that order it against
+  // the compute stream (h->stream)
+  float* rows_recv1 = nullptr;
+  float* grads_send1 = nullptr;
+  hipStream_t xs = nullptr;
+  hipEvent_t ev_rows[4] = {}, ev_k2[4] = {}, ev_fork = nullptr, ev_join = nullptr;
 };
 
 static void drop_dist_graphs(DistState* d) {
@@ -505,6 +512,13 @@ static void drop_dist_graphs(DistState* d) {
 void dist_free(DistState* d) {
   if (!d) return;
   drop_dist_graphs(d);
+  if (d->xs) (void)!hipStreamSynchronize(d->xs);
+  for (hipEvent_t e : {d->ev_rows[0], d->ev_rows[1], d->ev_rows[2], d->ev_rows[3], d->ev_k2[0],
+                       d->ev_k2[1], d->ev_k2[2], d->ev_k2[3], d->ev_fork, d->ev_join})
+    if (e) (void)!hipEventDestroy(e);
+  if (d->xs) (void)!hipStreamDestroy(d->xs);
+  for (void* p : {(void*)d->rows_recv1, (void*)d->grads_send1})
+    if (p) (void)!hipFree(p);
   void* shared[] = {d->ids_recv, d->vals, d->rows_recv, d->grads_recv};
   for (void* p : shared) d->tr->free_shared(p);
   void* ptrs[] = {d->ids_send, d->aplan[0], d->aplan[1], d->d_cap, d->rows_send, d->grads_send};
@@ -583,6 +597,19 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   // chunk ever reallocates one inside a call (a free synchronises the device)
   for (int par = 0; par < 2; ++par)
     if (int r = ensure_aplan(h, par, d->nmax, d->S)) return r;
+  if (h->semantics == BPRMF_SEM_STALE1) {  // enqueue_stale1's second parities, stream, events
+    if (dynamic_cast<IpcTransport*>(tr))
+      return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics: attach the rccl or loopback transport "
+                                       "(the IPC transport's step kernels wait on their own flags)");
+    if (int r = dalloc(&d->rows_recv1, rows)) return r;
+    if (int r = dalloc(&d->grads_send1, rows)) return r;
+    HIPCHK(hipMemsetAsync(d->rows_recv1, 0, sizeof(float) * rows, h->stream));
+    HIPCHK(hipMemsetAsync(d->grads_send1, 0, sizeof(float) * rows, h->stream));
+    HIPCHK(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&d->ev_rows[0], &d->ev_rows[1], &d->ev_rows[2], &d->ev_rows[3], &d->ev_k2[0],
+                          &d->ev_k2[1], &d->ev_k2[2], &d->ev_k2[3], &d->ev_fork, &d->ev_join})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
   // rows past a peer's request count are sent but never read; keep them finite
   HIPCHK(hipMemsetAsync(d->rows_send, 0, sizeof(float) * rows, h->stream));
   HIPCHK(hipMemsetAsync(d->grads_send, 0, sizeof(float) * rows, h->stream));
@@ -602,10 +629,97 @@ static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   return 0;
 }
 
+// Semantics STALE1 (include/bprmf.h, spec oracle/bpr_oracle.py sharded_stale1_serial): the
+// owner side of step k (its gradient exchange, the owners' apply, then the gather and row
+// exchange of step k+2) runs on the owner stream d->xs while step k+1 computes on h->stream.
+//   owner stream:   gather(0) xchg rows(0) [E_rows 0]  gather(1) xchg rows(1) [E_rows 1]
+//                   then per k: wait E_k2 k, xchg grads(k), apply(k), gather(k+2), xchg rows(k+2)
+//                   [E_rows k+2]
+//   compute stream: per k: wait E_rows k, K1(k) on rows parity k & 1, K2(k) -> grads parity
+//                   k & 1 [E_k2 k]
+// So step k+2 reads the rows after apply(k), brought to its step t-1 by weight decay alone
+// (owner_gather_body): one step stale, where the exact runner's gather waits for apply(k+1).
+// Hazards: rows(k+2) lands in parity k & 1 after K1(k) has read it (the owner stream waited for
+// K2(k), which follows K1(k)); K2(k+2) rewrites gradient parity k & 1 only after its K1 waited
+// for E_rows(k+2), which the owner stream records after it sent grads(k) from there; grads_recv,
+// rows_send and the table itself are touched by the owner stream alone, user rows and the step
+// buffers by the compute stream alone.  Exchanges run with h->stream switched to the owner
+// stream (the transports enqueue on h->stream).  hipGraph capture works as for the exact runner:
+// the owner stream forks from and joins the capturing stream through events.
+static int enqueue_stale1(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
+                          const int32_t* aplan) {
+  DistState* d = h->dist;
+  const int B = h->cfg.batch_size, W = h->cfg.world;
+  const int ld = h->geom.ld;
+  const BatchBuf bb{h->d_batch, B};
+  const int self = d->tr->self_exchange ? -1 : h->cfg.rank;
+  const int64_t R = h->cfg.rank;
+  const size_t row_bytes = sizeof(float) * (size_t)cap * ld;
+  hipStream_t cs = h->stream, xs = d->xs;
+  float* rows_par[2] = {d->rows_recv, d->rows_recv1};
+  float* grads_par[2] = {d->grads_send, d->grads_send1};
+  std::vector<const void*> sp(W);
+  std::vector<void*> rp(W);
+  struct Restore {  // h->stream back to the compute stream on every exit
+    bprmf_handle* h;
+    hipStream_t s;
+    ~Restore() { h->stream = s; }
+  } restore{h, cs};
+  auto gather_and_send = [&](int64_t k) -> int {  // on the owner stream
+    float* rin = rows_par[k & 1];
+    PushArgs gd{};
+    for (int p = 0; p < W; ++p)
+      gd.dst[p] = p == self ? rin + R * d->S * ld : d->rows_send + (int64_t)p * cap * ld;
+    HIPCHK(dist_owner_gather(h->geom, h->Q, ids_recv, n, W, cap, (int)k, h->hp, h->d_tbase, gd,
+                             nullptr, h->d_err, kBoardMax, xs));
+    for (int p = 0; p < W; ++p) {
+      sp[p] = p == self ? nullptr : d->rows_send + (int64_t)p * cap * ld;
+      rp[p] = rin + (int64_t)p * d->S * ld;
+    }
+    h->stream = xs;
+    const int r = d->tr->exchange(h, Xchg{X_ROWS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0});
+    h->stream = cs;
+    if (r) return r;
+    HIPCHK(hipEventRecord(d->ev_rows[k & 3], xs));
+    return 0;
+  };
+  HIPCHK(hipEventRecord(d->ev_fork, cs));  // the chunk's batches, plan and cursor are in place
+  HIPCHK(hipStreamWaitEvent(xs, d->ev_fork, 0));
+  for (int64_t k = 0; k < std::min<int64_t>(2, n); ++k)
+    if (int r = gather_and_send(k)) return r;
+  for (int64_t k = 0; k < n; ++k) {
+    const BatchView v = bb.view(k);
+    float* gs = grads_par[k & 1];
+    HIPCHK(hipStreamWaitEvent(cs, d->ev_rows[k & 3], 0));
+    HIPCHK(user_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_xloss, h->d_contrib,
+                     h->d_ugrad, rows_par[k & 1], cs));
+    HIPCHK(item_step(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib, h->d_ugrad,
+                     gs, cs, h->d_xloss, h->d_loss));
+    HIPCHK(hipEventRecord(d->ev_k2[k & 3], cs));
+    HIPCHK(hipStreamWaitEvent(xs, d->ev_k2[k & 3], 0));
+    for (int p = 0; p < W; ++p) {
+      sp[p] = p == self ? nullptr : gs + (int64_t)p * d->S * ld;
+      rp[p] = d->grads_recv + (int64_t)p * cap * ld;
+    }
+    h->stream = xs;
+    const int r = d->tr->exchange(h, Xchg{X_GRADS, sp.data(), rp.data(), row_bytes, h->d_tbase, (int)k, 0});
+    h->stream = cs;
+    if (r) return r;
+    HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)k, h->hp, h->d_tbase,
+                            d->grads_recv, self, gs + R * d->S * ld, nullptr, h->d_err, xs));
+    if (k + 2 < n)
+      if (int r2 = gather_and_send(k + 2)) return r2;
+  }
+  HIPCHK(hipEventRecord(d->ev_join, xs));  // the last apply before anything after the chunk
+  HIPCHK(hipStreamWaitEvent(cs, d->ev_join, 0));
+  return 0;
+}
+
 // The per-step launches and exchanges of a chunk of n steps (plan of `cap` rows per peer):
 // enqueued eagerly or captured into a hipGraph by dist_chunk.
 static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
                          const int32_t* aplan, bool prof_kernels) {
+  if (h->semantics == BPRMF_SEM_STALE1) return enqueue_stale1(h, n, cap, ids_recv, aplan);
   DistState* d = h->dist;
   const int B = h->cfg.batch_size, W = h->cfg.world;
   const int ld = h->geom.ld;
@@ -1139,8 +1253,9 @@ int bprmf_dist_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, 
     return end_call(h, st, trip, n_steps);
   }
   // one rank: nothing to exchange, so the single-GPU fused step runs (the same sampler stream,
-  // the same step; BPRMF_DIST_W1_RUNNER=1 keeps the runner, to measure it)
-  if (h->cfg.world == 1 && !h->dist->tr->self_exchange) {
+  // the same step; BPRMF_DIST_W1_RUNNER=1 keeps the runner, to measure it).  STALE1 keeps the
+  // runner (its rows are stale at one rank too).
+  if (h->cfg.world == 1 && !h->dist->tr->self_exchange && h->semantics != BPRMF_SEM_STALE1) {
     const char* e = getenv("BPRMF_DIST_W1_RUNNER");
     if (!(e && e[0] == '1')) return bprmf_train_steps(h, epoch, first_step, n_steps, st);
   }

@@ -39,7 +39,7 @@ def _as_pairs(train_set):
 # (the default); "hogwild" is the opt-in relaxed mode (lock-free per-triplet updates, weight decay
 # still once per row per step; single GPU); "local" is hogwild with the hot items
 # in per-XCD replicas merged every local_steps steps
-SEMANTICS = {"exact": 0, "hogwild": 1, "local": 2}
+SEMANTICS = {"exact": 0, "hogwild": 1, "local": 2, "stale1": 3}
 # how an exact step sums duplicate rows (include/bprmf.h BPRMF_STEP_*): "segmented" = sorted,
 # one writer per row, bitwise reproducible (batch_size <= 8192); "atomic" = f32 atomics, any batch
 # size, the same step up to the order of the fp32 sums

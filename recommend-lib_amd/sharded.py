@@ -276,7 +276,12 @@ class ShardedBPRMF:
     tables are merged (decayed base + the sum of the ranks' changes; one all-reduce) every
     `dp_steps` steps and at the end of every call (`dp_overlap`: each merge's all-reduce runs
     beside the next period, its sum added one period later).  Runner only (attach_runner "rccl" or
-    "loopback"); get_weights / set_weights then take (P_local, Q_full)."""
+    "loopback"); get_weights / set_weights then take (P_local, Q_full).
+
+    semantics="stale1" (opt-in, not the reference step): the exact sharded step with
+    the item rows one step stale (oracle/bpr_oracle.py sharded_stale1_serial): each step's
+    gradient exchange and the owners' apply run beside the next step's compute.  Runner only
+    (attach_runner "rccl" or "loopback")."""
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, init_std=0.01, seed=0, device=0, group=None, comm=None, backend=None,
@@ -308,8 +313,8 @@ class ShardedBPRMF:
     def _per_step_ok(self):
         # semantics "local" keeps the whole item table on every rank; the per-step calls address
         # items by owner (i % world), so only the runner (train_steps / train_replay) runs it
-        if self.semantics == "local":
-            raise ValueError('semantics="local" runs through the library runner only '
+        if self.semantics in ("local", "stale1"):
+            raise ValueError(f'semantics="{self.semantics}" runs through the library runner only '
                              '(attach_runner + train_steps / train_replay), not per-step orchestration')
 
     def _ensure_plan(self, epoch, step):
@@ -365,8 +370,10 @@ class ShardedBPRMF:
             self.b.runner_rccl(uid)
         elif transport == "ipc":
             self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
-        elif transport == "auto" and self.semantics == "local":
-            return self.attach_runner("rccl")  # the item merge is an all-reduce
+        elif transport == "auto" and self.semantics in ("local", "stale1"):
+            # local: the item merge is an all-reduce; stale1: the owner stream's exchanges are
+            # host-ordered RCCL send/recv (the IPC transport's kernels wait on their own flags)
+            return self.attach_runner("rccl")
         elif transport == "auto":  # ipc where every rank can map its peers, else rccl
             # Every rank joins every collective whatever failed locally: a status byte travels
             # with the handles, so a rank whose export failed cannot leave its peers waiting in

@@ -286,3 +286,34 @@ def test_local_dp_spec_one_rank_is_local_serial_and_ranks_add_changes():
             O.local_serial(Pr, Qr, tr[r][0][sl] // 2, tr[r][1][sl], tr[r][2][sl], 0.05, 0.0, B, [], 3, t0=t0)
         half = slice(12 * r, 12 * (r + 1))
         np.testing.assert_allclose(Qm[half], Qr[half], rtol=1e-5, atol=1e-7)
+
+
+def test_stale1_spec_reduces_to_reference_and_reads_stale_rows():
+    """sharded_stale1_serial (semantics "stale1"): with one step per runner chunk every step reads
+    the current table, i.e. the reference step exactly; with longer chunks step t's forward reads
+    a * Q_{t-2}: checked against a direct construction of step 2 from the stored tables."""
+    g = np.random.default_rng(4)
+    U_, I_, d = 17, 11, 8
+    lr, wd = 0.05, 0.01
+    P0 = (0.1 * g.standard_normal((U_, d))).astype(np.float32)
+    Q0 = (0.1 * g.standard_normal((I_, d))).astype(np.float32)
+    bs = [(g.integers(0, U_, 9), g.integers(0, I_, 9), g.integers(0, I_, 9)) for _ in range(4)]
+    P1, Q1 = P0.copy(), Q0.copy()
+    l1 = O.sharded_stale1_serial(P1, Q1, bs, lr, wd, 1)
+    P2, Q2 = P0.copy(), Q0.copy()
+    l2 = [O.bpr_step_dense(P2, Q2, *b, lr, wd) for b in bs]
+    assert np.array_equal(P1, P2) and np.array_equal(Q1, Q2) and np.allclose(l1, l2, rtol=0)
+    # chunk 4: steps 0 and 1 read Q0 (step 1: a * Q0), step 2 reads a * (Q after step 0)
+    P3, Q3 = P0.copy(), Q0.copy()
+    O.sharded_stale1_serial(P3, Q3, bs[:3], lr, wd, 4)
+    a = np.float32(1) - np.float32(lr) * np.float32(wd)
+    Pa, Qa = P0.copy(), Q0.copy()
+    O.bpr_step_dense(Pa, Qa, *bs[0], lr, wd)          # step 0: exact
+    Q_after0 = Qa.copy()
+    O.bpr_step_stale(Pa, Qa, (Q0 * a).astype(np.float32), *bs[1], lr, wd)
+    O.bpr_step_stale(Pa, Qa, (Q_after0 * a).astype(np.float32), *bs[2], lr, wd)
+    assert np.array_equal(P3, Pa) and np.array_equal(Q3, Qa)
+    Pe, Qe = P0.copy(), Q0.copy()
+    for b in bs[:3]:
+        O.bpr_step_dense(Pe, Qe, *b, lr, wd)
+    assert np.abs(Q3 - Qe).max() > 1e-6  # not the reference step

@@ -2,13 +2,63 @@
 per world size, each rank's distinct items per step, how many are remote, the largest per-owner
 request count (the exchange capacity), the union of all ranks' items per step, and the share of a
 rank's rows at step k+1 that some rank updated at step k.  CPU only (the oracle's C sampler, each
-rank's shard seed, 8 steps of B = 4096)."""
+rank's shard seed, 8 steps of B = 4096).
+
+  python tools/xch_stats.py            # ml-20m shape (C3), then the one-hop schedule
+  python tools/xch_stats.py c5         # the C5 shape (100M items, d = 256): drawn directly
+
+C5 (BASELINE configs[4]: 10M users x 100M items, d = 256, 8 GPUs): building the 1.4e8-positive
+set and its sampler is not needed for the exchange volume -- a step's positive items follow the
+items' popularity (Zipf alpha = 1 over a random order, synthetic.make_positives) and its negatives
+are uniform over the catalogue, so each rank's 8 steps are drawn that way (the user side never
+crosses a link)."""
 import sys, importlib, numpy as np
 sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 from oracle import bpr_oracle as O
 from oracle import c_oracle as C
 syn = importlib.import_module("recommend-lib_amd.synthetic")
 U, I, B = 138493, 26744, 4096
+
+if len(sys.argv) > 1 and sys.argv[1] == "c5":
+    I5, d5, steps = 100_000_000, 256, 8
+    g = np.random.default_rng(5)
+    # inverse CDF of Zipf(1) over ranks 1..I5: H(r) ~ ln r + gamma
+    gamma = 0.5772156649
+    HN = np.log(I5) + gamma
+    order_seed = np.random.default_rng(6)
+    perm_a, perm_b = int(order_seed.integers(1, I5)) | 1, int(order_seed.integers(0, I5))
+
+    def item_of_rank(r):  # a fixed random order of the catalogue (affine bijection mod I5)
+        return (perm_a * r + perm_b) % I5
+
+    for W in (1, 2, 4, 8):
+        caps, distinct, remote, union, upd = [], [], [], [], []
+        sets = [[None] * steps for _ in range(W)]
+        for r in range(W):
+            for k in range(steps):
+                # B positives (each triplet one; a positive recurs num_ng times per epoch) + B negatives
+                rk = np.minimum(np.exp(g.random(B) * HN - gamma), I5 - 1).astype(np.int64)
+                i = item_of_rank(rk)
+                j = g.integers(0, I5, B)
+                it = np.unique(np.concatenate([i, j]))
+                sets[r][k] = it
+                distinct.append(len(it))
+                own = np.bincount(it % W, minlength=W)
+                caps.append(own.max())
+                remote.append(len(it) - own[r])
+        for k in range(steps):
+            union.append(len(np.unique(np.concatenate([sets[r][k] for r in range(W)]))))
+        for r in range(W):
+            for k in range(steps - 1):
+                prev = np.unique(np.concatenate([sets[q][k] for q in range(W)]))
+                upd.append(np.isin(sets[r][k + 1], prev).mean())
+        rb = 4 * d5
+        print(f"C5 W={W}: distinct/rank/step {np.mean(distinct):.0f} of {2 * B} refs, remote "
+              f"{np.mean(remote):.0f}, max per-owner cap {np.max(caps)}, union/step {np.mean(union):.0f}, "
+              f"frac of next-step rows updated last step {np.mean(upd):.3f}, per-link bytes/hop "
+              f"(padded cap x {rb} B) {np.max(caps) * rb / 1e3:.0f} KB, all links/rank/hop "
+              f"{np.max(caps) * rb * max(W - 1, 0) / 1e6:.2f} MB")
+    sys.exit(0)
 pos = syn.make_positives(U, I, 10_000_000, 20261015)
 for W in (1, 2, 4, 8):
     caps, distinct, remote, union = [], [], [], []

@@ -177,11 +177,36 @@ static __device__ __forceinline__ bool build_failed(const BatchView& bv) {
 // rows with t (users: only those K2 finishes), for K1 of step t+1.  pw (sharded, fused front
 // launch): the record and the user row are loaded first, then the workgroup waits for the row
 // flags, then the item rows are read.
+// Diagnostic builds only (-DBPRMF_DIAG_WAIT=m, tools/gpu/ab_prof.sh; WRONG results, timing only):
+// which of K1's waits for rows K2 publishes set the fused launch's length.  The K2 batch's hot
+// items (its lrec list, > kLongSeg references) are staged in LDS; m = 1: K1 never waits for the
+// other (cold) rows, m = 2: never for the hot ones, m = 3: waits as shipped (the staging's cost).
+#ifdef BPRMF_DIAG_WAIT
+#define BPRMF_DIAG_PREV , const BatchView* prev = nullptr
+#else
+#define BPRMF_DIAG_PREV
+#endif
 template <int G4, int S, bool SH, bool WT, bool WAIT>
 static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, const float* __restrict__ item_rows,
-                                               int B, int32_t* err, const PeerWait* pw = nullptr) {
+                                               int B, int32_t* err, const PeerWait* pw = nullptr
+                                               BPRMF_DIAG_PREV) {
+#ifdef BPRMF_DIAG_WAIT
+  __shared__ int32_t s_hot[kMaxLongItems];
+  __shared__ int s_nhot;
+  if (WAIT && prev) {
+    if (threadIdx.x == 0) s_nhot = prev->meta[3];
+    if (threadIdx.x < kMaxLongItems) s_hot[threadIdx.x] = prev->lrec[(int64_t)threadIdx.x * kRec];
+    __syncthreads();
+  }
+  auto is_hot = [&](int32_t item) {
+    bool h = false;
+    if (prev)
+      for (int m = 0; m < s_nhot; ++m) h |= s_hot[m] == item;
+    return h;
+  };
+#endif
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = WAIT || !kFusedStampsOnly;
 #endif
@@ -260,6 +285,15 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       wi = mi == tp;
       wj = mj == tp;
       wu = mu == tp;
+#ifdef BPRMF_DIAG_WAIT
+      {
+        const bool hi = is_hot(i), hj = is_hot(j);
+        const bool skip_i = BPRMF_DIAG_WAIT == 1 ? !hi : BPRMF_DIAG_WAIT == 2 ? hi : false;
+        const bool skip_j = BPRMF_DIAG_WAIT == 1 ? !hj : BPRMF_DIAG_WAIT == 2 ? hj : false;
+        if (skip_i) wi = false;
+        if (skip_j) wj = false;
+      }
+#endif
       if (wi && si != tp) wait_stamp(Q.stamp + i, tp, err);
       if (wj && sj != tp) wait_stamp(Q.stamp + j, tp, err);
       if (wu && su0 != tp) wait_stamp(P.stamp + u, tp, err);
@@ -713,8 +747,16 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
     k2_body<G4, S, false, KB, true, true>(blockIdx.x, bv0.shifted(kb * bstride), P, Q, hp, ld, t, sb,
                                           long_blocks, item_blocks, nullptr, loss, B);
   else
+  {
+#ifdef BPRMF_DIAG_WAIT
+    const BatchView prev = bv0.shifted(kb * bstride);
+    k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
+                                      hp, ld, t + 1, sb, nullptr, B, err, nullptr, &prev);
+#else
     k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
                                       hp, ld, t + 1, sb, nullptr, B, err);
+#endif
+  }
 }
 
 // ---- the fused sharded step over the IPC transport (dist.cpp enqueue_steps, two launches/step) ----

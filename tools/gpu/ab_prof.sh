@@ -16,10 +16,10 @@ for r in $(seq 1 "$reps"); do
       case "${BPRMF_DIAG_LIB:-/}" in /*) ;; *) export BPRMF_DIAG_LIB="$R/$BPRMF_DIAG_LIB" ;; esac
       cd /tmp &&
       timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/prof_${name}_$r" -o run \
-        --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
+        --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-relaxed \
         > "$out/prof_${name}_$r.log" 2>&1 &&
       cd "$R" &&
-      timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+      timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-relaxed \
         > "$out/bench_${name}_$r.log" 2>&1 ) || { echo "variant $name rep $r failed"; tail -n 5 "$out/prof_${name}_$r.log" "$out/bench_${name}_$r.log"; exit 1; }
     st=$(find "$out/prof_${name}_$r" -name '*kernel_stats.csv' | head -n 1)
     echo "$name $r $(python3 tools/kstats.py --only k_fused_step,k_user_step,k_build_split "$st" | cut -d: -f2-) | bench $(grep '^{' "$out/bench_${name}_$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e8,4), "e8", d["ms_per_step"]*1e3, "us/step", d["roofline"]["avg_us_per_step"])')" | tee -a "$out/summary.txt"

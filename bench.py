@@ -178,7 +178,7 @@ def main():
     ap.add_argument("--python-orchestration", action="store_true",
                     help="sharded: per-step Python orchestration over torch.distributed instead of "
                          "the library's runner")
-    ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild", "local"],
+    ap.add_argument("--semantics", default="exact", choices=["exact", "hogwild", "local", "stale1"],
                     help="exact: the reference's batch-synchronous step (default, the headline); "
                          "hogwild: opt-in relaxed synchronisation (a separate, labelled line)")
     ap.add_argument("--local-steps", type=int, default=0,
@@ -210,14 +210,14 @@ def main():
     local = local % max(1, torch.cuda.device_count())  # ranks beyond the GPUs: rehearsal only
     torch.cuda.set_device(local)
     dist = None
-    sharded = world > 1 or a.sharded
+    sharded = world > 1 or a.sharded or a.semantics == "stale1"  # stale1: the sharded runner only
     hog = a.semantics in ("hogwild", "local")
     if a.semantics == "hogwild" and sharded:
         raise SystemExit("--semantics hogwild is single-GPU (run N independent replicas instead)")
     # users sharded, item table replicated and merged (§5d): only with peers to merge with (a
     # one-rank --sharded handle runs the single-GPU local path unless BPRMF_DP_ONE_RANK is set)
     dpi = a.semantics == "local" and sharded and (world > 1 or os.environ.get("BPRMF_DP_ONE_RANK") == "1")
-    if a.semantics == "local" and a.python_orchestration:
+    if a.semantics in ("local", "stale1") and a.python_orchestration:
         raise SystemExit("--semantics local runs through the library runner only (per-step Python "
                          "orchestration addresses items by owner)")
     if a.step == "atomic" and (sharded or hog):
@@ -322,7 +322,8 @@ def main():
         roof = None
         if kp and (kp["step_graph"]["count"] or kp["user_step"]["count"]):
             us = {k: v["ms"] / v["count"] * 1e3 for k, v in kp.items() if v["count"]}
-            if "step_graph" in us and sharded and world == 1 and not a.python_orchestration and not hog:
+            if ("step_graph" in us and sharded and world == 1 and not a.python_orchestration
+                    and a.semantics == "exact"):
                 # one rank: the runner dispatches to the single-GPU fused step (nothing to exchange)
                 step_us, what = us["step_graph"], ("world 1: the single-GPU fused step launches (the "
                                                    "runner has no peer to exchange with)")
@@ -335,6 +336,10 @@ def main():
                 step_us, what = us["step_graph"], ("k_hogwild<LOCAL> (in-kernel sampling + gather + dots "
                                                    "+ sigmoid + SGD scatter, hot items in per-XCD replicas) "
                                                    "+ k_local_merge every period")
+            elif "step_graph" in us and a.semantics == "stale1":  # two streams per rank
+                step_us, what = us["step_graph"], ("stale1 sharded step, per rank: K1 + K2 on the compute "
+                                                   "stream beside the owner stream's gradient exchange, "
+                                                   "apply, gather and row exchange of the step before")
             elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")
@@ -416,6 +421,9 @@ def main():
                                         "relaxed (local: hogwild for users and cold items, the hot items "
                                         "in one replica per XCD merged every local_steps steps; NOT the "
                                         "reference step)" if a.semantics == "local" else
+                                        "relaxed (stale1: the exact sharded step with the item rows one "
+                                        "step stale, the exchange of step k beside the compute of step "
+                                        "k+1; NOT the reference step)" if a.semantics == "stale1" else
                                         "exact batch-synchronous SGD (reference step), lazy weight decay, "
                                         "duplicate rows summed by f32 atomics (not bitwise reproducible)"
                                         if a.step == "atomic" else

@@ -187,6 +187,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
+  TRY(dalloc(&h->d_fold_cnt, 1));
   if (dpi) {
     TRY(dalloc(&h->d_qbase, h->I * ld));
     // the delta table padded to world slices of ceil(I / world) rows (the IPC all-reduce pushes
@@ -218,6 +219,7 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
   if (h->d_qdelta) TRY(memz(h->d_qdelta, sizeof(float) * (size_t)(W * ((h->I + W - 1) / W) * ld)));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
+  TRY(memz(h->d_fold_cnt, sizeof(int32_t)));
   TRY(memz(h->d_status, status_bytes));
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size
   const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
@@ -240,7 +242,10 @@ int bprmf_destroy(bprmf_handle* h) {
   if (!h) return 0;
   hipSetDevice(h->cfg.device);
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
-  void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
+  // a call returns once its status is out, possibly before its last launch has drained (the
+  // status folded into the last K2): a caller's stream is drained too before anything is freed
+  if (h->stream && h->stream != h->own_stream) hipStreamSynchronize(h->stream);
+  void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_fold_cnt, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
                   h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
@@ -509,7 +514,12 @@ int bprmf::wait_mapped_seq(bprmf_handle* h, size_t off, uint64_t seq) {
 int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   const bool ran = !h->loss_pending;
   h->loss_pending = false;
-  if (h->call_slots) {
+  h->fold_req = false;
+  if (h->fold_seq) {  // the call's last K2 wrote the status block and this sequence number
+    const uint64_t seq = h->fold_seq;
+    h->fold_seq = 0;
+    if (int r = wait_mapped_seq(h, kSeqEndOff, seq)) return r;
+  } else if (h->call_slots) {
     HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * kLossSlots,
                           hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -757,6 +767,16 @@ static int run_units(bprmf_handle* h, int64_t n, int64_t* base) {
   return 0;
 }
 
+// Opt-in (BPRMF_STATUS_FOLD=1; read per call): measured slower at the driver's settings (20-step
+// calls 13.3-13.9 against 12.9-13.0 us/step, profiles/r05_ab_status_fold.txt): the call then
+// returns while its last K2 still runs, and the caller's device synchronisation that follows
+// (torch.cuda.synchronize in bench.py) waits longer for it than the host's spin on the status
+// word of a k_status_out launch does.
+static bool fold_enabled() {
+  const char* e = getenv("BPRMF_STATUS_FOLD");
+  return e && e[0] == '1';
+}
+
 // the chunk's nb steps (cursor {h->t, 0}, batches built)
 static int launch_steps(bprmf_handle* h, int64_t nb) {
   int64_t base = 0;
@@ -768,8 +788,23 @@ static int launch_steps(bprmf_handle* h, int64_t nb) {
   HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, 0, nullptr, nullptr, nullptr,
                    nullptr, h->stream, PeerWait{}, stride, &sb));
   if (int r = run_units(h, nb - 1, &base)) return r;
+  // BPRMF_STATUS_FOLD=1: the call's last K2 publishes the call's status itself (no k_status_out
+  // launch and boundary; measured slower, see fold_enabled)
+  StatusFold sf;
+  const StatusFold* sfp = nullptr;
+  if (h->fold_req && h->d_fold_cnt && !h->call_slots && fold_enabled()) {
+    sf.cnt = h->d_fold_cnt;
+    sf.host = reinterpret_cast<uint64_t*>(h->h_status_dev);
+    sf.dstatus = reinterpret_cast<const uint64_t*>(h->d_status);
+    sf.seq_dst = reinterpret_cast<uint64_t*>(h->h_status_dev + kSeqEndOff);
+    sf.seq = ++h->status_seq;
+    sf.nslots = kSegLossSlots;
+    sfp = &sf;
+    h->fold_seq = sf.seq;
+  }
+  h->fold_req = false;
   HIPCHK(item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)(nb - 1 - base), nullptr,
-                   nullptr, nullptr, h->stream, nullptr, h->d_loss, stride, &sb));
+                   nullptr, nullptr, h->stream, nullptr, h->d_loss, stride, &sb, sfp));
   return 0;
 }
 
@@ -969,9 +1004,15 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   trace_mark();
   if (int r = begin_call(h)) return r;
   int64_t steps = 0;
-  for (int64_t off = beg; off < end; off += chunk)
-    if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps))
+  for (int64_t off = beg; off < end; off += chunk) {
+    h->fold_req = off + chunk >= end;  // the call's last chunk: its last K2 carries the status
+    if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps)) {
+      h->fold_req = false;
+      h->fold_seq = 0;
       return r;
+    }
+  }
+  h->fold_req = false;
   trace_mark();
   const int rc_end = end_call(h, st, end - beg, steps);
   trace_mark();

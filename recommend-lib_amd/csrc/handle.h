@@ -110,6 +110,11 @@ struct bprmf_handle {
   unsigned char* h_status = nullptr;      // pinned, mapped host mirror
   unsigned char* h_status_dev = nullptr;  // its device address (k_status_out writes there)
   uint64_t status_seq = 0;                // sequence number of the last call's status block
+  // the call's status folded into its last K2 (StatusFold): fold_req set by the entry point for
+  // its last chunk, fold_seq != 0 once that launch carries the status (end_call then only waits)
+  int32_t* d_fold_cnt = nullptr;
+  bool fold_req = false;
+  uint64_t fold_seq = 0;
   double* d_loss = nullptr;               // = d_status + 16
   int32_t* d_err = nullptr;               // = d_status
   bool loss_pending = false;    // a call began: the loss slots are zeroed before the first step

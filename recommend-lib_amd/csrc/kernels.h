@@ -235,10 +235,23 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 // loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
 // x K1 left in xloss, to loss[0 .. ceil(B / 256)) (one slot per loss workgroup, fixed order;
 // at most kSegLossSlots slots)
+// The call's status folded into its last K2: each loss workgroup stores its
+// final slot into the mapped host block and arrives on `cnt`; the last of the lb arrivals copies
+// the error words and the unused slots, resets `cnt` and stores `seq` (what k_status_out does in
+// a launch of its own).  host / seq_dst: mapped host memory (device addresses).
+struct StatusFold {
+  int32_t* cnt = nullptr;            // arrivals, 0 between calls
+  uint64_t* host = nullptr;          // {err word, dist word, loss slots...} as k_status_out writes
+  const uint64_t* dstatus = nullptr; // the device status block it mirrors
+  uint64_t* seq_dst = nullptr;
+  uint64_t seq = 0;
+  int nslots = 0;                    // loss slots mirrored (kSegLossSlots)
+};
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss = nullptr,
-                     double* loss = nullptr, int64_t bstride = 0, const StepBufs* sb = nullptr);
+                     double* loss = nullptr, int64_t bstride = 0, const StepBufs* sb = nullptr,
+                     const StatusFold* sf = nullptr);
 // (sb != null: its buffers replace contrib / ugrad / xloss)
 // K2 of step t = tbase[0] + step + 1 on batch tbase[1] + step, and K1 of step t + 1 on the next
 // batch, in one launch (bv0: batch 0's view; single GPU, sb with both halves and pend arrays)

@@ -716,11 +716,32 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   const int32_t* __restrict__ tbase, int step,
                                                   StepBufs sb, int long_blocks, int item_blocks,
                                                   float* __restrict__ grads, double* __restrict__ loss,
-                                                  int64_t bstride, int B) {
+                                                  int64_t bstride, int B, StatusFold sf) {
   CsScope cs_(62);
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   k2_body<G4, S, SH, KB, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, long_blocks,
                                     item_blocks, grads, loss, B);
+  // the call's status (StatusFold): the loss workgroups come first in the grid, and only their
+  // slots and the error words (set by earlier launches) make the status, so the last loss
+  // workgroup to finish publishes it while item workgroups may still run (later calls, and any
+  // read of the tables, are ordered after this launch on the stream)
+  const int lb = loss && sb.xloss ? (B + KB - 1) / KB : 0;
+  if (sf.cnt && (int)blockIdx.x < lb && threadIdx.x == 0) {
+    const double v = loss[blockIdx.x];  // written by this thread in k2_body (or untouched: dead)
+    __hip_atomic_store(sf.host + 2 + blockIdx.x, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the host slot written before arriving
+    if (__hip_atomic_fetch_add(sf.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lb - 1) {
+      for (int k = lb; k < sf.nslots; ++k)  // slots no loss workgroup owns (zeroed at call start)
+        __hip_atomic_store(sf.host + 2 + k, sf.dstatus[2 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sf.host, __hip_atomic_load(sf.dstatus, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // the error word
+      __hip_atomic_store(sf.host + 1, sf.dstatus[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sf.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(sf.seq_dst, sf.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // The fused step: K2 of step t (batch c[1] + step) and K1 of step t + 1 (the next batch) in one
@@ -896,7 +917,7 @@ template <int G4, int S, int KB>
 static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, Table Q,
                                    const Hyper& hp, const int32_t* tbase, int step,
                                    const StepBufs& sb, float* grads, hipStream_t s, double* loss,
-                                   int64_t bstride, bool wt) {
+                                   int64_t bstride, bool wt, const StatusFold& sf) {
   // single GPU: capped, when the items are many against the batch's 2B references (few items, as
   // at the ml-1m shape, send most of their segments to K2, which the capped grid serialises)
   const K2Grid k = k2_grid<G4, S, KB>(B, loss != nullptr, grads == nullptr && Q.rows >= 2LL * B);
@@ -904,7 +925,7 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
 #define BPRMF_K2(SH_, WT_)                                                                        \
   k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,       \
                                                         k.long_blocks, k.item_blocks, grads, loss, \
-                                                        bstride, B)
+                                                        bstride, B, sf)
   if (grads && wt) BPRMF_K2(true, true);
   else if (grads) BPRMF_K2(true, false);
   else if (wt) BPRMF_K2(false, true);
@@ -920,19 +941,20 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss, double* loss,
-                     int64_t bstride, const StepBufs* sbp) {
+                     int64_t bstride, const StepBufs* sbp, const StatusFold* sfp) {
   const StepBufs sb = plain_bufs(const_cast<float*>(contrib), const_cast<float*>(ugrad),
                                  const_cast<float*>(xloss), sbp);
   if (!sb.xloss) loss = nullptr;
+  const StatusFold sf = sfp && loss ? *sfp : StatusFold{};
   const bool wt = use_wt();
   const char* kb = getenv("BPRMF_K2_BLOCK");
   const bool big = kb && atoi(kb) == 1024;
   BPRMF_DISPATCH4(g, ({
     if (big)
       return launch_item_step<G4_, S_, (S_ == 1 ? 1024 : 512)>(g, bv, B, P, Q, hp, tbase, step, sb,
-                                                               grads, s, loss, bstride, wt);
+                                                               grads, s, loss, bstride, wt, sf);
     return launch_item_step<G4_, S_, 256>(g, bv, B, P, Q, hp, tbase, step, sb, grads, s, loss,
-                                          bstride, wt);
+                                          bstride, wt, sf);
   }));
   return hipGetLastError();
 }

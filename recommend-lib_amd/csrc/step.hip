@@ -496,12 +496,21 @@ constexpr int item_rounds() { return S == 1 ? 6 : 1; }
 // one K2 item segment (record r0/r1): the sum of -/+ c P_u over its references in order, then the
 // update (single GPU) or the per-slot gradient (sharded)
 template <int G4, int S, bool SH, bool WT, bool PUB>
+// Diagnostic build only (-DBPRMF_DIAG_SLOTS, WRONG results, timing only): what K2's cold item
+// segments would gain if their first 4 contribution rows sat at positions known without the
+// record (a slot-major contribution layout): 4 rows per lane group are requested in the same
+// round as the record, and used in place of the segment's first 4 references.
+#ifdef BPRMF_DIAG_SLOTS
+#define BPRMF_DIAG_PRE(S) , const float4 (*pre)[S] = nullptr
+#else
+#define BPRMF_DIAG_PRE(S)
+#endif
 static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const BatchView& bv,
                                                        const Table& Q, const Hyper& hp, int ld,
                                                        int32_t t, int sub,
                                                        const float* __restrict__ contrib,
                                                        float* __restrict__ grads, const GradRoute* gr,
-                                                       int blk) {
+                                                       int blk BPRMF_DIAG_PRE(S)) {
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = PUB || !kFusedStampsOnly;
 #endif
@@ -525,6 +534,13 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 #pragma unroll
     for (int m = 0; m < kInlineRefs; ++m) {
       rf[m] = (pk[m >> 1] >> (16 * (m & 1))) & 0xFFFF;
+#ifdef BPRMF_DIAG_SLOTS
+      if (pre && m < 4) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) rows[m][k] = pre[m][k];
+        continue;
+      }
+#endif
       if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
     }
 #pragma unroll
@@ -693,6 +709,17 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const int s0 = (bid - long_blocks) * NG + grp;
   const int stride = item_blocks * NG;
   const int sc = min(s0, 2 * B - 1);
+#ifdef BPRMF_DIAG_SLOTS
+  float4 pre[4][S];
+  if (!SH) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float* cb = contrib + (int64_t)((sc * 4 + m) % B) * ld + 4 * sub;
+#pragma unroll
+      for (int k = 0; k < S; ++k) pre[m][k] = *reinterpret_cast<const float4*>(cb + 4 * G4 * k);
+    }
+  }
+#endif
   int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
   int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
   const int n_iseg = bv.meta[2];
@@ -707,7 +734,12 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
       r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
       r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
     }
+#ifdef BPRMF_DIAG_SLOTS
+    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk,
+                                        (!SH && round == 0) ? pre : nullptr);
+#else
     k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
+#endif
   }
 }
 

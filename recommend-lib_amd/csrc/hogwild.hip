@@ -60,6 +60,13 @@ static __device__ __forceinline__ void hw_st4(float* p, float4 v) {
   const v4f x = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
 }
+// p += s * g, four no-return f32 atomic adds (executed at the memory side)
+static __device__ __forceinline__ void hw_add4(float* p, float4 g, float s) {
+  atomicAdd(p, s * g.x);
+  atomicAdd(p + 1, s * g.y);
+  atomicAdd(p + 2, s * g.z);
+  atomicAdd(p + 3, s * g.w);
+}
 static __device__ __forceinline__ void hw_st_word(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -164,6 +171,10 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
   const bool nostore = fl & 4;
   const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
   const bool user_wb = fl & 64;  // A/B: user rows stored write-back (plain), item rows sc1
+  // LOCAL, BPRMF_LOCAL_HOT_ATOMIC=1 (A/B): a hot replica row takes its change -lr g by f32
+  // atomic adds instead of a store of the read value minus lr g, so concurrent updates of one
+  // hot row in this XCD are all kept (a store overwrites the others' changes in flight)
+  const bool hot_atomic = LOCAL && (fl & 128);
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
@@ -222,10 +233,12 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
         // replica rows: written back into this XCD's L2 (plain stores), no weight-decay term
         // (their stamps read INT32_MAX: fi1 / fj1 false); shared rows: write-through, as hogwild
         const float4 ni = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f), nj = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
-        if (hoti) *reinterpret_cast<float4*>(qi + 4 * G4 * k) = ni;
+        if (hoti && hot_atomic) hw_add4(qi + 4 * G4 * k, gi, -lr);
+        else if (hoti) *reinterpret_cast<float4*>(qi + 4 * G4 * k) = ni;
         else hw_st4(qi + 4 * G4 * k, ni);
         if (!same) {
-          if (hotj) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = nj;
+          if (hotj && hot_atomic) hw_add4(qj + 4 * G4 * k, gj, -lr);
+          else if (hotj) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = nj;
           else hw_st4(qj + 4 * G4 * k, nj);
         }
       }
@@ -607,6 +620,8 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
   // diagnostic timing only (wrong results): bit 1 = no row loads, bit 2 = no row stores, bit 3 =
   // plain (write-back) row stores, bit 4 = no item row stores, bit 5 = no user row stores
   if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 126);
+  if (const char* e = getenv("BPRMF_LOCAL_HOT_ATOMIC"))
+    if (e[0] == '1') fl |= 128;
   SamplerArgs a{};
   if (sa) a = *sa;
   if (lap) {  // semantics "local": the hot items in per-XCD replicas

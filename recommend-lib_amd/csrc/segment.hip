@@ -585,11 +585,17 @@ constexpr int kPartE2 = kItemParts >= 8 ? 2 : kItemParts == 4 ? 4 : 8;
 // elements take no part (no count, no rank), and the sorted elements come out in a blocked
 // E2-per-thread arrangement (positions past the count: kNone).  The caller guarantees
 // count <= T * E2.  Returns the count.
+// tie != nullptr: element k of this thread sorts by (key[k], tie[k]) (ties unique) instead of
+// (key, input position), and key_of / val_of receive the tie as the element's identity.  The split
+// builder's item parts sort their references in slot order this way with tie = (side, user, slot):
+// the order of k_build_batches's references (i before j, then user order, stable by slot) without
+// sorting the batch by user first.
 template <int T, int E, int E2, class KeyOf, class ValOf>
 static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E], uint32_t lo,
                                                          int bits, const BucketScratch<T>& sc,
                                                          KeyOf key_of, ValOf val_of,
-                                                         uint32_t (&okey)[E2], uint32_t (&oval)[E2]) {
+                                                         uint32_t (&okey)[E2], uint32_t (&oval)[E2],
+                                                         const uint32_t* tie = nullptr) {
   using Scan = rocprim::block_scan<int, T>;
   constexpr int PB = kBuckets / T;
   const int tid = threadIdx.x;
@@ -619,7 +625,8 @@ static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E
 #pragma unroll
   for (int k = 0; k < E; ++k)
     if (li[k] >= 0)
-      sc.bk[sc.start[(key[k] - lo) >> shift] + li[k]] = ((uint64_t)key[k] << 32) | (uint32_t)(tid * E + k);
+      sc.bk[sc.start[(key[k] - lo) >> shift] + li[k]] =
+          ((uint64_t)key[k] << 32) | (tie ? tie[k] : (uint32_t)(tid * E + k));
   __syncthreads();
   // rank inside the bucket (bucket_sort's phase 4), over the count's elements only
   constexpr int R = (E2 * T + T - 1) / T;  // elements per thread in the strided rank pass
@@ -682,6 +689,11 @@ static __device__ __forceinline__ int bucket_sort_sparse(const uint32_t (&key)[E
 constexpr int kXchWords = 2 + kMaxWorld / 2;
 constexpr uint32_t kTagMark = 0x80000000u;
 constexpr uint32_t kBoardMagic = 0x534D504Bu;  // "SMPK": high half of a sampling-board mark
+// the user-order flag: {nvalid << 48 | kUposMagic16 << 32 | tag} (the valid count rides along)
+constexpr uint32_t kUposMagic = 0x5550u;   // "UP": bits 32..47 of the user-order flag
+// fast item parts' tie words: side (1 bit) | local user row | slot (kTieSlotBits): the user rows
+// must fit the remaining bits (the host falls back to every part sorting by user otherwise)
+constexpr int kTieSlotBits = 13;  // slots < kBuildThreads * 4 = 4096 (bucket builds)
 static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
   return reinterpret_cast<uint64_t*>(v.ioff + 1);
 }
@@ -733,7 +745,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     const int32_t* __restrict__ rj, int64_t u_rows, int64_t i_rows, int world_in, int64_t iloc,
     int slot_stride, int user_bits, int item_bits, int tpb, int k1_items, BatchBuf bb,
     int32_t* __restrict__ err, CursorInit ci, uint32_t tag, SamplerArgs sa, uint32_t epoch,
-    int64_t first_slot, FastDiv wdiv, FastDiv ldiv) {
+    int64_t first_slot, FastDiv wdiv, FastDiv ldiv, int fast_parts) {
   constexpr int T = kBuildThreads;
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
@@ -822,6 +834,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     key[k] = kNone;
     val[k] = (uint32_t)p;
     const int32_t ug = p < nb ? staged(ru + b0 + p) : -1;
+    if (p < nb) s_u[p] = kNone;  // (fast item parts: an invalid or empty slot has no references)
     if (ug >= 0) {  // u < 0: an empty slot
       const int32_t u = SL ? (int32_t)wdiv.div((uint32_t)ug) : ug, i = staged(ri + b0 + p),
                     j = staged(rj + b0 + p);
@@ -837,9 +850,33 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     }
   }
   SPSTAMP(1);
-  const int nvalid = bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
-                                         [](int q) { return (uint32_t)q; });
+  // fast_parts: only the user workgroup sorts the batch by user; it publishes every slot's
+  // position in user order (upos, in the batch's useg area, which bucket builds leave unused) for
+  // the item parts, which sort their references in slot order by (item, side, user, slot) -- the
+  // same order -- and read upos only to write the references' values (kernel-launch A/B:
+  // BPRMF_SPLIT_UPOS=0 has every workgroup sort by user, as before)
+  uint64_t* upos_flag = xch_of(v) + (int64_t)kItemParts * kXchWords + kItemParts + 1;
+  const uint64_t upos_mark = (uint64_t)kUposMagic << 32 | tag;
+  int nvalid = 0;
+  if (role == 0 || !fast_parts) {
+  nvalid = bucket_sort<T, IPT>(key, val, user_bits, bs, [&](int q) { return s_u[q]; },
+                               [](int q) { return (uint32_t)q; });
   SPSTAMP(2);
+  if (role == 0 && fast_parts) {
+    // the permutation in sorted order (useg[p] = the slot at sorted position p, p < B): one
+    // 16-byte write-through store per thread, 1 KB contiguous per wave (scattered 4-byte stores
+    // of upos[slot] took ~5.7 us), then the flag with the valid count.  (fast_parts needs B % 4
+    // == 0: useg is then 16-byte aligned.)
+    if (tid * IPT < B) {
+      uint64_t* pw = reinterpret_cast<uint64_t*>(v.useg + tid * IPT);
+      __hip_atomic_store(pw, (uint64_t)val[0] | (uint64_t)val[1] << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pw + 1, (uint64_t)val[2] | (uint64_t)val[3] << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(upos_flag, upos_mark | (uint64_t)nvalid << 48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // blocked arrangement: sorted position p = tid*IPT + k holds key[k] (user) and val[k] (slot)
   int32_t my_i[IPT], my_j[IPT];
 #pragma unroll
@@ -855,6 +892,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
     s_i[tid * IPT + k] = my_i[k];  // sorted order from here on
     s_j[tid * IPT + k] = my_j[k];
   }
+  }  // role == 0 || !fast_parts
 
   if (role == 0) {
     // ---- user side: segments, w, trec {u, w}, mrec, meta (k_build_batches lines for these) ----
@@ -933,18 +971,38 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
       return item;
     }
   };
-  __syncthreads();  // s_i/s_j in sorted order; s_key free
-  uint32_t ik[IPT2];
+  __syncthreads();  // s_i/s_j in sorted order (fast_parts: slot order, s_u valid); s_key free
+  uint32_t ik[IPT2], tie[IPT2];
   int below = 0, mine = 0;  // references of this thread in the parts before / in this part
+  if (fast_parts) {  // references in slot order: r < nb the i side of slot r, else the j side
 #pragma unroll
-  for (int k = 0; k < IPT2; ++k) {
-    const int r = tid * IPT2 + k;
-    ik[k] = kNone;
-    if (r < 2 * nvalid) {
-      const uint32_t kk = key_of_item((uint32_t)(r < nvalid ? s_i[r] : s_j[r - nvalid]));
-      if (kk >= lo && ((kk - lo) >> rb) == 0) ik[k] = kk;
-      below += kk < lo;
-      mine += ik[k] != kNone;
+    for (int k = 0; k < IPT2; ++k) {
+      const int r = tid * IPT2 + k;
+      ik[k] = kNone;
+      tie[k] = 0;
+      if (r < 2 * nb) {
+        const int side = r >= nb, slot = side ? r - nb : r;
+        const uint32_t u = s_u[slot];
+        if (u == kNone) continue;
+        const uint32_t kk = key_of_item((uint32_t)(side ? s_j[slot] : s_i[slot]));
+        if (kk >= lo && ((kk - lo) >> rb) == 0) ik[k] = kk;
+        tie[k] = (uint32_t)side << 31 | u << kTieSlotBits | (uint32_t)slot;
+        below += kk < lo;
+        mine += ik[k] != kNone;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT2; ++k) {
+      const int r = tid * IPT2 + k;
+      ik[k] = kNone;
+      tie[k] = 0;
+      if (r < 2 * nvalid) {
+        const uint32_t kk = key_of_item((uint32_t)(r < nvalid ? s_i[r] : s_j[r - nvalid]));
+        if (kk >= lo && ((kk - lo) >> rb) == 0) ik[k] = kk;
+        below += kk < lo;
+        mine += ik[k] != kNone;
+      }
     }
   }
   int cpre0 = 0, ctot0 = 0;  // (refs before << 16 | refs here), each <= 2B <= 8192
@@ -957,10 +1015,64 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   constexpr int E2 = decltype(e2)::value;
   uint32_t ok_[E2], ov[E2];
   const int nv = nvalid;
-  const int total = bucket_sort_sparse<T, IPT2, E2>(
-      ik, lo, rb, bs,
-      [&](int r) { return key_of_item((uint32_t)(r < nv ? s_i[r] : s_j[r - nv])); },
-      [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, ok_, ov);
+  int total;
+  if (fast_parts) {
+    constexpr uint32_t smask = (1u << kTieSlotBits) - 1;
+    total = bucket_sort_sparse<T, IPT2, E2>(
+        ik, lo, rb, bs,
+        [&](int id) {
+          const uint32_t t = (uint32_t)id, slot = t & smask;
+          return key_of_item((uint32_t)((t >> 31) ? s_j[slot] : s_i[slot]));
+        },
+        [](int id) { return (uint32_t)id; }, ok_, ov, tie);
+    // the user workgroup's permutation (one sc1 poll by thread 0, bounded; sc1 loads), inverted
+    // in LDS (the sort's bucket starts, free now): s_upos[slot] = the slot's position in user order
+    int32_t* s_upos = bs.start;
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t w = 0;
+      for (uint32_t polls = 0;; ++polls) {
+        w = __hip_atomic_load(upos_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w & 0x0000FFFFFFFFFFFFull) == upos_mark) break;
+        __builtin_amdgcn_s_sleep(1);
+        if ((polls & 255) == 255 && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 10 s
+          atomicOr(err, 16);
+          __hip_atomic_store(v.meta + kMetaDead, kDeadMark, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          w = 0;
+          break;
+        }
+      }
+      s_ninv = (int)(w >> 48);  // the batch's valid triplet count
+    }
+    __syncthreads();
+    {
+      const int nval = s_ninv;
+      if (tid * IPT < nval) {
+        const uint64_t* pw = reinterpret_cast<const uint64_t*>(v.useg + tid * IPT);
+        const uint64_t a = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t b = __hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t sl[IPT] = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+          const int p = tid * IPT + k;
+          if (p < nval && sl[k] < (uint32_t)nb) s_upos[sl[k]] = p;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E2; ++k) {  // (side, user, slot) -> the reference's value (pos << 1 | side)
+      if (ok_[k] == kNone) continue;
+      const uint32_t t = ov[k];
+      ov[k] = (uint32_t)s_upos[t & smask] << 1 | (t >> 31);
+    }
+    __syncthreads();  // s_upos (bucket starts) free again
+  } else {
+    total = bucket_sort_sparse<T, IPT2, E2>(
+        ik, lo, rb, bs,
+        [&](int r) { return key_of_item((uint32_t)(r < nv ? s_i[r] : s_j[r - nv])); },
+        [&](int r) { return r < nv ? ((uint32_t)r << 1) : (((uint32_t)(r - nv) << 1) | 1u); }, ok_, ov);
+  }
   SPSTAMP(4);
 #pragma unroll
   for (int k = 0; k < E2; ++k) s_key[tid * E2 + k] = ok_[k];
@@ -1202,8 +1314,11 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // triplets already in memory: the split builder (1 + kItemParts workgroups per batch; one rank,
   // or the sharded runner's slots; BPRMF_SPLIT_ITEMS=0 keeps the one-workgroup build, A/B)
   const char* spe = getenv("BPRMF_SPLIT_ITEMS");
-  const bool split = (w1 || slots) && ru && B >= kItemParts * kXchWords + kItemParts + 1 &&
+  const bool split = (w1 || slots) && ru && B >= kItemParts * kXchWords + kItemParts + 2 &&
                      B <= kBuildThreads * 4 && !radix && !(spe && spe[0] == '0');
+  // the item parts skip the user sort when a (side, user, slot) tie word holds the user rows
+  const char* upe = getenv("BPRMF_SPLIT_UPOS");
+  const int fast_parts = (1 + ub + kTieSlotBits <= 32 && B % 4 == 0 && !(upe && upe[0] == '0')) ? 1 : 0;
   // sample_first: ru/ri/rj are staging arrays for slots first_slot .. first_slot + n_slots; the
   // split builder samples them itself (BPRMF_SPLIT_SAMPLE=0: k_sample first, A/B), any other
   // build after a k_sample launch
@@ -1220,7 +1335,7 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
 #define BPRMF_SPLIT(SL_, SMP_, W_, STRIDE_, K1_)                                                 \
   k_build_split<SL_, SMP_><<<grid, kBuildThreads, 0, s>>>(                                       \
       n_slots, B, ru, ri, rj, u_rows, i_rows, W_, iloc, STRIDE_, ub, ib, tpb, K1_, bb, err, ci, tag, \
-      a, epoch, first_slot, FastDiv((uint32_t)W_), FastDiv((uint32_t)iloc))
+      a, epoch, first_slot, FastDiv((uint32_t)W_), FastDiv((uint32_t)iloc), fast_parts)
     if (w1 && smp) BPRMF_SPLIT(false, true, 1, 0, k1_items);
     else if (w1) BPRMF_SPLIT(false, false, 1, 0, k1_items);
     else if (smp) BPRMF_SPLIT(true, true, world, slot_stride, 0);

@@ -1332,6 +1332,9 @@ static int dist_per_step_ok(bprmf_handle* h) {
     return fail(BPRMF_E_UNSUPPORTED,
                 "the per-step sharded calls address items by owner; semantics local at world > 1 "
                 "replicates the item table: use bprmf_dist_train_steps / bprmf_dist_train_replay");
+  if (h && h->semantics == BPRMF_SEM_STALE1)  // its staleness is the runner's two-stream schedule
+    return fail(BPRMF_E_UNSUPPORTED,
+                "semantics stale1 runs through the runner: use bprmf_dist_train_steps / _replay");
   return 0;
 }
 

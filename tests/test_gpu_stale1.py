@@ -93,6 +93,8 @@ def test_stale1_refuses_per_step_calls_and_single_gpu_path(rl):
         m.set_train(pos)
         with pytest.raises(ValueError, match="runner"):
             m.step(0, 0)
+        with pytest.raises(Exception, match="runner"):  # the C ABI itself refuses too
+            m.b.plan(0, 0, 1)
         return True
 
     assert all(_threads(rl, 2, fn))

@@ -76,6 +76,7 @@ int bprmf::check_err_flag(bprmf_handle* h) {
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 16) HIPCHK(clear_batches(h));
+    h->persist_t = -1;
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
@@ -248,7 +249,7 @@ int bprmf_destroy(bprmf_handle* h) {
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_fold_cnt, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
+                  h->d_pend_q, h->d_pend_p, h->d_pflags, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
                   h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -534,6 +535,7 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 16) HIPCHK(clear_batches(h));
+    h->persist_t = -1;  // a persistent launch may have given up part-way: its flags are reset
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 8) return fail(BPRMF_E_HIP, "fused step: a row's owner never published it (wait timed out)");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
@@ -606,6 +608,12 @@ extern "C" int bprmf_debug_fail_build(bprmf_handle* h) {
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(bb.view(k).meta + kMetaDead), kDeadMark, 1, h->stream));
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_err, kErrBuild, 1, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int bprmf_debug_persist_grid(bprmf_handle* h, int32_t* workgroups) {
+  if (!h || !workgroups) return fail(BPRMF_E_INVALID, "null argument");
+  *workgroups = h->persist_total;
   return 0;
 }
 
@@ -777,6 +785,33 @@ static bool fold_enabled() {
   return e && e[0] == '1';
 }
 
+// BPRMF_PERSIST=1 runs each chunk as ONE persistent launch (step.hip k_persist_steps; read per
+// call).  Opt-in: bitwise equal to the fused launches but measured 1.4-2.2x slower per step
+// (profiles/r05_persist_*: 13.6-20.7 against 9.4-9.5 us), see DESIGN.md §5 "Round 5".
+static bool persist_enabled() {
+  const char* e = getenv("BPRMF_PERSIST");
+  return e && e[0] == '1';
+}
+
+// the persistent step's flags and grid, probed once per handle: 0 when its workgroups would not
+// all be resident at once (or the item table is too small for the capped K2 grid it assumes)
+static int persist_ready(bprmf_handle* h) {
+  if (h->persist_total < 0) {
+    const int B = h->cfg.batch_size;
+    h->persist_total = 0;
+    if (h->Q.rows >= 2LL * B) {
+      const int total = persist_grid(h->geom, B, true, &h->persist_k2, &h->persist_k1);
+      if (total > 0) {
+        // two int32 arrays, each padded to whole 16-byte groups (the pollers read 4 flags per lane)
+        const int64_t words = 4 * ((h->persist_k1 + 3) / 4 + (h->persist_k2 + 3) / 4);
+        if (int r = dalloc(&h->d_pflags, words)) return r;
+        h->persist_total = total;
+      }
+    }
+  }
+  return 0;
+}
+
 // the chunk's nb steps (cursor {h->t, 0}, batches built)
 static int launch_steps(bprmf_handle* h, int64_t nb) {
   int64_t base = 0;
@@ -785,6 +820,21 @@ static int launch_steps(bprmf_handle* h, int64_t nb) {
   const BatchView v0 = BatchBuf{h->d_batch, B}.view(0);
   const int64_t stride = BatchBuf::stride_for(B);
   const StepBufs sb = step_bufs(h);
+  if (persist_enabled() && nb >= 2) {
+    if (int r = persist_ready(h)) return r;
+    if (h->persist_total > 0 && nb < INT32_MAX) {
+      // the flags must all read h->t now (they do after an uninterrupted persistent chunk ending
+      // there; otherwise they are set: steps run another way, or a failed launch left them)
+      const int64_t words = 4 * ((h->persist_k1 + 3) / 4 + (h->persist_k2 + 3) / 4);
+      if (h->persist_t != h->t)
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_pflags, h->t, words, h->stream));
+      h->persist_t = h->t + nb;
+      HIPCHK(persist_step(h->geom, v0, stride, B, h->P, h->Q, h->hp, h->d_tbase, (int)nb, sb, h->d_loss,
+                          h->d_err, h->d_pflags, h->d_pflags + 4 * ((h->persist_k1 + 3) / 4), h->stream));
+      h->fold_req = false;
+      return 0;
+    }
+  }
   HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, 0, nullptr, nullptr, nullptr,
                    nullptr, h->stream, PeerWait{}, stride, &sb));
   if (int r = run_units(h, nb - 1, &base)) return r;

@@ -102,6 +102,11 @@ struct bprmf_handle {
   float* d_qsum = nullptr;      // [I][ld] the overlapped all-reduce's result (RCCL, out of place)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
+  // the persistent step (step.hip k_persist_steps, BPRMF_PERSIST): per-workgroup progress flags
+  // [K1 workgroups][K2 workgroups] and the launch's workgroup count (0: not resident, fused)
+  int32_t* d_pflags = nullptr;
+  int persist_k1 = 0, persist_k2 = 0, persist_total = -1;  // -1: not probed yet
+  int64_t persist_t = -1;  // every flag holds this step (mod 256); -1: unknown, reset before use
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;
   // misc device scalars

@@ -258,6 +258,15 @@ hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
                       const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
                       double* loss, int32_t* err, hipStream_t s);
+// the chunk's n steps (steps tbase[0] + 1 .. + n on batches tbase[1] ..) in ONE launch of resident
+// workgroups (step.hip k_persist_steps); f1 / f2: progress flags of K1 / K2 workgroups (k1_blocks
+// and k2_blocks int32, each array 16-byte aligned and padded to 4; they hold step numbers and
+// must all read the chunk's first step - 1 when it starts).  persist_grid: the
+// launch's workgroup count, 0 when they would not all be resident at once.
+int persist_grid(const Geom& g, int B, bool loss, int* k2_blocks, int* k1_blocks);
+hipError_t persist_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
+                        const Hyper& hp, const int32_t* tbase, int n, const StepBufs& sb, double* loss,
+                        int32_t* err, int32_t* f1, int32_t* f2, hipStream_t s);
 int item_long_blocks(int B);
 // relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
 // sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s

@@ -125,6 +125,41 @@ static __device__ __forceinline__ float4 ld4_sc1(const float* p) {
                      __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
 }
 
+// PS (the persistent step, k_persist_steps): every row, contribution and stamp another workgroup
+// may have written earlier in the same launch is read with sc1 loads (no kernel boundary has
+// invalidated this CU's L1 since); otherwise plain loads
+// (diagnostic build -DBPRMF_PERSIST_PLAIN: plain loads there too -- WRONG results, timing only)
+#ifdef BPRMF_PERSIST_PLAIN
+constexpr bool kPsLoads = false;
+#else
+constexpr bool kPsLoads = true;
+#endif
+template <bool PS>
+static __device__ __forceinline__ float4 ld4p(const float* p) {
+  if constexpr (PS && kPsLoads) return ld4_sc1(p);
+  else return ld4(p);
+}
+template <bool PS>
+static __device__ __forceinline__ int32_t ldw(const int32_t* p) {
+  if constexpr (PS && kPsLoads) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+#ifdef BPRMF_PERSIST_STAMPS  // diagnostic knobs: {stamp-poll sleeps, K2 priority, gate-poll sleeps}
+__device__ int g_pknob[4];
+extern "C" int bprmf_debug_persist_knobs(const int* k) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pknob), k, sizeof(g_pknob)) == hipSuccess ? 0 : -3;
+}
+#define PKNOB_SLEEP(i)                                   \
+  do {                                                   \
+    for (int z_ = 0; z_ < g_pknob[i]; ++z_) __builtin_amdgcn_s_sleep(4); \
+  } while (0)
+#else
+#define PKNOB_SLEEP(i) \
+  do {                 \
+  } while (0)
+#endif
+
 // Wait (sc1 polls) until a row's stamp reaches step tp, i.e. its owner in the same launch has
 // stored the row and then the stamp.  Bounded: after ~10 s err bit 8 is raised and the wait gives
 // up (the call then fails) instead of hanging the queue.
@@ -134,6 +169,7 @@ static __device__ __forceinline__ void wait_stamp(const int32_t* stamp, int32_t 
     uint32_t polls = 0;
     while (__hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tp) {
       __builtin_amdgcn_s_sleep(1);
+      PKNOB_SLEEP(0);
       if ((++polls & 255) == 0) {  // a wait that already timed out elsewhere ends this one too
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 100 MHz: 10 s
@@ -186,7 +222,13 @@ static __device__ __forceinline__ bool build_failed(const BatchView& bv) {
 #else
 #define BPRMF_DIAG_PREV
 #endif
-template <int G4, int S, bool SH, bool WT, bool WAIT>
+#ifdef BPRMF_PERSIST_STAMPS  // per step (t mod 32), K1 workgroup and triplet slot: its waits done
+__device__ uint64_t g_persist_k1wait[32][1024][32];
+extern "C" int bprmf_debug_persist_k1wait(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_persist_k1wait), sizeof(g_persist_k1wait)) == hipSuccess ? 0 : -3;
+}
+#endif
+template <int G4, int S, bool SH, bool WT, bool WAIT, bool PS = false>
 static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, const float* __restrict__ item_rows,
@@ -269,16 +311,16 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       // here; a marked one is read again (sc1) once its stamp says it is published
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        pu[k] = ld4(prow + 4 * G4 * k);
-        vi[k] = ld4(qi + 4 * G4 * k);
-        vj[k] = ld4(qj + 4 * G4 * k);
+        pu[k] = ld4p<PS>(prow + 4 * G4 * k);
+        vi[k] = ld4p<PS>(qi + 4 * G4 * k);
+        vj[k] = ld4p<PS>(qj + 4 * G4 * k);
       }
       // marks and stamps in ONE round of loads (sc1 stamps: the first poll of a marked row); a
       // marked row whose stamp is not yet tp is then polled alone, so a triplet with two or three
       // rows already published pays one load latency here instead of one per row
       const int64_t o = (int64_t)(tp & 1);
-      const int32_t mi = sb.pend_q[o * sb.qrows + i], mj = sb.pend_q[o * sb.qrows + j];
-      const int32_t mu = sb.pend_p[o * sb.prows + u];
+      const int32_t mi = ldw<PS>(sb.pend_q + o * sb.qrows + i), mj = ldw<PS>(sb.pend_q + o * sb.qrows + j);
+      const int32_t mu = ldw<PS>(sb.pend_p + o * sb.prows + u);
       si = __hip_atomic_load(Q.stamp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sj = __hip_atomic_load(Q.stamp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       su0 = __hip_atomic_load(P.stamp + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -298,6 +340,11 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       if (wj && sj != tp) wait_stamp(Q.stamp + j, tp, err);
       if (wu && su0 != tp) wait_stamp(P.stamp + u, tp, err);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the row loads stay after the stamp reads
+#ifdef BPRMF_PERSIST_STAMPS
+      if (PS && sub == 0 && blk < 1024)
+        g_persist_k1wait[t & 31][blk][(threadIdx.x / G4) & 31] =
+            __builtin_amdgcn_s_memrealtime() | ((uint64_t)(wi | wj << 1 | wu << 2) << 60);
+#endif
     }
     SSTAMP(0, 4);
     if (WAIT) {
@@ -409,21 +456,22 @@ template <int G4, int S, bool SH>
 struct ItemRow {
   float4 x[S];
   int32_t stamp = 0;
+  template <bool PS = false>
   __device__ __forceinline__ void load(const Table& Q, int32_t item, int ld, int sub) {
     if (SH) return;
     const float* w = Q.W + (int64_t)item * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) x[k] = ld4(w + 4 * G4 * k);
-    stamp = Q.stamp[item];
+    for (int k = 0; k < S; ++k) x[k] = ld4p<PS>(w + 4 * G4 * k);
+    stamp = ldw<PS>(Q.stamp + item);
   }
 };
 
-template <int G4, int S>
+template <int G4, int S, bool PS = false>
 static __device__ __forceinline__ void load_ref(float4 (&row)[S], const float* __restrict__ contrib,
                                                 int32_t ref, int ld, int sub) {
   const float* cb = contrib + (int64_t)(ref >> 1) * ld + 4 * sub;
 #pragma unroll
-  for (int k = 0; k < S; ++k) row[k] = ld4(cb + 4 * G4 * k);
+  for (int k = 0; k < S; ++k) row[k] = ld4p<PS>(cb + 4 * G4 * k);
 }
 
 template <int S>
@@ -463,7 +511,7 @@ static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int sl
 }
 
 // sum of the rows src[beg..end) in order (lanes fetch G4 indices at once, 8 rows in flight)
-template <int G4, int S>
+template <int G4, int S, bool PS = false>
 static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __restrict__ src,
                                                 int beg, int end, int ld, int sub) {
 #pragma unroll
@@ -475,7 +523,7 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
       if (m0 + m < end) {
         const float* rp = src + (int64_t)(m0 + m) * ld + 4 * sub;
 #pragma unroll
-        for (int k = 0; k < S; ++k) rows[m][k] = ld4(rp + 4 * G4 * k);
+        for (int k = 0; k < S; ++k) rows[m][k] = ld4p<PS>(rp + 4 * G4 * k);
       }
 #pragma unroll
     for (int m = 0; m < 8; ++m)
@@ -495,7 +543,7 @@ template <int S>
 constexpr int item_rounds() { return S == 1 ? 6 : 1; }
 // one K2 item segment (record r0/r1): the sum of -/+ c P_u over its references in order, then the
 // update (single GPU) or the per-slot gradient (sharded)
-template <int G4, int S, bool SH, bool WT, bool PUB>
+template <int G4, int S, bool SH, bool WT, bool PUB, bool PS>
 // Diagnostic build only (-DBPRMF_DIAG_SLOTS, WRONG results, timing only): what K2's cold item
 // segments would gain if their first 4 contribution rows sat at positions known without the
 // record (a slot-major contribution layout): 4 rows per lane group are requested in the same
@@ -523,7 +571,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
   if (kStampHere && threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
 #endif
   ItemRow<G4, S, SH> row;
-  row.load(Q, item, ld, sub);
+  row.template load<PS>(Q, item, ld, sub);
   float4 g[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -541,7 +589,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
         continue;
       }
 #endif
-      if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+      if (m < len) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
     }
 #pragma unroll
     for (int m = 0; m < kInlineRefs; ++m)
@@ -560,7 +608,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 #pragma unroll
         for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
-          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+          if (m0 + m < cnt) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
         for (int m = 0; m < F; ++m)
@@ -576,7 +624,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 // segments (one lane group each), user segments spanning K1 workgroups.  PUB (fused step): every
 // updated row's stamp is published after the row (put_stamp), for K1 of step t+1 in the same
 // launch.
-template <int G4, int S, bool SH, int KB, bool WT, bool PUB>
+template <int G4, int S, bool SH, int KB, bool WT, bool PUB, bool PS = false>
 static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, int long_blocks, int item_blocks,
@@ -604,7 +652,8 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     __shared__ double red[KB / 64];
     const int n = bv.meta[0];
     const int p = blk * KB + threadIdx.x;
-    double acc = p < n ? (double)softplus(-xloss[p]) : 0.0;
+    double acc =
+        p < n ? (double)softplus(-__int_as_float(ldw<PS>(reinterpret_cast<const int32_t*>(xloss) + p))) : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);  // fixed butterfly
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -630,9 +679,9 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
     float4 cur[S], g[S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) cur[k] = ld4(pw + 4 * G4 * k);
-    const int32_t su = P.stamp[u];
-    sum_rows<G4, S>(g, ugrad, r0.y, r0.z, ld, sub);
+    for (int k = 0; k < S; ++k) cur[k] = ld4p<PS>(pw + 4 * G4 * k);
+    const int32_t su = ldw<PS>(P.stamp + u);
+    sum_rows<G4, S, PS>(g, ugrad, r0.y, r0.z, ld, sub);
     SSTAMP(1, 2);
     const float f = decay_pow(hp.log2a, t - 1 - su);
 #pragma unroll
@@ -651,7 +700,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
     ItemRow<G4, S, SH> row;
-    if (grp == 0) row.load(Q, item, ld, sub);
+    if (grp == 0) row.template load<PS>(Q, item, ld, sub);
     float4 g[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -669,7 +718,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
 #pragma unroll
         for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
-          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
+          if (m0 + m < cnt) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
         for (int m = 0; m < F; ++m)
@@ -735,10 +784,10 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
       r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
     }
 #ifdef BPRMF_DIAG_SLOTS
-    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk,
-                                        (!SH && round == 0) ? pre : nullptr);
+    k2_item_segment<G4, S, SH, WT, PUB, PS>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk,
+                                            (!SH && round == 0) ? pre : nullptr);
 #else
-    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
+    k2_item_segment<G4, S, SH, WT, PUB, PS>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
 #endif
   }
 }
@@ -809,6 +858,139 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
     k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
                                       hp, ld, t + 1, sb, nullptr, B, err);
 #endif
+  }
+}
+
+// ---- the persistent step: a whole chunk in one launch (BPRMF_PERSIST, k_persist_steps) ----
+// Each workgroup keeps one role for the chunk: K2 workgroup b runs K2 of every step, K1
+// workgroup w runs K1 of every step, and the kernel boundary between fused launches becomes two
+// flag gates.  Every workgroup publishes its progress after each step (its stores acknowledged,
+// a workgroup barrier, then an sc1 store of the step number: MI355X_MICROARCH.md "Valid forms",
+// the first table row); f1[w] = the last step K1 workgroup w finished, f2[b] likewise for K2.
+//   K2 of step t starts once every K1 workgroup has finished step t (all contributions, xloss,
+//     ugrad and K1's in-place row updates of step t are in; the step's pend marks too);
+//   K1 of step t starts once every K1 workgroup has finished step t-1 (the marks of step t-1 are
+//     final, so the fused K1's mark-and-stamp protocol applies unchanged) and every K2 workgroup
+//     has finished step t-2 (the contribution / ugrad / xloss half of step t is free again, and
+//     every row update of steps <= t-2 is complete).
+// K2 of step t therefore runs beside K1 of step t+1 exactly as in k_fused_step, without the
+// boundary, the dispatch of ~850 workgroups and their record loads between steps.  Flags hold
+// global step numbers, which only grow, so they are never reset.  All of the launch's workgroups
+// must be resident at once (persist_step checks the occupancy); every wait is bounded (err bit 8
+// after ~10 s, and a raised bit 8 ends every other wait), so a violated assumption fails the call
+// instead of hanging the queue.
+// diagnostic build only (-DBPRMF_PERSIST_STAMPS, tools/ubench_persist_stamps.py): per step k < 32
+// and workgroup, s_memrealtime after its gate, after its step's body, after its arrival
+#ifdef BPRMF_PERSIST_STAMPS
+__device__ uint64_t g_persist_stamps[32][2048][3];
+#define PSTAMP(k, which)                                                             \
+  do {                                                                               \
+    if (threadIdx.x == 0 && (k) < 32 && blk < 2048)                                  \
+      g_persist_stamps[k][blk][which] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
+extern "C" int bprmf_debug_persist_stamps(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_persist_stamps), sizeof(g_persist_stamps)) == hipSuccess ? 0 : -3;
+}
+#else
+#define PSTAMP(k, which) \
+  do {                   \
+  } while (0)
+#endif
+// Progress flags: one int32 per workgroup (the step it finished), polled by wave 0 of a waiting
+// workgroup alone, 4 flags per lane per round (two 8-byte sc1 loads).  (Byte flags, 4x fewer
+// lines, measured slower: profiles/r05_persist.)
+static __device__ __forceinline__ bool flags_reached(const int32_t* f, int n, int32_t target, int lane) {
+  bool ok = true;
+  for (int base = 4 * lane; base < n; base += 256) {
+    const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(f + base), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(f + base) + 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t v[4] = {(int32_t)a, (int32_t)(a >> 32), (int32_t)b, (int32_t)(b >> 32)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (base + q < n) ok &= v[q] >= target;
+  }
+  return ok;
+}
+
+static __device__ __forceinline__ void gate_wait(const int32_t* f, int n, int32_t target,
+                                                 const int32_t* f2, int n2, int32_t target2,
+                                                 int32_t* err) {
+  __shared__ int s_bail;
+  if (threadIdx.x < 64) {  // wave 0 polls; the others wait at the barrier below
+    const int lane = threadIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int bail = 0;
+    for (uint32_t polls = 1;; ++polls) {
+      const bool ok = flags_reached(f, n, target, lane) && flags_reached(f2, n2, target2, lane);
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(2);
+      PKNOB_SLEEP(2);
+      if ((polls & 127) == 0) {
+        bail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8;
+        if (!bail && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 100 MHz: 10 s
+          if (lane == 0) atomicOr(err, 8);
+          bail = 1;
+        }
+        if (bail) break;  // uniform over the wave (every lane read the same word and clock)
+      }
+    }
+    if (lane == 0) s_bail = bail;
+  }
+  __syncthreads();  // every later load of the step sits behind the polling wave's match
+}
+
+static __device__ __forceinline__ void gate_arrive(int32_t* f, int32_t t) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores of the step acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(f, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int G4, int S, int KB>
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(4))) void k_persist_steps(BatchView bv0, Table P, Table Q, Hyper hp, int ld,
+                                                      const int32_t* __restrict__ tbase, StepBufs sb,
+                                                      int long_blocks, int item_blocks, int k2_blocks,
+                                                      int k1_blocks, double* __restrict__ loss,
+                                                      int64_t bstride, int B, int n, int32_t* err,
+                                                      int32_t* f1, int32_t* f2) {
+  static_assert(KB == kBlock, "K1 and K2 workgroups share the launch's block size");
+  const int32_t t0 = tbase[0];
+  const int64_t kb0 = tbase[1];
+  const int blk = blockIdx.x;
+  if (blk < k2_blocks) {
+    for (int k = 0; k < n; ++k) {
+      const int32_t t = t0 + k + 1;
+      gate_wait(f1, k1_blocks, t, nullptr, 0, 0, err);
+      PSTAMP(k, 0);
+#ifdef BPRMF_PERSIST_STAMPS
+      if (g_pknob[1] == 1) __builtin_amdgcn_s_setprio(1);
+      if (g_pknob[1] == 2) __builtin_amdgcn_s_setprio(2);
+      if (g_pknob[1] == 3) __builtin_amdgcn_s_setprio(3);
+#endif
+      k2_body<G4, S, false, KB, true, true, true>(blk, bv0.shifted((kb0 + k) * bstride), P, Q, hp, ld, t,
+                                                  sb, long_blocks, item_blocks, nullptr, loss, B);
+      PSTAMP(k, 1);
+      gate_arrive(f2 + blk, t);
+      PSTAMP(k, 2);
+    }
+    return;
+  }
+  const int w = blk - k2_blocks;
+  for (int k = 0; k < n; ++k) {
+    const int32_t t = t0 + k + 1;
+    const BatchView bv = bv0.shifted((kb0 + k) * bstride);
+    if (k == 0) {  // the rows are final since the previous launch: plain loads, no marks to read
+      PSTAMP(k, 0);
+      k1_body<G4, S, false, true, false>(w, bv, P, Q, hp, ld, t, sb, nullptr, B, err);
+    } else {
+      gate_wait(f1, k1_blocks, t - 1, f2, k >= 2 ? k2_blocks : 0, t - 2, err);
+      PSTAMP(k, 0);
+      k1_body<G4, S, false, true, true, true>(w, bv, P, Q, hp, ld, t, sb, nullptr, B, err);
+    }
+    PSTAMP(k, 1);
+    gate_arrive(f1 + w, t);
+    PSTAMP(k, 2);
   }
 }
 
@@ -1002,6 +1184,45 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
     k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
         bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,
         bstride, B, err);
+  }));
+  return hipGetLastError();
+}
+
+// the persistent step's grid: every workgroup must be resident at once (its waits are on the
+// others); 0 = it does not fit this device at this shape (the caller runs the fused launches)
+int persist_grid(const Geom& g, int B, bool loss, int* k2_blocks, int* k1_blocks) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  int total = 0;
+  BPRMF_DISPATCH4(g, ({
+    // one stripe (d <= 256) only: wider rows need more registers than 4 resident workgroups per
+    // CU leave (the kernel is held to 128 VGPRs, and spills there at S >= 2)
+    if (S_ != 1) return 0;
+    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss, true);
+    *k2_blocks = k.total();
+    *k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_persist_steps<G4_, S_, kBlock>, kBlock, 0) !=
+        hipSuccess)
+      return 0;
+    total = *k2_blocks + *k1_blocks;
+  }));
+  return (int64_t)per_cu * cus >= total ? total : 0;
+}
+
+hipError_t persist_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
+                        const Hyper& hp, const int32_t* tbase, int n, const StepBufs& sb, double* loss,
+                        int32_t* err, int32_t* f1, int32_t* f2, hipStream_t s) {
+  if (!sb.pend_q || !sb.pend_p || !sb.pstride || !bstride || n <= 0) return hipErrorInvalidValue;
+  if (!sb.xloss) loss = nullptr;
+  BPRMF_DISPATCH4(g, ({
+    // the same item-grid cap as the fused launches (Q.rows >= 2B), which persist_grid assumes
+    if (Q.rows < 2LL * B) return hipErrorInvalidValue;
+    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss != nullptr, true);
+    const int k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
+    k_persist_steps<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
+        bv0, P, Q, hp, g.ld, tbase, sb, k.long_blocks, k.item_blocks, k.total(), k1_blocks, loss,
+        bstride, B, n, err, f1, f2);
   }));
   return hipGetLastError();
 }

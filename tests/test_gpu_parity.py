@@ -793,3 +793,35 @@ def test_status_folded_into_last_k2_equals_status_launch(rl, golden, monkeypatch
     with pytest.raises(rl.BprmfError, match="batch builder"):
         m.train_steps(0, 2, 3)
     assert m.train_steps(0, 5, 3)["loss"] > 0
+
+
+@pytest.mark.parametrize("U,I,d,B", [(138493, 26744, 128, 4096), (3000, 9000, 32, 2048),
+                                     (943, 1682, 64, 512), (200, 400, 8, 64)])
+def test_persistent_step_equals_fused_launches_bitwise(rl, monkeypatch, U, I, d, B):
+    """The persistent step (one launch per chunk, K1 / K2 workgroups handing steps over by
+    progress flags, step.hip k_persist_steps) gives the fused launches' result bit for bit: the
+    same K1 / K2 arithmetic, only the schedule differs.  Chunks of 2 .. 300 steps, a second epoch,
+    the call losses equal too; the persistent launch must actually have run."""
+    syn = __import__("importlib").import_module("recommend-lib_amd.synthetic")
+    pos = syn.make_positives(U, I, min(40 * U, 2_000_000), 5)
+    outs = []
+    for persist in ("1", "0"):
+        monkeypatch.setenv("BPRMF_PERSIST", persist)
+        m = _model(rl, U, I, d, B, seed=13)
+        m.set_train(pos)
+        n = m.epoch_size()[1]
+        losses, first = [], 0
+        for c in (2, 3, 20, 1, 64, 300):
+            c = min(c, n - first)
+            if c <= 0:
+                break
+            losses.append(m.train_steps(0, first, c)["loss"])
+            first += c
+        losses.append(m.train_steps(1, 0, min(n, 21))["loss"])
+        if persist == "1":
+            assert m.debug_persist_grid() > 0
+        outs.append((m.get_weights(), losses))
+    (P0, Q0), l0 = outs[0]
+    (P1, Q1), l1 = outs[1]
+    assert np.array_equal(P0, P1) and np.array_equal(Q0, Q1)
+    assert l0 == l1

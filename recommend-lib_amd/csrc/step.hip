@@ -948,7 +948,10 @@ static __device__ __forceinline__ void gate_arrive(int32_t* f, int32_t t) {
 }
 
 template <int G4, int S, int KB>
-__global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(4))) void k_persist_steps(BatchView bv0, Table P, Table Q, Hyper hp, int ld,
+#ifndef BPRMF_PERSIST_WAVES  // waves per SIMD the persistent kernel is held to (diagnostic builds vary it)
+#define BPRMF_PERSIST_WAVES 4
+#endif
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(BPRMF_PERSIST_WAVES))) void k_persist_steps(BatchView bv0, Table P, Table Q, Hyper hp, int ld,
                                                       const int32_t* __restrict__ tbase, StepBufs sb,
                                                       int long_blocks, int item_blocks, int k2_blocks,
                                                       int k1_blocks, double* __restrict__ loss,

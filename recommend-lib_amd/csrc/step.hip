@@ -709,7 +709,11 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int lane0 = (threadIdx.x & 63) - sub;
     for (int base = beg + grp; base < end; base += NG * G4) {
       const int ridx = base + NG * sub;
+#ifdef BPRMF_DIAG_HOTPRE  // diagnostic only (WRONG results): no refs level, as a slot-major layout
+      const int32_t myref = ridx < end ? (int32_t)((ridx % B) << 1) : 0;
+#else
       const int32_t myref = ridx < end ? bv.refs[ridx] : 0;
+#endif
       const int cnt = min(G4, (end - base + NG - 1) / NG);
       constexpr int F = S == 1 ? 16 : 8;  // rows in flight per group (a hot item has ~80 refs)
       for (int m0 = 0; m0 < cnt; m0 += F) {

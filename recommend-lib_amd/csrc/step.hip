@@ -307,14 +307,14 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
     const float* qj = qbase + (int64_t)j * ld + 4 * sub;
     float4 vi[S], vj[S];
     if (WAIT) {
-      // the rows too, speculatively in the same round: a row step t-1 does not update is final
-      // here; a marked one is read again (sc1) once its stamp says it is published
+      // the user row too, speculatively in the same round (a user step t-1 does not update is
+      // final here; a marked one is read again, sc1, once its stamp says it is published).  The
+      // item rows wait for their marks: most triplets hold a marked item, whose speculative read
+      // was wasted bytes in the launch's opening burst, and the triplets with unmarked items are
+      // not the launch's tail (round 5 A/B: fused launch 9.45 -> 9.37 us by rocprofv3, 9.37-9.47
+      // -> 9.21-9.24 us by events, profiles/r05_ab_k1_late_items.txt)
 #pragma unroll
-      for (int k = 0; k < S; ++k) {
-        pu[k] = ld4p<PS>(prow + 4 * G4 * k);
-        vi[k] = ld4p<PS>(qi + 4 * G4 * k);
-        vj[k] = ld4p<PS>(qj + 4 * G4 * k);
-      }
+      for (int k = 0; k < S; ++k) pu[k] = ld4p<PS>(prow + 4 * G4 * k);
       // marks and stamps in ONE round of loads (sc1 stamps: the first poll of a marked row); a
       // marked row whose stamp is not yet tp is then polled alone, so a triplet with two or three
       // rows already published pays one load latency here instead of one per row
@@ -351,8 +351,8 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         if (wu) pu[k] = ld4_sc1(prow + 4 * G4 * k);
-        if (wi) vi[k] = ld4_sc1(qi + 4 * G4 * k);
-        if (wj) vj[k] = ld4_sc1(qj + 4 * G4 * k);
+        vi[k] = wi ? ld4_sc1(qi + 4 * G4 * k) : ld4p<PS>(qi + 4 * G4 * k);
+        vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4p<PS>(qj + 4 * G4 * k);
       }
     } else {
 #pragma unroll

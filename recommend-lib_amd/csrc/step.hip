@@ -921,7 +921,6 @@ static __device__ __forceinline__ bool flags_reached(const int32_t* f, int n, in
 static __device__ __forceinline__ void gate_wait(const int32_t* f, int n, int32_t target,
                                                  const int32_t* f2, int n2, int32_t target2,
                                                  int32_t* err) {
-  __shared__ int s_bail;
   if (threadIdx.x < 64) {  // wave 0 polls; the others wait at the barrier below
     const int lane = threadIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -937,10 +936,10 @@ static __device__ __forceinline__ void gate_wait(const int32_t* f, int n, int32_
           if (lane == 0) atomicOr(err, 8);
           bail = 1;
         }
-        if (bail) break;  // uniform over the wave (every lane read the same word and clock)
+        if (bail) break;  // uniform over the wave (every lane read the same word and clock); the
+                          // step then runs on whatever it reads, and the call fails on err bit 8
       }
     }
-    if (lane == 0) s_bail = bail;
   }
   __syncthreads();  // every later load of the step sits behind the polling wave's match
 }

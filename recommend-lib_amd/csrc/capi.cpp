@@ -786,8 +786,9 @@ static bool fold_enabled() {
 }
 
 // BPRMF_PERSIST=1 runs each chunk as ONE persistent launch (step.hip k_persist_steps; read per
-// call).  Opt-in: bitwise equal to the fused launches but measured 1.4-2.2x slower per step
-// (profiles/r05_persist_*: 13.6-20.7 against 9.4-9.5 us), see DESIGN.md §5 "Round 5".
+// call).  Opt-in: bitwise equal to the fused launches but measured 1.6x slower per step (this
+// form: 15.5 against 9.5 us; earlier flag layouts 13.6-20.7, profiles/r05_persist/), see
+// DESIGN.md §5 "Round 5".
 static bool persist_enabled() {
   const char* e = getenv("BPRMF_PERSIST");
   return e && e[0] == '1';

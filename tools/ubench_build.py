@@ -50,6 +50,22 @@ if "--split" in sys.argv:  # the split builder (k_build_split): user workgroup, 
     res["user workgroup (us from its start)"] = {n: round(float(med[k]), 2) for k, n in enumerate(names_u)}
     res["first item part"] = {n: round(float(med[8 + k]), 2) for k, n in enumerate(names_i)}
     res["last item part"] = {n: round(float(med[16 + k]), 2) for k, n in enumerate(names_i)}
+    # every workgroup of the last call's launch: start / end spread, per role, per batch
+    L.bprmf_debug_split_se.argtypes = [ctypes.c_void_p]
+    se = np.zeros((4096, 2), np.uint64)
+    assert L.bprmf_debug_split_se(se.ctypes.data) == 0
+    se = se[:20 * 9].astype(np.int64)
+    t0 = se[:, 0].min()
+    st, en = (se[:, 0] - t0) * 0.01, (se[:, 1] - t0) * 0.01
+    role = np.arange(len(se)) % 9
+    res["all workgroups (us from the first start)"] = {
+        "start (median, max)": [round(float(np.median(st)), 2), round(float(st.max()), 2)],
+        "user workgroup end (median, max)": [round(float(np.median(en[role == 0])), 2), round(float(en[role == 0].max()), 2)],
+        "item part end (median, p90, max)": [round(float(np.median(en[role > 0])), 2),
+                                             round(float(np.percentile(en[role > 0], 90)), 2), round(float(en[role > 0].max()), 2)],
+        "slowest batch's ends": [round(float(x), 2) for x in en.reshape(20, 9)[int(np.argmax(en.reshape(20, 9).max(1)))]],
+        "item part duration (median, max)": [round(float(np.median((en - st)[role > 0])), 2), round(float((en - st)[role > 0].max()), 2)],
+    }
     print(json.dumps(res, indent=1))
     sys.exit(0)
 for radix in ("0",) if "--quick" in sys.argv else ("0", "1"):

@@ -708,9 +708,26 @@ static __device__ __forceinline__ uint64_t* xch_of(const BatchView& v) {
       g_build_stamps[(blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 8 : 16) + (k)] =               \
           __builtin_amdgcn_s_memrealtime();                                                  \
   } while (0)
+// and every workgroup's start and end (g_split_se[wg] = {start, end}, up to 4096 workgroups)
+__device__ uint64_t g_split_se[4096][2];
+struct SplitSE {
+  __device__ SplitSE() {
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_split_se[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ ~SplitSE() {
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_split_se[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+  }
+};
+extern "C" int bprmf_debug_split_se(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_se), sizeof(g_split_se)) == hipSuccess ? 0 : -3;
+}
+#define SPLIT_SE SplitSE split_se_
 #else
 #define SPSTAMP(k) \
   do {             \
+  } while (0)
+#define SPLIT_SE \
+  do {           \
   } while (0)
 #endif
 // x / d for 32-bit unsigned x by a multiply-high and a shift (round-up method: l = ceil(log2 d),
@@ -750,6 +767,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_split(
   constexpr int IPT = 4;
   constexpr int IPT2 = 2 * IPT;
   CsScope cs_(0);  // diagnostic builds only (BPRMF_CALL_STAMPS)
+  SPLIT_SE;
   using Scan = rocprim::block_scan<int, T>;
   using ScanL = rocprim::block_scan<uint64_t, T>;
   constexpr size_t kBucketBytes = 12 * (size_t)T * IPT2 + 4 * (kBuckets + 4);

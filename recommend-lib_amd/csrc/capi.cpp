@@ -249,8 +249,9 @@ int bprmf_destroy(bprmf_handle* h) {
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_fold_cnt, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p, h->d_pflags, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
-                  h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec};
+                  h->d_pend_q, h->d_pend_p, h->d_pflags, h->d_hbits, h->d_hhash, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
+                  h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec,
+                  h->d_pos4};
   for (void* p : ptrs)
     if (p) hipFree(p);
   drop_graphs(h);
@@ -294,11 +295,22 @@ int bprmf_row_stride(bprmf_handle* h, int32_t* ld) {
   return 0;
 }
 
+extern "C++" LocalArgs bprmf::local_args(const bprmf_handle* h) {
+  LocalArgs la;
+  la.hot = h->d_hot;
+  la.rep = h->d_qrep;
+  la.H = h->hot_H;
+  la.hbits = h->d_hbits;
+  la.hhash = h->d_hhash;
+  la.hlog = h->hot_hlog;
+  return la;
+}
+
 // semantics LOCAL: the hot items (the most frequent positives; BPRMF_LOCAL_HOT overrides how many)
 // get one replica row per XCD, filled from the base table (a refresh merge at the current step)
 static int local_refresh(bprmf_handle* h) {
   if (!h->d_qrep) return 0;
-  LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  LocalArgs la = local_args(h);
   HIPCHK(local_merge(h->geom, h->Q, la, h->d_hot_rows, h->hp, h->t, h->t, true, h->stream));
   h->rep_t = h->t;
   return 0;
@@ -319,16 +331,43 @@ static int local_setup(bprmf_handle* h, const std::vector<int32_t>& pos_items) {
     hot[order[k]] = (int32_t)k;
   }
   const size_t rep_bytes = sizeof(float) * (size_t)kLocalXcds * H * h->geom.ld;
-  for (void* p : {(void*)h->d_hot, (void*)h->d_hot_rows, (void*)h->d_qrep})
+  for (void* p : {(void*)h->d_hot, (void*)h->d_hot_rows, (void*)h->d_qrep, (void*)h->d_hbits, (void*)h->d_hhash})
     if (p) HIPCHK(hipFree(p));
   h->d_hot = h->d_hot_rows = nullptr;
   h->d_qrep = nullptr;
+  h->d_hbits = nullptr;
+  h->d_hhash = nullptr;
+  h->hot_hlog = 0;
   h->hot_H = H;
   if (int r = dalloc(&h->d_hot, I)) return r;
   if (int r = dalloc(&h->d_hot_rows, std::max<int64_t>(H, 1))) return r;
   if (H > 0) HIPCHK(hipMalloc((void**)&h->d_qrep, rep_bytes));
   HIPCHK(hipMemcpy(h->d_hot, hot.data(), 4 * I, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->d_hot_rows, rows.data(), 4 * rows.size(), hipMemcpyHostToDevice));
+  // a catalogue whose hot[] (4 B per item) is past the caches: the kernels' per-triplet lookup
+  // reads a bit per item instead (I / 8 bytes, mostly cache-resident) and, for the hot items
+  // alone, a small open-addressing table (BPRMF_LOCAL_HOT_BITS: the item count from which the
+  // bits are used; 0 = always, default 16M items = a 64 MB hot[])
+  int64_t bits_from = 16LL << 20;
+  if (const char* e = getenv("BPRMF_LOCAL_HOT_BITS")) bits_from = std::max<int64_t>(0, atoll(e));
+  if (H > 0 && I >= bits_from) {
+    int hlog = 1;
+    while ((1LL << hlog) < 2 * H) ++hlog;
+    std::vector<uint32_t> bits((I + 31) / 32, 0u);
+    std::vector<int2> tab((size_t)1 << hlog, int2{-1, -1});
+    for (int64_t k = 0; k < H; ++k) {
+      const uint32_t it = (uint32_t)rows[k];
+      bits[it >> 5] |= 1u << (it & 31);
+      uint32_t q = (it * 0x9E3779B1u) >> (32 - hlog);  // hogwild.hip hot_probe's hash
+      while (tab[q].x >= 0) q = (q + 1) & ((1u << hlog) - 1);
+      tab[q] = int2{(int32_t)it, (int32_t)k};
+    }
+    if (int r = dalloc(&h->d_hbits, (int64_t)bits.size())) return r;
+    if (int r = dalloc(&h->d_hhash, (int64_t)tab.size())) return r;
+    HIPCHK(hipMemcpy(h->d_hbits, bits.data(), 4 * bits.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_hhash, tab.data(), sizeof(int2) * tab.size(), hipMemcpyHostToDevice));
+    h->hot_hlog = hlog;
+  }
   return local_refresh(h);
 }
 
@@ -350,12 +389,14 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   const std::vector<int64_t>& indptr = csr.indptr;
   const std::vector<int32_t>& indices = csr.indices;
   const int64_t n = (int64_t)pu.size();
-  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices, h->d_soff, h->d_skeys, h->d_pos2, h->d_urec};
+  void* olds[] = {h->d_pos_u, h->d_pos_i, h->d_indptr, h->d_indices, h->d_soff, h->d_skeys, h->d_pos2, h->d_urec,
+                  h->d_pos4};
   for (void* p : olds)
     if (p) HIPCHK(hipFree(p));
   h->d_pos_u = h->d_pos_i = h->d_indices = h->d_skeys = nullptr;
   h->d_indptr = h->d_soff = nullptr;
   h->d_pos2 = h->d_urec = nullptr;
+  h->d_pos4 = nullptr;
   // packed sampler reads (BPRMF_SAMPLE_PACKED=0: the separate arrays, A/B)
   const char* pk = getenv("BPRMF_SAMPLE_PACKED");
   const bool packed = !(pk && pk[0] == '0');
@@ -378,7 +419,23 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
       }
     }
   }
-  if (packed && !pu.empty()) {
+  // a large positive set: its user records (40+ MB of random reads) join the positives' records,
+  // one 16-byte line per draw instead of two lines (BPRMF_SAMPLE_POS4: the positive count from
+  // which; 0 = always, default 64M)
+  int64_t pos4_from = 64LL << 20;
+  if (const char* e = getenv("BPRMF_SAMPLE_POS4")) pos4_from = std::max<int64_t>(0, atoll(e));
+  if (packed && h->d_urec && !pu.empty() && (int64_t)pu.size() >= pos4_from) {
+    std::vector<int2> ur(h->U);
+    HIPCHK(hipMemcpy(ur.data(), h->d_urec, 8 * ur.size(), hipMemcpyDeviceToHost));
+    std::vector<int4> p4(pu.size());
+    const int64_t W = h->cfg.world;
+    for (size_t k = 0; k < pu.size(); ++k) {
+      const int2 r = ur[pu[k] / W];
+      p4[k] = make_int4(pu[k], pi[k], r.x, r.y);
+    }
+    if (int r = dalloc(&h->d_pos4, (int64_t)p4.size())) return r;
+    HIPCHK(hipMemcpy(h->d_pos4, p4.data(), 16 * p4.size(), hipMemcpyHostToDevice));
+  } else if (packed && !pu.empty()) {
     std::vector<int2> p2(pu.size());
     for (size_t k = 0; k < pu.size(); ++k) p2[k] = make_int2(pu[k], pi[k]);
     if (int r = dalloc(&h->d_pos2, (int64_t)p2.size())) return r;
@@ -443,6 +500,7 @@ SamplerArgs bprmf::sampler_args(bprmf_handle* h) {
   a.soff = h->d_soff;
   a.pos2 = h->d_pos2;
   a.urec = h->d_urec;
+  a.pos4 = h->d_pos4;
   return a;
 }
 
@@ -876,7 +934,7 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     // merge; the call's last period is merged too, so the base table is current when it returns
     if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
     const SamplerArgs sa = sampler_args(h);
-    const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+    const LocalArgs la = local_args(h);
     hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
     if (ea) HIPCHK(hipEventRecord(ea, h->stream));
     for (int64_t s0 = 0; s0 < n;) {

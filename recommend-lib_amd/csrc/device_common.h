@@ -222,7 +222,13 @@ static __device__ __forceinline__ bool sample_slot(const SamplerArgs& a, uint32_
   const uint64_t q = permute(slot, N, a.feistel_a, a.feistel_c, a.k0, a.k1, epoch);
 #endif
   const int64_t p = div_small(q, (uint32_t)a.num_ng);
-  if (a.pos2) {  // one 8-byte load: one line per positive instead of two
+  int2 ur4 = make_int2(0, 0);
+  if (a.pos4) {  // one 16-byte load: the positive and its user's record
+    const int4 pr = a.pos4[p];
+    u = pr.x;
+    i = pr.y;
+    ur4 = make_int2(pr.z, pr.w);
+  } else if (a.pos2) {  // one 8-byte load: one line per positive instead of two
     const int2 pr = a.pos2[p];
     u = pr.x;
     i = pr.y;
@@ -232,8 +238,8 @@ static __device__ __forceinline__ bool sample_slot(const SamplerArgs& a, uint32_
   }
   const uint32_t d0 = bounded_draw0(q, epoch, a.k0, a.k1);  // while the loads are in flight
   const int64_t ul = u / a.world;
-  if (a.urec) {  // {first tree key, positive count}: one line per user instead of indptr + soff
-    const int2 ur = a.urec[ul];
+  if (a.pos4 || a.urec) {  // {first tree key, positive count}: one line per user instead of indptr + soff
+    const int2 ur = a.pos4 ? ur4 : a.urec[ul];
     const int64_t free_u = a.item_num - ur.y;
     j = -1;
     if (free_u <= 0) return false;

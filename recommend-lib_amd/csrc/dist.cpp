@@ -1041,7 +1041,7 @@ static int dp_merge(bprmf_handle* h, bool last) {
   const int32_t tp = pend ? h->dp_tp : h->dp_t;
   const bool start = h->dp_overlap && !last;
   // the hot items' XCD replicas are merged inside the delta pass (k_local_merge's rule)
-  const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  const LocalArgs la = local_args(h);
   HIPCHK(dp_delta(h->Q, h->d_qbase, h->d_qdelta, pend ? h->dp_sum : nullptr, h->geom.ld, h->hp, h->dp_t, tp,
                   h->t, la, h->rep_t, start, h->stream));
   h->dp_t = tp;  // the base is current at tp now
@@ -1080,7 +1080,7 @@ static int dp_run(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
   bprmf_epoch_size(h, &N, nullptr);
   if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
   const SamplerArgs sa = sampler_args(h);
-  const LocalArgs la{h->d_hot, h->d_qrep, h->hot_H};
+  const LocalArgs la = local_args(h);
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;  // one pair: the periods and the merges
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));
   h->dist->x_steps += n_steps;

@@ -66,6 +66,7 @@ struct bprmf_handle {
   int32_t* d_skeys = nullptr;
   int2* d_pos2 = nullptr;       // {pos_u, pos_i} interleaved (the sampler's packed reads)
   int2* d_urec = nullptr;       // per local user {first tree key, positive count}
+  int4* d_pos4 = nullptr;       // large positive sets: {pos_u, pos_i, urec of the user} per positive
   uint32_t feistel_a = 1, feistel_c = 1;  // permute's domain Z_a x Z_c (feistel_dims)
   uint32_t k0 = 0, k1 = 0;  // shard sampler key
   // triplet chunk
@@ -81,6 +82,9 @@ struct bprmf_handle {
   int32_t semantics = BPRMF_SEM_EXACT;  // cfg.semantics (BPRMF_SEM_HOGWILD / LOCAL: hogwild.hip)
   // BPRMF_SEM_LOCAL: the hot items' per-XCD replicas (hogwild.hip k_local_merge)
   int32_t* d_hot = nullptr;       // [I] replica slot of an item, -1 = cold
+  uint32_t* d_hbits = nullptr;    // large catalogues: [I / 32] hot bit per item ...
+  int2* d_hhash = nullptr;        // ... and [2^hot_hlog] {item, slot} of the hot items
+  int hot_hlog = 0;
   int32_t* d_hot_rows = nullptr;  // [H] item of each slot
   float* d_qrep = nullptr;        // [kLocalXcds][H][ld]
   int64_t hot_H = 0;
@@ -171,7 +175,8 @@ struct ProfScope {
 };
 int ensure_trip(bprmf_handle* h, int64_t n);
 int ensure_seg(bprmf_handle* h, int64_t n_batches);
-StepBufs step_bufs(const bprmf_handle* h);  // the single-GPU step buffers (both halves, pend)
+StepBufs step_bufs(const bprmf_handle* h);
+LocalArgs local_args(const bprmf_handle* h);  // semantics LOCAL: hot items, replicas, lookups  // the single-GPU step buffers (both halves, pend)
 int ensure_grad(bprmf_handle* h);
 bool seg_mode(const bprmf_handle* h);
 // a sampled chunk of nb batches draws its triplets with the grid-wide sampler before the builder

@@ -115,6 +115,19 @@ static __device__ __forceinline__ int hw_xcc() {
   return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7;  // hwreg(HW_REG_XCC_ID, 0, 4)
 }
 
+// a hot item's replica slot from la.hhash (the item is there: its bit in la.hbits is set; the
+// probe count is bounded all the same)
+static __device__ __forceinline__ int32_t hot_probe(const LocalArgs& la, int32_t item) {
+  const uint32_t mask = (1u << la.hlog) - 1;
+  uint32_t h = ((uint32_t)item * 0x9E3779B1u) >> (32 - la.hlog);
+  for (uint32_t n = 0; n <= mask; ++n, h = (h + 1) & mask) {
+    const int2 e = la.hhash[h];
+    if (e.x == item) return e.y;
+    if (e.x < 0) break;
+  }
+  return -1;
+}
+
 // issue the round starting at slot k0 of the wave's chunk (ids from the lanes that sampled them)
 template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
 static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
@@ -306,8 +319,14 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
         if (mj >= 0 || !SAMPLE) atomicOr(err, 1);
         mu = -1;
       } else if (LOCAL) {  // the items' replica slots, looked up once by the sampling lane
-        mhi = la.hot[mi];
-        mhj = la.hot[mj];
+        if (la.hbits) {  // large catalogue: a bit per item, then the hot items' table
+          const uint32_t bi = la.hbits[(uint32_t)mi >> 5], bj = la.hbits[(uint32_t)mj >> 5];
+          mhi = (bi >> (mi & 31)) & 1 ? hot_probe(la, mi) : -1;
+          mhj = (bj >> (mj & 31)) & 1 ? hot_probe(la, mj) : -1;
+        } else {
+          mhi = la.hot[mi];
+          mhj = la.hot[mj];
+        }
       }
     }
     HwRound<S, UNR> A, Bf;

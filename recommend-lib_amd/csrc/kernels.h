@@ -138,6 +138,9 @@ struct SamplerArgs {
   // pos2[p] = {pos_u[p], pos_i[p]}; urec[local user] = {its first tree key, its positive count}
   const int2* pos2 = nullptr;
   const int2* urec = nullptr;
+  // large positive sets: pos4[p] = {pos_u, pos_i, urec[local user]}, the positive's record and its
+  // user's in ONE line (null: pos2 + urec)
+  const int4* pos4 = nullptr;
 };
 
 // --- launches (all asynchronous on `s`) ---
@@ -283,6 +286,12 @@ struct LocalArgs {
   const int32_t* hot = nullptr;
   float* rep = nullptr;
   int64_t H = 0;
+  // for a large catalogue (hot[] past the caches), the per-triplet lookup instead reads a bit
+  // per item (hbits, I bits) and, for a hot item, an open-addressing table of {item, slot}
+  // (hhash, 2^hlog entries, item -1 = empty); null: hot[] is read
+  const uint32_t* hbits = nullptr;
+  const int2* hhash = nullptr;
+  int hlog = 0;
 };
 constexpr int kLocalXcds = 8;
 hipError_t local_merge(const Geom& g, Table Q, const LocalArgs& la, const int32_t* rows,

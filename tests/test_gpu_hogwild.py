@@ -145,14 +145,18 @@ def _hot_positives(U, I, hot_items, g):
     return np.unique(np.array(rows, np.int64), axis=0)
 
 
+@pytest.mark.parametrize("hot_bits", ["table", "bits"])
 @pytest.mark.parametrize("d,B,period", [(8, 16, 3), (32, 64, 2), (128, 32, 5)])
-def test_local_serial_replay_matches_oracle(rl, monkeypatch, d, B, period):
+def test_local_serial_replay_matches_oracle(rl, monkeypatch, d, B, period, hot_bits):
     """The SERIAL build (one lane group on one XCD, slot order) against oracle/bpr_oracle.py:
     local_serial: hogwild's rule for users and cold items, the hot items in the XCD's replica
     (no weight-decay term inside a period) and the merge every `period` steps and at the call's
-    end (decayed base + the replica's change)."""
+    end (decayed base + the replica's change).  hot_bits: the per-triplet replica-slot lookup
+    through hot[] or through the large-catalogue form (a bit per item, then the hot items' hash
+    table; BPRMF_LOCAL_HOT_BITS=0 forces it at this size)."""
     monkeypatch.setenv("BPRMF_HOGWILD_SERIAL", "1")
     monkeypatch.setenv("BPRMF_LOCAL_HOT", "6")
+    monkeypatch.setenv("BPRMF_LOCAL_HOT_BITS", "0" if hot_bits == "bits" else str(1 << 40))
     g = np.random.default_rng(d + period)
     U, I, n = 23, 31, 300
     hot = [4, 9, 0, 17, 22, 30]

@@ -217,7 +217,11 @@ def _ml100k_pos(golden):
     return f["positives"].astype(np.int64), int(f["U"]), int(f["I"])
 
 
-def test_sampler_bit_exact_ml100k(rl, golden):
+@pytest.mark.parametrize("records", ["pos2", "pos4"])
+def test_sampler_bit_exact_ml100k(rl, golden, monkeypatch, records):
+    """records: the sampler's reads as {u, i} + the user's record (default at this size) or the
+    large-set form, both in one 16-byte record per positive (BPRMF_SAMPLE_POS4=0 forces it)."""
+    monkeypatch.setenv("BPRMF_SAMPLE_POS4", "0" if records == "pos4" else str(1 << 40))
     pos, U, I = _ml100k_pos(golden)
     m = _model(rl, U, I, 32, 4096, seed=0xDEADBEEF12345)
     m.set_train(pos)
@@ -234,9 +238,11 @@ def test_sampler_bit_exact_ml100k(rl, golden):
         assert np.array_equal(x, y)
 
 
-def test_sampler_deep_lists_bit_exact(rl):
+@pytest.mark.parametrize("records", ["pos2", "pos4"])
+def test_sampler_deep_lists_bit_exact(rl, monkeypatch, records):
     """Users with thousands of positives (several rounds of the 9-ary search for the k-th
-    non-positive) draw exactly the oracle's triplets."""
+    non-positive) draw exactly the oracle's triplets (both record forms, as above)."""
+    monkeypatch.setenv("BPRMF_SAMPLE_POS4", "0" if records == "pos4" else str(1 << 40))
     syn = __import__("importlib").import_module("recommend-lib_amd.synthetic")
     U, I = 20000, 5000
     pos = syn.make_positives(U, I, 2_000_000, seed=5)
@@ -283,9 +289,12 @@ def test_sampler_bit_exact_sharded(rl, golden):
             assert np.array_equal(x, y)
 
 
-def test_device_sampled_training_equals_replay_of_oracle_triplets(rl, golden):
+@pytest.mark.parametrize("records", ["pos2", "pos4"])
+def test_device_sampled_training_equals_replay_of_oracle_triplets(rl, golden, monkeypatch, records):
     """train_steps (device sampler + segmented step) == train_triplets(oracle's triplets), bitwise:
-    the sampler is bit-exact and the step is deterministic (no atomics, fixed summation order)."""
+    the sampler is bit-exact and the step is deterministic (no atomics, fixed summation order);
+    both sampler record forms (BPRMF_SAMPLE_POS4)."""
+    monkeypatch.setenv("BPRMF_SAMPLE_POS4", "0" if records == "pos4" else str(1 << 40))
     pos, U, I = _ml100k_pos(golden)
     seed, B = 4242, 4096
     a = _model(rl, U, I, 32, B, seed=seed)

@@ -346,10 +346,6 @@ def main():
             elif "step_graph" in us and hog:  # one k_hogwild launch per chunk
                 step_us, what = us["step_graph"], ("k_hogwild (in-kernel sampling + gather + dots + "
                                                    "sigmoid + SGD scatter, one launch per chunk)")
-            elif "step_graph" in us and m.debug_persist_grid() > 0:  # one launch per chunk
-                step_us, what = us["step_graph"], ("k_persist_steps (the chunk's steps in one launch: "
-                                                   "K1 / K2 workgroups resident for the whole chunk, "
-                                                   "steps handed over by progress flags)")
             elif "step_graph" in us:  # events around each chunk's step launches (GPU-bound)
                 step_us, what = us["step_graph"], ("fused step launches (K2 of step t + K1 of step "
                                                    "t+1 per launch; a chunk is K1, n-1 fused, K2)")

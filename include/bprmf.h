@@ -294,9 +294,6 @@ int bprmf_debug_fill_batches(bprmf_handle* h, int32_t value);
 /* Leave the batch buffer as a timed-out split build would (every batch marked dead, err bit 16):
  * the next call's steps must skip every batch, leave the tables untouched and fail. */
 int bprmf_debug_fail_build(bprmf_handle* h);
-/* *workgroups = the persistent step's launch size once a call has probed it (0: the device cannot
- * keep them all resident at this shape, so chunks run as fused launches; -1: not probed yet). */
-int bprmf_debug_persist_grid(bprmf_handle* h, int32_t* workgroups);
 
 /* ---- ingestion: ratings files -> dense-coded rows (util/data_loader.py:27-146, :410-548) ---- */
 /* Host-only (no GPU).  Lines "<user> <sep> <item> <sep> <rating> <sep> <timestamp>" with any

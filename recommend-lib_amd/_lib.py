@@ -119,7 +119,6 @@ SIGNATURES = {
     "bprmf_debug_next_build_tag": [ctypes.POINTER(ctypes.c_uint32)],
     "bprmf_debug_fill_batches": [_P, ctypes.c_int32],
     "bprmf_debug_fail_build": [_P],
-    "bprmf_debug_persist_grid": [_P, ctypes.POINTER(ctypes.c_int32)],
     "bprmf_profile": [_P, ctypes.c_int32],
     "bprmf_profile_read": [_P, ctypes.POINTER(KProf)],
     # include/ncf.h

@@ -76,7 +76,6 @@ int bprmf::check_err_flag(bprmf_handle* h) {
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 16) HIPCHK(clear_batches(h));
-    h->persist_t = -1;
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
     if (e & 2) return fail(BPRMF_E_NO_NEGATIVE, "a user has every item as a positive: no negative to sample");
@@ -162,10 +161,9 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   }
   h->stream = h->own_stream;
   h->use_graphs = getenv("BPRMF_NO_GRAPH") == nullptr;
-  {  // the fused step needs the write-through row stores (its hand-off protocol)
+  {  // BPRMF_FUSED=0: K1 + K2 launch pairs instead of the fused launches (the bitwise A/B test)
     const char* f = getenv("BPRMF_FUSED");
-    const char* w = getenv("BPRMF_WT");
-    h->fused = !(f && f[0] == '0') && !(w && w[0] == '0');
+    h->fused = !(f && f[0] == '0');
   }
   const int64_t ld = g.ld;
   if (dpi) {  // every rank holds the whole item table several times over: fail early and clearly
@@ -188,7 +186,6 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(dalloc(&h->P.stamp, h->U));
   TRY(dalloc(&h->Q.W, h->I * ld));
   TRY(dalloc(&h->Q.stamp, h->I));
-  TRY(dalloc(&h->d_fold_cnt, 1));
   if (dpi) {
     TRY(dalloc(&h->d_qbase, h->I * ld));
     // the delta table padded to world slices of ceil(I / world) rows (the IPC all-reduce pushes
@@ -220,7 +217,6 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
   TRY(memz(h->P.stamp, sizeof(int32_t) * h->U));
   if (h->d_qdelta) TRY(memz(h->d_qdelta, sizeof(float) * (size_t)(W * ((h->I + W - 1) / W) * ld)));
   TRY(memz(h->Q.stamp, sizeof(int32_t) * h->I));
-  TRY(memz(h->d_fold_cnt, sizeof(int32_t)));
   TRY(memz(h->d_status, status_bytes));
   // init keyed by the global seed and GLOBAL row id: identical tables for any world size
   const uint32_t s0 = (uint32_t)cfg->seed, s1 = (uint32_t)(cfg->seed >> 32);
@@ -243,13 +239,12 @@ int bprmf_destroy(bprmf_handle* h) {
   if (!h) return 0;
   hipSetDevice(h->cfg.device);
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
-  // a call returns once its status is out, possibly before its last launch has drained (the
-  // status folded into the last K2): a caller's stream is drained too before anything is freed
+  // a caller's stream is drained too before anything is freed
   if (h->stream && h->stream != h->own_stream) hipStreamSynchronize(h->stream);
-  void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_fold_cnt, h->d_pos_u, h->d_pos_i,
+  void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
-                  h->d_pend_q, h->d_pend_p, h->d_pflags, h->d_hbits, h->d_hhash, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
+                  h->d_pend_q, h->d_pend_p, h->d_hbits, h->d_hhash, h->d_hot, h->d_hot_rows, h->d_qrep, h->d_soff,
                   h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec,
                   h->d_pos4};
   for (void* p : ptrs)
@@ -397,26 +392,22 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   h->d_indptr = h->d_soff = nullptr;
   h->d_pos2 = h->d_urec = nullptr;
   h->d_pos4 = nullptr;
-  // packed sampler reads (BPRMF_SAMPLE_PACKED=0: the separate arrays, A/B)
-  const char* pk = getenv("BPRMF_SAMPLE_PACKED");
-  const bool packed = !(pk && pk[0] == '0');
-  {  // the sampler's search trees (BPRMF_SAMPLE_TREE=0: the binary search, A/B)
-    const char* e = getenv("BPRMF_SAMPLE_TREE");
-    if (!(e && e[0] == '0')) {
-      SearchTree st;
-      build_search_tree(indptr, indices, &st);
-      if (int r = dalloc(&h->d_soff, (int64_t)st.soff.size())) return r;
-      if (int r = dalloc(&h->d_skeys, std::max<int64_t>(16, (int64_t)st.keys.size()))) return r;
-      HIPCHK(hipMemcpy(h->d_soff, st.soff.data(), 8 * st.soff.size(), hipMemcpyHostToDevice));
-      if (!st.keys.empty())
-        HIPCHK(hipMemcpy(h->d_skeys, st.keys.data(), 4 * st.keys.size(), hipMemcpyHostToDevice));
-      if (packed && st.soff.back() < INT32_MAX) {
-        std::vector<int2> ur(h->U);
-        for (int64_t lu = 0; lu < h->U; ++lu)
-          ur[lu] = make_int2((int32_t)st.soff[lu], (int32_t)(indptr[lu + 1] - indptr[lu]));
-        if (int r = dalloc(&h->d_urec, std::max<int64_t>(1, h->U))) return r;
-        if (h->U) HIPCHK(hipMemcpy(h->d_urec, ur.data(), 8 * ur.size(), hipMemcpyHostToDevice));
-      }
+  // the sampler's search trees and packed records (one line per dependent level; the separate
+  // arrays and the binary search remain for positive sets past 32-bit tree offsets)
+  {
+    SearchTree st;
+    build_search_tree(indptr, indices, &st);
+    if (int r = dalloc(&h->d_soff, (int64_t)st.soff.size())) return r;
+    if (int r = dalloc(&h->d_skeys, std::max<int64_t>(16, (int64_t)st.keys.size()))) return r;
+    HIPCHK(hipMemcpy(h->d_soff, st.soff.data(), 8 * st.soff.size(), hipMemcpyHostToDevice));
+    if (!st.keys.empty())
+      HIPCHK(hipMemcpy(h->d_skeys, st.keys.data(), 4 * st.keys.size(), hipMemcpyHostToDevice));
+    if (st.soff.back() < INT32_MAX) {
+      std::vector<int2> ur(h->U);
+      for (int64_t lu = 0; lu < h->U; ++lu)
+        ur[lu] = make_int2((int32_t)st.soff[lu], (int32_t)(indptr[lu + 1] - indptr[lu]));
+      if (int r = dalloc(&h->d_urec, std::max<int64_t>(1, h->U))) return r;
+      if (h->U) HIPCHK(hipMemcpy(h->d_urec, ur.data(), 8 * ur.size(), hipMemcpyHostToDevice));
     }
   }
   // a large positive set: its user records (40+ MB of random reads) join the positives' records,
@@ -424,7 +415,7 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
   // which; 0 = always, default 64M)
   int64_t pos4_from = 64LL << 20;
   if (const char* e = getenv("BPRMF_SAMPLE_POS4")) pos4_from = std::max<int64_t>(0, atoll(e));
-  if (packed && h->d_urec && !pu.empty() && (int64_t)pu.size() >= pos4_from) {
+  if (h->d_urec && !pu.empty() && (int64_t)pu.size() >= pos4_from) {
     std::vector<int2> ur(h->U);
     HIPCHK(hipMemcpy(ur.data(), h->d_urec, 8 * ur.size(), hipMemcpyDeviceToHost));
     std::vector<int4> p4(pu.size());
@@ -435,7 +426,7 @@ int bprmf_set_train_ex(bprmf_handle* h, const int32_t* users, const int32_t* ite
     }
     if (int r = dalloc(&h->d_pos4, (int64_t)p4.size())) return r;
     HIPCHK(hipMemcpy(h->d_pos4, p4.data(), 16 * p4.size(), hipMemcpyHostToDevice));
-  } else if (packed && !pu.empty()) {
+  } else if (!pu.empty()) {
     std::vector<int2> p2(pu.size());
     for (size_t k = 0; k < pu.size(); ++k) p2[k] = make_int2(pu[k], pi[k]);
     if (int r = dalloc(&h->d_pos2, (int64_t)p2.size())) return r;
@@ -508,10 +499,14 @@ static double host_seconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// diagnostic (BPRMF_HOST_TRACE=1): host timestamps of a thread's first calls' phases, to stderr
+// diagnostic build only (-DBPRMF_HOST_TRACE, tools/gpu/host_trace.sh): host timestamps of a
+// thread's first calls' phases, to stderr
 static bool trace_on() {
-  static const bool on = getenv("BPRMF_HOST_TRACE") != nullptr;  // initialised once, thread-safe
-  return on;
+#ifdef BPRMF_HOST_TRACE
+  return true;
+#else
+  return false;
+#endif
 }
 static thread_local int g_trace_calls = 0;
 static thread_local double g_trace_t[8];
@@ -573,12 +568,7 @@ int bprmf::wait_mapped_seq(bprmf_handle* h, size_t off, uint64_t seq) {
 int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t steps) {
   const bool ran = !h->loss_pending;
   h->loss_pending = false;
-  h->fold_req = false;
-  if (h->fold_seq) {  // the call's last K2 wrote the status block and this sequence number
-    const uint64_t seq = h->fold_seq;
-    h->fold_seq = 0;
-    if (int r = wait_mapped_seq(h, kSeqEndOff, seq)) return r;
-  } else if (h->call_slots) {
+  if (h->call_slots) {
     HIPCHK(hipMemcpyAsync(h->h_status, h->d_status, 16 + sizeof(double) * kLossSlots,
                           hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -593,7 +583,6 @@ int bprmf::end_call(bprmf_handle* h, bprmf_stats* st, int64_t triplets, int64_t 
   if (e) {
     HIPCHK(hipMemsetAsync(h->d_err, 0, sizeof(int32_t), h->stream));
     if (e & 16) HIPCHK(clear_batches(h));
-    h->persist_t = -1;  // a persistent launch may have given up part-way: its flags are reset
     if (e & 4) return fail(BPRMF_E_HIP, "sharded exchange timed out: a peer stopped signalling");
     if (e & 8) return fail(BPRMF_E_HIP, "fused step: a row's owner never published it (wait timed out)");
     if (e & 16) return fail(BPRMF_E_HIP, "batch builder: an item part never published its counts (wait timed out)");
@@ -666,12 +655,6 @@ extern "C" int bprmf_debug_fail_build(bprmf_handle* h) {
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(bb.view(k).meta + kMetaDead), kDeadMark, 1, h->stream));
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_err, kErrBuild, 1, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  return 0;
-}
-
-extern "C" int bprmf_debug_persist_grid(bprmf_handle* h, int32_t* workgroups) {
-  if (!h || !workgroups) return fail(BPRMF_E_INVALID, "null argument");
-  *workgroups = h->persist_total;
   return 0;
 }
 
@@ -779,15 +762,11 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
     return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
   }
   // the executable graph's device-side setup now (set_train) rather than inside its first replay
-  // (BPRMF_GRAPH_UPLOAD=0: lazily, A/B)
-  const char* up = getenv("BPRMF_GRAPH_UPLOAD");
-  if (!(up && up[0] == '0')) {
-    const hipError_t eu = hipGraphUpload(out->exec, h->stream);
-    if (eu != hipSuccess) {  // the caller never keeps a failed graph: destroy it here
-      hipGraphExecDestroy(out->exec);
-      out->exec = nullptr;
-      return fail(BPRMF_E_HIP, "step graph upload: %s", hipGetErrorString(eu));
-    }
+  const hipError_t eu = hipGraphUpload(out->exec, h->stream);
+  if (eu != hipSuccess) {  // the caller never keeps a failed graph: destroy it here
+    hipGraphExecDestroy(out->exec);
+    out->exec = nullptr;
+    return fail(BPRMF_E_HIP, "step graph upload: %s", hipGetErrorString(eu));
   }
   return 0;
 }
@@ -833,44 +812,6 @@ static int run_units(bprmf_handle* h, int64_t n, int64_t* base) {
   return 0;
 }
 
-// Opt-in (BPRMF_STATUS_FOLD=1; read per call): measured slower at the driver's settings (20-step
-// calls 13.3-13.9 against 12.9-13.0 us/step, profiles/r05_ab_status_fold.txt): the call then
-// returns while its last K2 still runs, and the caller's device synchronisation that follows
-// (torch.cuda.synchronize in bench.py) waits longer for it than the host's spin on the status
-// word of a k_status_out launch does.
-static bool fold_enabled() {
-  const char* e = getenv("BPRMF_STATUS_FOLD");
-  return e && e[0] == '1';
-}
-
-// BPRMF_PERSIST=1 runs each chunk as ONE persistent launch (step.hip k_persist_steps; read per
-// call).  Opt-in: bitwise equal to the fused launches but measured 1.6x slower per step (this
-// form: 15.5 against 9.5 us; earlier flag layouts 13.6-20.7, profiles/r05_persist/), see
-// DESIGN.md §5 "Round 5".
-static bool persist_enabled() {
-  const char* e = getenv("BPRMF_PERSIST");
-  return e && e[0] == '1';
-}
-
-// the persistent step's flags and grid, probed once per handle: 0 when its workgroups would not
-// all be resident at once (or the item table is too small for the capped K2 grid it assumes)
-static int persist_ready(bprmf_handle* h) {
-  if (h->persist_total < 0) {
-    const int B = h->cfg.batch_size;
-    h->persist_total = 0;
-    if (h->Q.rows >= 2LL * B) {
-      const int total = persist_grid(h->geom, B, true, &h->persist_k2, &h->persist_k1);
-      if (total > 0) {
-        // two int32 arrays, each padded to whole 16-byte groups (the pollers read 4 flags per lane)
-        const int64_t words = 4 * ((h->persist_k1 + 3) / 4 + (h->persist_k2 + 3) / 4);
-        if (int r = dalloc(&h->d_pflags, words)) return r;
-        h->persist_total = total;
-      }
-    }
-  }
-  return 0;
-}
-
 // the chunk's nb steps (cursor {h->t, 0}, batches built)
 static int launch_steps(bprmf_handle* h, int64_t nb) {
   int64_t base = 0;
@@ -879,41 +820,11 @@ static int launch_steps(bprmf_handle* h, int64_t nb) {
   const BatchView v0 = BatchBuf{h->d_batch, B}.view(0);
   const int64_t stride = BatchBuf::stride_for(B);
   const StepBufs sb = step_bufs(h);
-  if (persist_enabled() && nb >= 2) {
-    if (int r = persist_ready(h)) return r;
-    if (h->persist_total > 0 && nb < INT32_MAX) {
-      // the flags must all read h->t now (they do after an uninterrupted persistent chunk ending
-      // there; otherwise they are set: steps run another way, or a failed launch left them)
-      const int64_t words = 4 * ((h->persist_k1 + 3) / 4 + (h->persist_k2 + 3) / 4);
-      if (h->persist_t != h->t)
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)h->d_pflags, h->t, words, h->stream));
-      h->persist_t = h->t + nb;
-      HIPCHK(persist_step(h->geom, v0, stride, B, h->P, h->Q, h->hp, h->d_tbase, (int)nb, sb, h->d_loss,
-                          h->d_err, h->d_pflags, h->d_pflags + 4 * ((h->persist_k1 + 3) / 4), h->stream));
-      h->fold_req = false;
-      return 0;
-    }
-  }
   HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, 0, nullptr, nullptr, nullptr,
                    nullptr, h->stream, PeerWait{}, stride, &sb));
   if (int r = run_units(h, nb - 1, &base)) return r;
-  // BPRMF_STATUS_FOLD=1: the call's last K2 publishes the call's status itself (no k_status_out
-  // launch and boundary; measured slower, see fold_enabled)
-  StatusFold sf;
-  const StatusFold* sfp = nullptr;
-  if (h->fold_req && h->d_fold_cnt && !h->call_slots && fold_enabled()) {
-    sf.cnt = h->d_fold_cnt;
-    sf.host = reinterpret_cast<uint64_t*>(h->h_status_dev);
-    sf.dstatus = reinterpret_cast<const uint64_t*>(h->d_status);
-    sf.seq_dst = reinterpret_cast<uint64_t*>(h->h_status_dev + kSeqEndOff);
-    sf.seq = ++h->status_seq;
-    sf.nslots = kSegLossSlots;
-    sfp = &sf;
-    h->fold_seq = sf.seq;
-  }
-  h->fold_req = false;
   HIPCHK(item_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, (int)(nb - 1 - base), nullptr,
-                   nullptr, nullptr, h->stream, nullptr, h->d_loss, stride, &sb, sfp));
+                   nullptr, nullptr, h->stream, nullptr, h->d_loss, stride, &sb));
   return 0;
 }
 
@@ -967,16 +878,6 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     // own (hogwild.hip); the loss goes to the segmented path's kSegLossSlots slots
     if (int z = loss_zero_slots(h)) HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * z, h->stream));
     const SamplerArgs sa = sampler_args(h);
-    const char* pre = getenv("BPRMF_HOGWILD_PRESAMPLE");  // A/B: k_sample first, then replay
-    if (!ru && pre && pre[0] == '1') {
-      if (int r = ensure_trip(h, n)) return r;
-      int32_t* tu = h->d_trip;
-      HIPCHK(sample(sa, epoch, first_slot, n, tu, tu + h->trip_cap, tu + 2 * h->trip_cap, h->d_err,
-                    h->stream));
-      ru = tu;
-      ri = tu + h->trip_cap;
-      rj = tu + 2 * h->trip_cap;
-    }
     {
       hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
       if (ea) HIPCHK(hipEventRecord(ea, h->stream));
@@ -1045,14 +946,12 @@ static int run_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_slot, int64_
     // the step kernels and their gaps; per-kernel splits come from rocprofv3)
     hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
     if (ea) HIPCHK(hipEventRecord(ea, h->stream));
-#ifdef BPRMF_BUILD_STAMPS
+#if defined(BPRMF_BUILD_STAMPS) && defined(BPRMF_DIAG_BUILD_ONLY)
     // diagnostic builder builds (tools/ubench_build.py) may write wrong batches on purpose: the
     // step kernels must never index rows with them
-    if (getenv("BPRMF_DIAG_BUILD_ONLY")) {
-      h->t += (int32_t)nb;
-      *steps_done += nb;
-      return 0;
-    }
+    h->t += (int32_t)nb;
+    *steps_done += nb;
+    return 0;
 #endif
     if (int r = launch_steps(h, nb)) return r;
     if (ea) {
@@ -1113,15 +1012,9 @@ int bprmf_train_steps(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
   trace_mark();
   if (int r = begin_call(h)) return r;
   int64_t steps = 0;
-  for (int64_t off = beg; off < end; off += chunk) {
-    h->fold_req = off + chunk >= end;  // the call's last chunk: its last K2 carries the status
-    if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps)) {
-      h->fold_req = false;
-      h->fold_seq = 0;
+  for (int64_t off = beg; off < end; off += chunk)
+    if (int r = run_chunk(h, epoch, off, std::min(chunk, end - off), nullptr, nullptr, nullptr, &steps))
       return r;
-    }
-  }
-  h->fold_req = false;
   trace_mark();
   const int rc_end = end_call(h, st, end - beg, steps);
   trace_mark();

@@ -5,10 +5,10 @@
 //   ipc       kernels write each peer's block straight into the peer's buffer (mapped with
 //             hipIpc; xGMI peer writes) and raise a per-source flag.  Per step, the owners'
 //             gather writes the rows into the requesters' landing buffers itself and K1 waits on
-//             its row flags; K2's gradients go out with one push kernel and the owners' apply
-//             waits on its gradient flags, no host in the loop.  Default (fused2): two launches
-//             per step, the owner phase beside K1 (step.hip k_dist_front) and K2 writing its
-//             gradients straight into the owners' landing buffers (k_item_step_push).
+//             its row flags; the owners' apply waits on its gradient flags, no host in the loop:
+//             two launches per step, the owner phase beside K1 (step.hip k_dist_front) and K2
+//             writing its gradients straight into the owners' landing buffers
+//             (k_item_step_push).  Ranks sharing one device: push kernels + receive copies.
 //   rccl      an RCCL communicator owned by the handle (ncclCommInitRank from a unique id the
 //             caller broadcasts); per-peer blocks move with grouped ncclSend/ncclRecv over xGMI.
 //   loopback  handles of one process exchanging through a shared table + device copies (the
@@ -213,12 +213,9 @@ struct IpcTransport final : Transport {
   int alloc_shared(bprmf_handle* h, int kind, size_t bytes, void** p) override {
     (void)h;
     *p = nullptr;
-    // landing memory (BPRMF_DIST_LANDING, A/B): uncached (default), fine-grained, or plain
-    const char* lm = getenv("BPRMF_DIST_LANDING");
-    const unsigned flags = !lm || !*lm ? hipDeviceMallocUncached
-                           : lm[0] == 'f' ? hipDeviceMallocFinegrained
-                           : lm[0] == 'p' ? hipDeviceMallocDefault : hipDeviceMallocUncached;
-    HIPCHK(hipExtMallocWithFlags(&local[kind], std::max<size_t>(bytes, 256), flags));
+    // landing memory uncached: a reader never sees a stale L2 line after a peer's xGMI write
+    // (fine-grained and plain allocations measured the same)
+    HIPCHK(hipExtMallocWithFlags(&local[kind], std::max<size_t>(bytes, 256), hipDeviceMallocUncached));
     if (copied(kind)) {
       HIPCHK(hipMalloc(&recv_base[kind], std::max<size_t>(bytes, 256)));
     } else {
@@ -237,28 +234,16 @@ struct IpcTransport final : Transport {
   // with spinning workgroups until a peer cannot run the kernel that would release them (8
   // ranks on one GPU timed out).  Shared device: every exchange is a push kernel plus a receive
   // copy (or one waiting block), and no step kernel spins.  BPRMF_DIST_FUSE=0/1 forces either
-  // (1: also at world 1, to measure what the fused forms cost on one device); BPRMF_DIST_FUSE2=1
-  // forces the two-launch form.
+  // (1: also at world 1 or on a shared device, to measure and test the fused form there).
+  // The fused form is two launches per step (step.hip k_dist_front + k_item_step_push): the
+  // owner phase beside K1, K2's gradients straight into the owners' landing buffers.  (A
+  // three-launch form, owner step / K1 / K2 + a push kernel, measured slower and was removed in
+  // round 6; a chunk whose plan has no rows to exchange, cap 0, still runs its launch sequence.)
   bool fused() const {
     if (!opened || self_exchange) return false;
     const char* e = getenv("BPRMF_DIST_FUSE");
     if (e && *e) return e[0] != '0';
-    const char* e2 = getenv("BPRMF_DIST_FUSE2");
-    if (e2 && *e2 && e2[0] != '0') return true;
     return world > 1 && !shared_device;
-  }
-  // two launches per step (step.hip k_dist_front + k_item_step_push): the owner phase beside K1,
-  // K2's gradients straight into the owners' landing buffers (BPRMF_DIST_FUSE2=0: the owner step,
-  // K1, K2 and the push kernel as separate launches)
-  // Off when ranks share a device: a launch's K1 workgroups spin on every rank's row flag, and
-  // with several ranks' launches on one GPU the spinning workgroups can hold the CUs a peer's
-  // owner workgroups need (measured: 4 ranks on one MI355X time out).  One rank per GPU (the
-  // 8-GPU node) has no such coupling: each launch's owner workgroups are dispatched first.
-  bool fused2() const {
-    if (!fused()) return false;
-    const char* e = getenv("BPRMF_DIST_FUSE2");
-    if (e && *e) return e[0] != '0';
-    return !shared_device;
   }
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
   void* peer_landing(int kind, int p) const { return remote[kind][p]; }
@@ -619,7 +604,7 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
 
 static int ensure_aplan(bprmf_handle* h, int par, int64_t n, int cap) {
   DistState* d = h->dist;
-  const int64_t ap = aplan_words(n, h->cfg.world, cap);  // rec, gdep, gfree, pflag
+  const int64_t ap = aplan_words(n, h->cfg.world, cap);  // rec, gdep, gfree
   if (ap <= d->aplan_n[par]) return 0;
   if (d->aplan[par]) HIPCHK(hipFree(d->aplan[par]));
   d->aplan[par] = nullptr;
@@ -743,7 +728,7 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
     }
   }
   const PeerWait pw{fused ? ipc->my_flags(X_ROWS) : nullptr, W, (int)R, h->d_err};
-  if (fused && ipc->fused2() && cap > 0) {
+  if (fused && cap > 0) {
     // two launches per step: [owner phase of step k | K1(k)], [K2(k) -> owners' landing buffers]
     const int64_t WC0 = (int64_t)W * cap;
     OwnerArgs oa;
@@ -995,8 +980,7 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
     d->tr->self_exchange = se;
     if (r) return r;
     HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, aplan + n * W * (int64_t)cap * W,
-                           aplan + 2 * n * W * (int64_t)cap * W, h->stream,
-                           aplan + 2 * n * W * (int64_t)cap * W + n * W * (int64_t)cap));
+                           aplan + 2 * n * W * (int64_t)cap * W, h->stream));
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;
   if (ea) HIPCHK(hipEventRecord(ea, h->stream));

@@ -78,120 +78,6 @@ static __device__ __forceinline__ int find_row(const int32_t* __restrict__ list,
 // searches side by side (three binary searches a lane: step k-1, k and k+1 of peer q's list, one
 // dependent chain each) instead of one thread walking ~3W searches in sequence; the group's "any
 // peer" answers (the row was applied last step; a lower peer requests it too) are ballots.
-// The plan by list pairs (BPRMF_PLAN_PAIRS=1, opt-in): one workgroup per (step k, owner list p, peer q, step k + dk,
-// dk = -1, 0, +1) holds peer q's list of step k + dk in LDS, and every position of p's list of
-// step k finds its row there with a binary search in LDS (no dependent global loads): dk = 0
-// writes aplan's entry q, dk = +1 gdep's entry q, dk = -1 a found flag (pflag).  A second kernel,
-// one thread per position, turns the flags and the lower peers' entries into gfree and the
-// leader mark aplan[..][0] = -2.  Same plan as the forms below, entry for entry, except the
-// entries 1.. of a non-leader position (never read: the owner kernels skip it on entry 0).
-__global__ __launch_bounds__(256) void k_plan_pairs(const int32_t* __restrict__ ids_recv, int64_t n,
-                                                    int world, int cap, int32_t* __restrict__ aplan,
-                                                    int32_t* __restrict__ gdep,
-                                                    int32_t* __restrict__ pflag) {
-  extern __shared__ int32_t s_list[];
-  int64_t b = blockIdx.x;
-  const int dk = (int)(b % 3) - 1;
-  b /= 3;
-  const int q = (int)(b % world);
-  b /= world;
-  const int p = (int)(b % world);
-  const int64_t k = b / world;
-  const int64_t kk = k + dk;
-  const bool has = kk >= 0 && kk < n;
-  const bool self = dk == 0 && q == p;
-  if (has && !self) {
-    const int32_t* src = ids_recv + ((int64_t)q * n + kk) * cap;
-    for (int i = threadIdx.x; i < cap; i += blockDim.x) s_list[i] = src[i];
-  }
-  __syncthreads();
-  const int32_t* mine = ids_recv + ((int64_t)p * n + k) * cap;
-  for (int idx = threadIdx.x; idx < cap; idx += blockDim.x) {
-    const int32_t row = mine[idx];
-    int pos = -1;
-    if (row >= 0 && has) {
-      if (self) {
-        pos = idx;
-      } else {
-        int lo = 0, hi = cap;  // first position of row (lists ascending, -1 pads compare last)
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if ((uint32_t)s_list[mid] < (uint32_t)row) lo = mid + 1; else hi = mid;
-        }
-        pos = lo < cap && s_list[lo] == row ? lo : -1;
-      }
-    }
-    const int64_t x = (k * world + p) * cap + idx;
-    if (dk == 0)
-      aplan[x * world + q] = pos < 0 ? -1 : q * cap + pos;
-    else if (dk > 0)
-      gdep[x * world + q] = pos;
-    else
-      pflag[x * world + q] = pos >= 0;
-  }
-}
-
-__global__ void k_plan_lead(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
-                            int32_t* __restrict__ aplan, const int32_t* __restrict__ pflag,
-                            int32_t* __restrict__ gfree) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= n * world * (int64_t)cap) return;
-  const int idx = (int)(x % cap);
-  const int p = (int)((x / cap) % world);
-  const int64_t k = x / ((int64_t)cap * world);
-  int32_t* rec = aplan + x * world;
-  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
-  if (row < 0) {
-    rec[0] = -2;
-    gfree[x] = 0;
-    return;
-  }
-  bool applied = false, lower = false;
-  for (int q = 0; q < world; ++q) {
-    applied |= pflag[x * world + q] != 0;
-    lower |= q < p && rec[q] >= 0;
-  }
-  gfree[x] = applied ? 0 : 1;
-  if (lower) rec[0] = -2;
-}
-
-// (BPRMF_PLAN_LANES=0, A/B: the one-thread-per-position form, every peer's searches in sequence)
-__global__ void k_owner_plan_seq(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
-                                 int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
-                                 int32_t* __restrict__ gfree) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= n * world * (int64_t)cap) return;
-  const int idx = (int)(x % cap);
-  const int p = (int)((x / cap) % world);
-  const int64_t k = x / ((int64_t)cap * world);
-  int32_t* rec = aplan + x * world;
-  int32_t* dep = gdep + x * world;
-  for (int q = 0; q < world; ++q) dep[q] = -1;
-  const int32_t row = ids_recv[((int64_t)p * n + k) * cap + idx];
-  gfree[x] = 0;
-  if (row < 0) {
-    rec[0] = -2;
-    return;
-  }
-  bool free_row = true;
-  if (k > 0)
-    for (int q = 0; q < world && free_row; ++q)
-      if (find_row(ids_recv + ((int64_t)q * n + k - 1) * cap, cap, (uint32_t)row) >= 0) free_row = false;
-  gfree[x] = free_row ? 1 : 0;
-  for (int q = 0; q < p; ++q)
-    if (find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row) >= 0) {
-      rec[0] = -2;
-      return;
-    }
-  for (int q = 0; q < world; ++q) {
-    int pos = -1;
-    if (q == p) pos = idx;
-    else if (q > p) pos = find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row);
-    rec[q] = pos < 0 ? -1 : q * cap + pos;
-    if (k + 1 < n) dep[q] = find_row(ids_recv + ((int64_t)q * n + k + 1) * cap, cap, (uint32_t)row);
-  }
-}
-
 __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
                              int gshift, int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
                              int32_t* __restrict__ gfree) {
@@ -480,22 +366,8 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
 }
 
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           int32_t* gdep, int32_t* gfree, hipStream_t s, int32_t* pflag) {
+                           int32_t* gdep, int32_t* gfree, hipStream_t s) {
   if (n <= 0 || cap <= 0) return hipSuccess;
-  const char* pp = getenv("BPRMF_PLAN_PAIRS");  // opt-in until measured on the GPU
-  if (pflag && pp && pp[0] == '1') {
-    k_plan_pairs<<<(unsigned)(n * world * world * 3), 256, sizeof(int32_t) * (size_t)cap, s>>>(
-        ids_recv, n, world, cap, aplan, gdep, pflag);
-    k_plan_lead<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap,
-                                                                       aplan, pflag, gfree);
-    return hipGetLastError();
-  }
-  const char* pl = getenv("BPRMF_PLAN_LANES");
-  if (pl && pl[0] == '0') {
-    k_owner_plan_seq<<<blocks_for(n * world * (int64_t)cap), kBlock, 0, s>>>(ids_recv, n, world, cap,
-                                                                          aplan, gdep, gfree);
-    return hipGetLastError();
-  }
   int gshift = 0;
   while ((1 << gshift) < world) ++gshift;  // world <= kMaxWorld = 16
   k_owner_plan<<<blocks_for((n * world * (int64_t)cap) << gshift), kBlock, 0, s>>>(

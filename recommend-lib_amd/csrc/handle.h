@@ -106,11 +106,6 @@ struct bprmf_handle {
   float* d_qsum = nullptr;      // [I][ld] the overlapped all-reduce's result (RCCL, out of place)
   bool fused = true;           // chunks run K1, fused K2+K1 launches, K2 (BPRMF_FUSED=0: K1+K2 pairs)
   int32_t* d_tbase = nullptr;  // step cursor {t, batch}: t before the chunk (kernels read it here)
-  // the persistent step (step.hip k_persist_steps, BPRMF_PERSIST): per-workgroup progress flags
-  // [K1 workgroups][K2 workgroups] and the launch's workgroup count (0: not resident, fused)
-  int32_t* d_pflags = nullptr;
-  int persist_k1 = 0, persist_k2 = 0, persist_total = -1;  // -1: not probed yet
-  int64_t persist_t = -1;  // every flag holds this step (mod 256); -1: unknown, reset before use
   int64_t plan_steps = 0;      // batches of the current sharded plan
   int64_t trip_cap = 0;
   // misc device scalars
@@ -119,11 +114,6 @@ struct bprmf_handle {
   unsigned char* h_status = nullptr;      // pinned, mapped host mirror
   unsigned char* h_status_dev = nullptr;  // its device address (k_status_out writes there)
   uint64_t status_seq = 0;                // sequence number of the last call's status block
-  // the call's status folded into its last K2 (StatusFold): fold_req set by the entry point for
-  // its last chunk, fold_seq != 0 once that launch carries the status (end_call then only waits)
-  int32_t* d_fold_cnt = nullptr;
-  bool fold_req = false;
-  uint64_t fold_seq = 0;
   double* d_loss = nullptr;               // = d_status + 16
   int32_t* d_err = nullptr;               // = d_status
   bool loss_pending = false;    // a call began: the loss slots are zeroed before the first step
@@ -175,8 +165,8 @@ struct ProfScope {
 };
 int ensure_trip(bprmf_handle* h, int64_t n);
 int ensure_seg(bprmf_handle* h, int64_t n_batches);
-StepBufs step_bufs(const bprmf_handle* h);
-LocalArgs local_args(const bprmf_handle* h);  // semantics LOCAL: hot items, replicas, lookups  // the single-GPU step buffers (both halves, pend)
+StepBufs step_bufs(const bprmf_handle* h);    // the single-GPU step buffers (both halves, pend)
+LocalArgs local_args(const bprmf_handle* h);  // semantics LOCAL: hot items, replicas, lookups
 int ensure_grad(bprmf_handle* h);
 bool seg_mode(const bprmf_handle* h);
 // a sampled chunk of nb batches draws its triplets with the grid-wide sampler before the builder

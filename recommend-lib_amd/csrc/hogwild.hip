@@ -60,13 +60,6 @@ static __device__ __forceinline__ void hw_st4(float* p, float4 v) {
   const v4f x = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
 }
-// p += s * g, four no-return f32 atomic adds (executed at the memory side)
-static __device__ __forceinline__ void hw_add4(float* p, float4 g, float s) {
-  atomicAdd(p, s * g.x);
-  atomicAdd(p + 1, s * g.y);
-  atomicAdd(p + 2, s * g.z);
-  atomicAdd(p + 3, s * g.w);
-}
 static __device__ __forceinline__ void hw_st_word(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -132,10 +125,9 @@ static __device__ __forceinline__ int32_t hot_probe(const LocalArgs& la, int32_t
 template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
 static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
                                                int32_t mi, int32_t mj, const Table& P,
-                                               const Table& Q, int ld, int sub, int gw, int fl,
+                                               const Table& Q, int ld, int sub, int gw,
                                                int32_t mhi = -1, int32_t mhj = -1,
                                                const float* repx = nullptr) {
-  const bool nt = fl & 1, noload = fl & 2;
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
@@ -145,21 +137,15 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
     R.hi[r] = LOCAL ? __shfl(mhi, src & 63) : -1;
     R.hj[r] = LOCAL ? __shfl(mhj, src & 63) : -1;
     R.ok[r] = (SERIAL ? gw == 0 : true) && src < cnt && R.uu[r] >= 0;
-    if (R.ok[r] && !noload) {
+    if (R.ok[r]) {
       const float* pr = P.W + (int64_t)R.uu[r] * ld + 4 * sub;
       const float* qi = (LOCAL && R.hi[r] >= 0 ? repx + (int64_t)R.hi[r] * ld : Q.W + (int64_t)R.ii[r] * ld) + 4 * sub;
       const float* qj = (LOCAL && R.hj[r] >= 0 ? repx + (int64_t)R.hj[r] * ld : Q.W + (int64_t)R.jj[r] * ld) + 4 * sub;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        if (nt) {
-          R.pu[r][k] = hw_ld4(pr + 4 * G4 * k);
-          R.vi[r][k] = hw_ld4(qi + 4 * G4 * k);
-          R.vj[r][k] = hw_ld4(qj + 4 * G4 * k);
-        } else {
-          R.pu[r][k] = *reinterpret_cast<const float4*>(pr + 4 * G4 * k);
-          R.vi[r][k] = *reinterpret_cast<const float4*>(qi + 4 * G4 * k);
-          R.vj[r][k] = *reinterpret_cast<const float4*>(qj + 4 * G4 * k);
-        }
+        R.pu[r][k] = hw_ld4(pr + 4 * G4 * k);
+        R.vi[r][k] = hw_ld4(qi + 4 * G4 * k);
+        R.vj[r][k] = hw_ld4(qj + 4 * G4 * k);
       }
       R.su[r] = hw_ld_word(P.stamp + R.uu[r]);
       // a replica row has no stamp: it is current within its period (the merge applies the
@@ -179,15 +165,8 @@ template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
 static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base, int k0,
                                                 const Table& P, const Table& Q, const Hyper& hp,
                                                 int ld, int32_t t0, int B, int sub, int gw,
-                                                float& lacc, int fl, float* repx = nullptr) {
+                                                float& lacc, float* repx = nullptr) {
   const float lr = hp.lr, wd = hp.wd;
-  const bool nostore = fl & 4;
-  const bool plainst = fl & 8, noitems = fl & 16, nousers = fl & 32;  // diagnostic timing only
-  const bool user_wb = fl & 64;  // A/B: user rows stored write-back (plain), item rows sc1
-  // LOCAL, BPRMF_LOCAL_HOT_ATOMIC=1 (A/B): a hot replica row takes its change -lr g by f32
-  // atomic adds instead of a store of the read value minus lr g, so concurrent updates of one
-  // hot row in this XCD are all kept (a store overwrites the others' changes in flight)
-  const bool hot_atomic = LOCAL && (fl & 128);
 #pragma unroll
   for (int r = 0; r < UNR; ++r) {
     const int src = k0 + r * GPW + gw;
@@ -213,7 +192,7 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
     // whatever ok[] says (inactive groups carry zeros)
     di = group_sum<G4>(R.ok[r] ? di : 0.f);
     dj = group_sum<G4>(R.ok[r] ? dj : 0.f);
-    if (!R.ok[r] || nostore) continue;
+    if (!R.ok[r]) continue;
     const float x = di - dj;
     const float c = 1.0f / (1.0f + expf(x));  // sigmoid(-x) = -dL/dx
     if (sub == 0) lacc += softplus(-x);       // -log sigmoid(x)
@@ -230,30 +209,15 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
       const float4 gj = make_float4(c * pu.x, c * pu.y, c * pu.z, c * pu.w);
       float4 gi = make_float4(-c * pu.x, -c * pu.y, -c * pu.z, -c * pu.w);
       if (same) gi = make_float4(gi.x + gj.x, gi.y + gj.y, gi.z + gj.z, gi.w + gj.w);
-      if (plainst) {
-        if (!nousers) *reinterpret_cast<float4*>(pr + 4 * G4 * k) = hw_sgd(pu, gu, lr, fu1 ? wd : 0.f);
-        if (!noitems) {
-          *reinterpret_cast<float4*>(qi + 4 * G4 * k) = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f);
-          if (!same) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
-        }
-        continue;
-      }
-      if (user_wb)
-        *reinterpret_cast<float4*>(pr + 4 * G4 * k) = hw_sgd(pu, gu, lr, fu1 ? wd : 0.f);
-      else if (!nousers)
-        hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
-      if (!noitems) {
-        // replica rows: written back into this XCD's L2 (plain stores), no weight-decay term
-        // (their stamps read INT32_MAX: fi1 / fj1 false); shared rows: write-through, as hogwild
-        const float4 ni = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f), nj = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
-        if (hoti && hot_atomic) hw_add4(qi + 4 * G4 * k, gi, -lr);
-        else if (hoti) *reinterpret_cast<float4*>(qi + 4 * G4 * k) = ni;
-        else hw_st4(qi + 4 * G4 * k, ni);
-        if (!same) {
-          if (hotj && hot_atomic) hw_add4(qj + 4 * G4 * k, gj, -lr);
-          else if (hotj) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = nj;
-          else hw_st4(qj + 4 * G4 * k, nj);
-        }
+      hw_st4(pr + 4 * G4 * k, hw_sgd(pu, gu, lr, fu1 ? wd : 0.f));
+      // replica rows: written back into this XCD's L2 (plain stores), no weight-decay term (their
+      // stamps read INT32_MAX: fi1 / fj1 false); shared rows: write-through, as hogwild
+      const float4 ni = hw_sgd(vi, gi, lr, fi1 ? wd : 0.f), nj = hw_sgd(vj, gj, lr, fj1 ? wd : 0.f);
+      if (hoti) *reinterpret_cast<float4*>(qi + 4 * G4 * k) = ni;
+      else hw_st4(qi + 4 * G4 * k, ni);
+      if (!same) {
+        if (hotj) *reinterpret_cast<float4*>(qj + 4 * G4 * k) = nj;
+        else hw_st4(qj + 4 * G4 * k, nj);
       }
     }
     if (sub == 0) {
@@ -279,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
                                                     const int32_t* __restrict__ ti,
                                                     const int32_t* __restrict__ tj, int64_t n,
                                                     Table P, Table Q, Hyper hp, int ld, int32_t t0,
-                                                    int B, int tpw, int fl, double* __restrict__ loss,
+                                                    int B, int tpw, double* __restrict__ loss,
                                                     int32_t* __restrict__ err, LocalArgs la = LocalArgs{},
                                                     int uw = 1) {
   constexpr int GPW = SERIAL ? 1 : 64 / G4;  // triplets per wave per round and unroll step
@@ -332,23 +296,23 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
     HwRound<S, UNR> A, Bf;
     if (SERIAL) {  // each triplet reads what the one before it stored: no prefetch
       for (int k0 = 0; k0 < cnt; k0 += STEP) {
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi, mhj, repx);
-        hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl, repx);
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
+        hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, repx);
       }
       continue;
     }
-    hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi, mhj, repx);
+    hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
     for (int k0 = 0; k0 < cnt; k0 += 2 * STEP) {
       const bool more1 = k0 + STEP < cnt, more2 = k0 + 2 * STEP < cnt;
       if (more1)
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl, mhi,
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi,
                                                 mhj, repx);
-      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, fl, repx);
+      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, repx);
       if (!more1) break;
       if (more2)
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, fl,
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw,
                                                 mhi, mhj, repx);
-      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc, fl,
+      hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc,
                                                repx);
     }
   }
@@ -556,8 +520,8 @@ hipError_t dp_sum(const DpSrcs& src, int world, float* out, int64_t n, hipStream
 
 // the geometries of the hogwild launch: by default half the rows' lanes per triplet and twice the
 // stripes for 32- and 64-lane rows (d = 65..256: twice the triplets, so twice the rows, in flight
-// per wave; local mode 1.56 -> 1.61e9 triplets/s at the ml-20m shape); BPRMF_HOGWILD_NARROW=0:
-// the rows' own (G4, S) (A/B)
+// per wave; local mode 1.56 -> 1.61e9 triplets/s at the ml-20m shape against the rows' own
+// (G4, S), round 4)
 #define HW_DISPATCH(geom, BODY)                                     \
   switch ((geom).G4 * 10 + (geom).S) {                             \
     case 11: { constexpr int G4_ = 1, S_ = 1; BODY; } break;       \
@@ -581,12 +545,8 @@ static bool hw_serial() {
 }
 
 // triplets per wave: enough waves to fill the chip for short chunks (>= ~2048 waves), 64 (one per
-// lane) for long ones; BPRMF_HOGWILD_TPW overrides (A/B)
+// lane) for long ones
 static int hw_tpw(int64_t n) {
-  if (const char* e = getenv("BPRMF_HOGWILD_TPW")) {
-    const int v = atoi(e);
-    if (v == 8 || v == 16 || v == 32 || v == 64) return v;
-  }
   if (n >= 64LL * 4096) return 64;
   if (n >= 32LL * 2048) return 32;
   return 16;
@@ -599,8 +559,7 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
   if (n <= 0) return hipSuccess;
   if (uw < 1) return hipErrorInvalidValue;
   Geom g = g0;
-  const char* nw = getenv("BPRMF_HOGWILD_NARROW");
-  if (!(nw && nw[0] == '0') && (g.G4 == 32 || g.G4 == 64) && g.S == 1) {
+  if ((g.G4 == 32 || g.G4 == 64) && g.S == 1) {
     g.G4 /= 2;
     g.S = 2;
   }
@@ -614,33 +573,16 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
   // so a row sees about one other update in flight at a time whatever the table size.  Measured
   // (ml-100k, d=32: 943 x 1,682 rows): ~1k in flight trains like the exact step, ~8k (64
   // workgroups) barely trains (lost updates on every row); ml-20m (26,744 items) at the full grid
-  // (~24k resident) matches the exact step's HR@10.  BPRMF_HOGWILD_WINDOW overrides (triplets),
-  // BPRMF_HOGWILD_BLOCKS caps the grid directly (A/B).
-  // Local mode, BPRMF_HOGWILD_LOCAL_WX = k: k times that window (A/B; late round 4, k = 4: the
-  // ml-20m shape 1.63 -> 1.71e9 triplets/s with HR@10 unchanged, but ml-100k's final training
-  // loss 58.6k -> 80k: the window's bound matters for small tables).
+  // (~24k resident) matches the exact step's HR@10.  BPRMF_HOGWILD_WINDOW overrides (triplets:
+  // the speed / quality frontier of DESIGN.md §5c is measured along it).
   {
     int64_t window = std::min<int64_t>(P.rows, Q.rows);
-    if (const char* wx = getenv("BPRMF_HOGWILD_LOCAL_WX"))
-      if (lap) window *= std::max(1, atoi(wx));
     if (const char* e = getenv("BPRMF_HOGWILD_WINDOW")) window = std::max<int64_t>(1, atoll(e));
     const int64_t per_block = (int64_t)wpb * (64 / g.G4) * 2 * kHwUnroll;  // two rounds in flight
     const int64_t cap = std::max<int64_t>(1, (window + per_block - 1) / per_block);
     if (blocks > cap) blocks = cap;
   }
-  if (const char* e = getenv("BPRMF_HOGWILD_BLOCKS")) {
-    const int64_t cap = atoll(e);
-    if (cap > 0 && blocks > cap) blocks = cap;
-  }
   const unsigned threads = serial ? 64 : kBlock;
-  // row loads past L1 (nt) by default; BPRMF_HOGWILD_PLAIN=1: plain loads (A/B)
-  const char* pl = getenv("BPRMF_HOGWILD_PLAIN");
-  int fl = (pl && pl[0] == '1') ? 0 : 1;
-  // diagnostic timing only (wrong results): bit 1 = no row loads, bit 2 = no row stores, bit 3 =
-  // plain (write-back) row stores, bit 4 = no item row stores, bit 5 = no user row stores
-  if (const char* e = getenv("BPRMF_HOGWILD_DIAG")) fl |= (atoi(e) & 126);
-  if (const char* e = getenv("BPRMF_LOCAL_HOT_ATOMIC"))
-    if (e[0] == '1') fl |= 128;
   SamplerArgs a{};
   if (sa) a = *sa;
   if (lap) {  // semantics "local": the hot items in per-XCD replicas
@@ -648,32 +590,32 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
     HW_DISPATCH(g, ({
       if (serial && sa)
         k_hogwild<G4_, S_, true, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
-                                                                  hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
+                                                                  hp, g.ld, t0, B, tpw, loss, err, la, uw);
       else if (serial)
         k_hogwild<G4_, S_, false, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
-                                                                   hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
+                                                                   hp, g.ld, t0, B, tpw, loss, err, la, uw);
       else if (sa)
         k_hogwild<G4_, S_, true, false, true><<<(unsigned)blocks, threads, 0, s>>>(
-            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, la, uw);
       else
         k_hogwild<G4_, S_, false, false, true><<<(unsigned)blocks, threads, 0, s>>>(
-            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, la, uw);
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, la, uw);
     }));
     return hipGetLastError();
   }
   HW_DISPATCH(g, ({
     if (serial && sa)
       k_hogwild<G4_, S_, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                          g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
+                                                          g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
     else if (serial)
       k_hogwild<G4_, S_, false, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
-                                                           g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
+                                                           g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
     else if (sa)
       k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
     else
       k_hogwild<G4_, S_, false, false><<<(unsigned)blocks, threads, 0, s>>>(
-          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, fl, loss, err, LocalArgs{}, uw);
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
   }));
   return hipGetLastError();
 }

@@ -112,7 +112,7 @@ int runner_geom(int64_t batch, int64_t item_num, int world, int ld, int64_t chun
 }
 
 int64_t aplan_words(int64_t n, int world, int cap) {
-  return n * world * (int64_t)std::max(cap, 1) * (3LL * world + 1);
+  return n * world * (int64_t)std::max(cap, 1) * (2LL * world + 1);
 }
 
 int exchange_capacity(int raw, int S, bool graph) {

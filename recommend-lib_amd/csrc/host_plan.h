@@ -59,8 +59,7 @@ struct RunnerGeom {
 };
 int runner_geom(int64_t batch, int64_t item_num, int world, int ld, int64_t chunk_steps,
                 RunnerGeom* g);
-// int32 words of one parity's apply plan: aplan + gdep [n][W][cap][W] each, gfree [n][W][cap],
-// and the list-pair form's flags [n][W][cap][W]
+// int32 words of one parity's apply plan: aplan + gdep [n][W][cap][W] each, gfree [n][W][cap]
 int64_t aplan_words(int64_t n, int world, int cap);
 // The exchange capacity a chunk runs with: the agreed maximum request count `raw`, checked
 // against the slot stride S, and (graph-captured chunks) rounded up to 64 rows so few distinct

@@ -47,9 +47,13 @@ struct bprmf_dataset {
 
 namespace {
 
-// BPRMF_INGEST_TIMING=1: phase times of bprmf_dataset_load on stderr
+// diagnostic build only (-DBPRMF_INGEST_TIMING): phase times of bprmf_dataset_load on stderr
 struct PhaseClock {
-  bool on = getenv("BPRMF_INGEST_TIMING") != nullptr;
+#ifdef BPRMF_INGEST_TIMING
+  bool on = true;
+#else
+  bool on = false;
+#endif
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void mark(const char* what) {
     if (!on) return;

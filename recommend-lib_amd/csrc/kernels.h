@@ -238,38 +238,16 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
 // loss != null: one more workgroup adds the step's loss, sum of log(1 + e^-x) over the x that K1
 // x K1 left in xloss, to loss[0 .. ceil(B / 256)) (one slot per loss workgroup, fixed order;
 // at most kSegLossSlots slots)
-// The call's status folded into its last K2: each loss workgroup stores its
-// final slot into the mapped host block and arrives on `cnt`; the last of the lb arrivals copies
-// the error words and the unused slots, resets `cnt` and stores `seq` (what k_status_out does in
-// a launch of its own).  host / seq_dst: mapped host memory (device addresses).
-struct StatusFold {
-  int32_t* cnt = nullptr;            // arrivals, 0 between calls
-  uint64_t* host = nullptr;          // {err word, dist word, loss slots...} as k_status_out writes
-  const uint64_t* dstatus = nullptr; // the device status block it mirrors
-  uint64_t* seq_dst = nullptr;
-  uint64_t seq = 0;
-  int nslots = 0;                    // loss slots mirrored (kSegLossSlots)
-};
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss = nullptr,
-                     double* loss = nullptr, int64_t bstride = 0, const StepBufs* sb = nullptr,
-                     const StatusFold* sf = nullptr);
+                     double* loss = nullptr, int64_t bstride = 0, const StepBufs* sb = nullptr);
 // (sb != null: its buffers replace contrib / ugrad / xloss)
 // K2 of step t = tbase[0] + step + 1 on batch tbase[1] + step, and K1 of step t + 1 on the next
 // batch, in one launch (bv0: batch 0's view; single GPU, sb with both halves and pend arrays)
 hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
                       const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
                       double* loss, int32_t* err, hipStream_t s);
-// the chunk's n steps (steps tbase[0] + 1 .. + n on batches tbase[1] ..) in ONE launch of resident
-// workgroups (step.hip k_persist_steps); f1 / f2: progress flags of K1 / K2 workgroups (k1_blocks
-// and k2_blocks int32, each array 16-byte aligned and padded to 4; they hold step numbers and
-// must all read the chunk's first step - 1 when it starts).  persist_grid: the
-// launch's workgroup count, 0 when they would not all be resident at once.
-int persist_grid(const Geom& g, int B, bool loss, int* k2_blocks, int* k1_blocks);
-hipError_t persist_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
-                        const Hyper& hp, const int32_t* tbase, int n, const StepBufs& sb, double* loss,
-                        int32_t* err, int32_t* f1, int32_t* f2, hipStream_t s);
 int item_long_blocks(int B);
 // relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
 // sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s
@@ -356,9 +334,8 @@ hipError_t max_vals(const int32_t* vals, int world, int32_t* out, hipStream_t s)
 hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s);
 hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
                          hipStream_t s);
-// pflag: [n][W][cap][W] scratch of the list-pair form (null: the one-kernel forms)
 hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           int32_t* gdep, int32_t* gfree, hipStream_t s, int32_t* pflag = nullptr);
+                           int32_t* gdep, int32_t* gfree, hipStream_t s);
 // ---- the fused sharded step over the IPC transport (step.hip; two launches per step) ----
 // K2 whose per-slot gradients go straight to the owners: slot s of owner p = s / S lands at
 // dst[p] + (s % S) * ld; once every workgroup's stores are acknowledged the launch's last

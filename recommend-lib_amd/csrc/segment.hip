@@ -1323,8 +1323,7 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   // the trec flag bits 30-31 need item ids below 2^30
   const char* k1e = getenv("BPRMF_K1_ITEMS");
   const int k1_items = (!slots && i_rows < (1LL << 30) && !(k1e && k1e[0] == '0')) ? 1 : 0;
-  const char* w1e = getenv("BPRMF_BUILD_W1");  // =0: the generic kernel at world 1 too (A/B)
-  const bool w1 = world == 1 && !slots && a.world == 1 && !(w1e && w1e[0] == '0');
+  const bool w1 = world == 1 && !slots && a.world == 1;  // one rank: no owner divisions
 #define BPRMF_BUILD(IPT_, BUCKET_, W1_)                                                          \
   k_build_batches<IPT_, BUCKET_, W1_><<<(unsigned)n_batches, kBuildThreads, 0, s>>>(               \
       a, epoch, first_slot, n_slots, B, ru, ri, rj, u_rows, i_rows, world, iloc, slots ? 1 : 0,  \
@@ -1335,8 +1334,8 @@ hipError_t build_batches(const SamplerArgs& a, uint32_t epoch, int64_t first_slo
   const bool split = (w1 || slots) && ru && B >= kItemParts * kXchWords + kItemParts + 2 &&
                      B <= kBuildThreads * 4 && !radix && !(spe && spe[0] == '0');
   // the item parts skip the user sort when a (side, user, slot) tie word holds the user rows
-  const char* upe = getenv("BPRMF_SPLIT_UPOS");
-  const int fast_parts = (1 + ub + kTieSlotBits <= 32 && B % 4 == 0 && !(upe && upe[0] == '0')) ? 1 : 0;
+  // (else, for very large user tables, every part sorts the batch by user itself)
+  const int fast_parts = (1 + ub + kTieSlotBits <= 32 && B % 4 == 0) ? 1 : 0;
   // sample_first: ru/ri/rj are staging arrays for slots first_slot .. first_slot + n_slots; the
   // split builder samples them itself (BPRMF_SPLIT_SAMPLE=0: k_sample first, A/B), any other
   // build after a k_sample launch

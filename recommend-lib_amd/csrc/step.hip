@@ -125,41 +125,6 @@ static __device__ __forceinline__ float4 ld4_sc1(const float* p) {
                      __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
 }
 
-// PS (the persistent step, k_persist_steps): every row, contribution and stamp another workgroup
-// may have written earlier in the same launch is read with sc1 loads (no kernel boundary has
-// invalidated this CU's L1 since); otherwise plain loads
-// (diagnostic build -DBPRMF_PERSIST_PLAIN: plain loads there too -- WRONG results, timing only)
-#ifdef BPRMF_PERSIST_PLAIN
-constexpr bool kPsLoads = false;
-#else
-constexpr bool kPsLoads = true;
-#endif
-template <bool PS>
-static __device__ __forceinline__ float4 ld4p(const float* p) {
-  if constexpr (PS && kPsLoads) return ld4_sc1(p);
-  else return ld4(p);
-}
-template <bool PS>
-static __device__ __forceinline__ int32_t ldw(const int32_t* p) {
-  if constexpr (PS && kPsLoads) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
-}
-
-#ifdef BPRMF_PERSIST_STAMPS  // diagnostic knobs: {stamp-poll sleeps, K2 priority, gate-poll sleeps}
-__device__ int g_pknob[4];
-extern "C" int bprmf_debug_persist_knobs(const int* k) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_pknob), k, sizeof(g_pknob)) == hipSuccess ? 0 : -3;
-}
-#define PKNOB_SLEEP(i)                                   \
-  do {                                                   \
-    for (int z_ = 0; z_ < g_pknob[i]; ++z_) __builtin_amdgcn_s_sleep(4); \
-  } while (0)
-#else
-#define PKNOB_SLEEP(i) \
-  do {                 \
-  } while (0)
-#endif
-
 // Wait (sc1 polls) until a row's stamp reaches step tp, i.e. its owner in the same launch has
 // stored the row and then the stamp.  Bounded: after ~10 s err bit 8 is raised and the wait gives
 // up (the call then fails) instead of hanging the queue.
@@ -169,7 +134,6 @@ static __device__ __forceinline__ void wait_stamp(const int32_t* stamp, int32_t 
     uint32_t polls = 0;
     while (__hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tp) {
       __builtin_amdgcn_s_sleep(1);
-      PKNOB_SLEEP(0);
       if ((++polls & 255) == 0) {  // a wait that already timed out elsewhere ends this one too
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 100 MHz: 10 s
@@ -197,12 +161,7 @@ static __device__ __forceinline__ void put_stamp(int32_t* stamp, int32_t t, bool
 
 // this batch's build timed out (kernels.h kMetaDead): the step leaves the tables alone
 static __device__ __forceinline__ bool build_failed(const BatchView& bv) {
-#ifdef BPRMF_NO_DEAD_CHECK  // diagnostic A/B only
-  (void)bv;
-  return false;
-#else
   return bv.meta[kMetaDead] == kDeadMark;
-#endif
 }
 
 // K1 of step t, one lane group per triplet p (sorted by user).  SH (sharded): i/j are slots of
@@ -213,42 +172,11 @@ static __device__ __forceinline__ bool build_failed(const BatchView& bv) {
 // rows with t (users: only those K2 finishes), for K1 of step t+1.  pw (sharded, fused front
 // launch): the record and the user row are loaded first, then the workgroup waits for the row
 // flags, then the item rows are read.
-// Diagnostic builds only (-DBPRMF_DIAG_WAIT=m, tools/gpu/ab_prof.sh; WRONG results, timing only):
-// which of K1's waits for rows K2 publishes set the fused launch's length.  The K2 batch's hot
-// items (its lrec list, > kLongSeg references) are staged in LDS; m = 1: K1 never waits for the
-// other (cold) rows, m = 2: never for the hot ones, m = 3: waits as shipped (the staging's cost).
-#ifdef BPRMF_DIAG_WAIT
-#define BPRMF_DIAG_PREV , const BatchView* prev = nullptr
-#else
-#define BPRMF_DIAG_PREV
-#endif
-#ifdef BPRMF_PERSIST_STAMPS  // per step (t mod 32), K1 workgroup and triplet slot: its waits done
-__device__ uint64_t g_persist_k1wait[32][1024][32];
-extern "C" int bprmf_debug_persist_k1wait(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_persist_k1wait), sizeof(g_persist_k1wait)) == hipSuccess ? 0 : -3;
-}
-#endif
-template <int G4, int S, bool SH, bool WT, bool WAIT, bool PS = false>
+template <int G4, int S, bool SH, bool WT, bool WAIT>
 static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, const float* __restrict__ item_rows,
-                                               int B, int32_t* err, const PeerWait* pw = nullptr
-                                               BPRMF_DIAG_PREV) {
-#ifdef BPRMF_DIAG_WAIT
-  __shared__ int32_t s_hot[kMaxLongItems];
-  __shared__ int s_nhot;
-  if (WAIT && prev) {
-    if (threadIdx.x == 0) s_nhot = prev->meta[3];
-    if (threadIdx.x < kMaxLongItems) s_hot[threadIdx.x] = prev->lrec[(int64_t)threadIdx.x * kRec];
-    __syncthreads();
-  }
-  auto is_hot = [&](int32_t item) {
-    bool h = false;
-    if (prev)
-      for (int m = 0; m < s_nhot; ++m) h |= s_hot[m] == item;
-    return h;
-  };
-#endif
+                                               int B, int32_t* err, const PeerWait* pw = nullptr) {
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = WAIT || !kFusedStampsOnly;
 #endif
@@ -314,45 +242,31 @@ static __device__ __forceinline__ void k1_body(int blk, BatchView bv, const Tabl
       // not the launch's tail (round 5 A/B: fused launch 9.45 -> 9.37 us by rocprofv3, 9.37-9.47
       // -> 9.21-9.24 us by events, profiles/r05_ab_k1_late_items.txt)
 #pragma unroll
-      for (int k = 0; k < S; ++k) pu[k] = ld4p<PS>(prow + 4 * G4 * k);
+      for (int k = 0; k < S; ++k) pu[k] = ld4(prow + 4 * G4 * k);
       // marks and stamps in ONE round of loads (sc1 stamps: the first poll of a marked row); a
       // marked row whose stamp is not yet tp is then polled alone, so a triplet with two or three
       // rows already published pays one load latency here instead of one per row
       const int64_t o = (int64_t)(tp & 1);
-      const int32_t mi = ldw<PS>(sb.pend_q + o * sb.qrows + i), mj = ldw<PS>(sb.pend_q + o * sb.qrows + j);
-      const int32_t mu = ldw<PS>(sb.pend_p + o * sb.prows + u);
+      const int32_t mi = *(sb.pend_q + o * sb.qrows + i), mj = *(sb.pend_q + o * sb.qrows + j);
+      const int32_t mu = *(sb.pend_p + o * sb.prows + u);
       si = __hip_atomic_load(Q.stamp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sj = __hip_atomic_load(Q.stamp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       su0 = __hip_atomic_load(P.stamp + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       wi = mi == tp;
       wj = mj == tp;
       wu = mu == tp;
-#ifdef BPRMF_DIAG_WAIT
-      {
-        const bool hi = is_hot(i), hj = is_hot(j);
-        const bool skip_i = BPRMF_DIAG_WAIT == 1 ? !hi : BPRMF_DIAG_WAIT == 2 ? hi : false;
-        const bool skip_j = BPRMF_DIAG_WAIT == 1 ? !hj : BPRMF_DIAG_WAIT == 2 ? hj : false;
-        if (skip_i) wi = false;
-        if (skip_j) wj = false;
-      }
-#endif
       if (wi && si != tp) wait_stamp(Q.stamp + i, tp, err);
       if (wj && sj != tp) wait_stamp(Q.stamp + j, tp, err);
       if (wu && su0 != tp) wait_stamp(P.stamp + u, tp, err);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the row loads stay after the stamp reads
-#ifdef BPRMF_PERSIST_STAMPS
-      if (PS && sub == 0 && blk < 1024)
-        g_persist_k1wait[t & 31][blk][(threadIdx.x / G4) & 31] =
-            __builtin_amdgcn_s_memrealtime() | ((uint64_t)(wi | wj << 1 | wu << 2) << 60);
-#endif
     }
     SSTAMP(0, 4);
     if (WAIT) {
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         if (wu) pu[k] = ld4_sc1(prow + 4 * G4 * k);
-        vi[k] = wi ? ld4_sc1(qi + 4 * G4 * k) : ld4p<PS>(qi + 4 * G4 * k);
-        vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4p<PS>(qj + 4 * G4 * k);
+        vi[k] = wi ? ld4_sc1(qi + 4 * G4 * k) : ld4(qi + 4 * G4 * k);
+        vj[k] = wj ? ld4_sc1(qj + 4 * G4 * k) : ld4(qj + 4 * G4 * k);
       }
     } else {
 #pragma unroll
@@ -456,22 +370,21 @@ template <int G4, int S, bool SH>
 struct ItemRow {
   float4 x[S];
   int32_t stamp = 0;
-  template <bool PS = false>
   __device__ __forceinline__ void load(const Table& Q, int32_t item, int ld, int sub) {
     if (SH) return;
     const float* w = Q.W + (int64_t)item * ld + 4 * sub;
 #pragma unroll
-    for (int k = 0; k < S; ++k) x[k] = ld4p<PS>(w + 4 * G4 * k);
-    stamp = ldw<PS>(Q.stamp + item);
+    for (int k = 0; k < S; ++k) x[k] = ld4(w + 4 * G4 * k);
+    stamp = *(Q.stamp + item);
   }
 };
 
-template <int G4, int S, bool PS = false>
+template <int G4, int S>
 static __device__ __forceinline__ void load_ref(float4 (&row)[S], const float* __restrict__ contrib,
                                                 int32_t ref, int ld, int sub) {
   const float* cb = contrib + (int64_t)(ref >> 1) * ld + 4 * sub;
 #pragma unroll
-  for (int k = 0; k < S; ++k) row[k] = ld4p<PS>(cb + 4 * G4 * k);
+  for (int k = 0; k < S; ++k) row[k] = ld4(cb + 4 * G4 * k);
 }
 
 template <int S>
@@ -511,7 +424,7 @@ static __device__ __forceinline__ void finish_item(Table Q, int32_t item, int sl
 }
 
 // sum of the rows src[beg..end) in order (lanes fetch G4 indices at once, 8 rows in flight)
-template <int G4, int S, bool PS = false>
+template <int G4, int S>
 static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __restrict__ src,
                                                 int beg, int end, int ld, int sub) {
 #pragma unroll
@@ -523,7 +436,7 @@ static __device__ __forceinline__ void sum_rows(float4 (&g)[S], const float* __r
       if (m0 + m < end) {
         const float* rp = src + (int64_t)(m0 + m) * ld + 4 * sub;
 #pragma unroll
-        for (int k = 0; k < S; ++k) rows[m][k] = ld4p<PS>(rp + 4 * G4 * k);
+        for (int k = 0; k < S; ++k) rows[m][k] = ld4(rp + 4 * G4 * k);
       }
 #pragma unroll
     for (int m = 0; m < 8; ++m)
@@ -543,22 +456,13 @@ template <int S>
 constexpr int item_rounds() { return S == 1 ? 6 : 1; }
 // one K2 item segment (record r0/r1): the sum of -/+ c P_u over its references in order, then the
 // update (single GPU) or the per-slot gradient (sharded)
-template <int G4, int S, bool SH, bool WT, bool PUB, bool PS>
-// Diagnostic build only (-DBPRMF_DIAG_SLOTS, WRONG results, timing only): what K2's cold item
-// segments would gain if their first 4 contribution rows sat at positions known without the
-// record (a slot-major contribution layout): 4 rows per lane group are requested in the same
-// round as the record, and used in place of the segment's first 4 references.
-#ifdef BPRMF_DIAG_SLOTS
-#define BPRMF_DIAG_PRE(S) , const float4 (*pre)[S] = nullptr
-#else
-#define BPRMF_DIAG_PRE(S)
-#endif
+template <int G4, int S, bool SH, bool WT, bool PUB>
 static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const BatchView& bv,
                                                        const Table& Q, const Hyper& hp, int ld,
                                                        int32_t t, int sub,
                                                        const float* __restrict__ contrib,
                                                        float* __restrict__ grads, const GradRoute* gr,
-                                                       int blk BPRMF_DIAG_PRE(S)) {
+                                                       int blk) {
 #ifdef BPRMF_STEP_STAMPS
   constexpr bool kStampHere = PUB || !kFusedStampsOnly;
 #endif
@@ -571,7 +475,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
   if (kStampHere && threadIdx.x == 0) g_step_stamps[1][blk][4] = (uint64_t)len;
 #endif
   ItemRow<G4, S, SH> row;
-  row.template load<PS>(Q, item, ld, sub);
+  row.load(Q, item, ld, sub);
   float4 g[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -582,14 +486,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 #pragma unroll
     for (int m = 0; m < kInlineRefs; ++m) {
       rf[m] = (pk[m >> 1] >> (16 * (m & 1))) & 0xFFFF;
-#ifdef BPRMF_DIAG_SLOTS
-      if (pre && m < 4) {
-#pragma unroll
-        for (int k = 0; k < S; ++k) rows[m][k] = pre[m][k];
-        continue;
-      }
-#endif
-      if (m < len) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
+      if (m < len) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
     }
 #pragma unroll
     for (int m = 0; m < kInlineRefs; ++m)
@@ -608,7 +505,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 #pragma unroll
         for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
-          if (m0 + m < cnt) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
+          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
         for (int m = 0; m < F; ++m)
@@ -624,7 +521,7 @@ static __device__ __forceinline__ void k2_item_segment(int4 r0, int4 r1, const B
 // segments (one lane group each), user segments spanning K1 workgroups.  PUB (fused step): every
 // updated row's stamp is published after the row (put_stamp), for K1 of step t+1 in the same
 // launch.
-template <int G4, int S, bool SH, int KB, bool WT, bool PUB, bool PS = false>
+template <int G4, int S, bool SH, int KB, bool WT, bool PUB>
 static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Table& P, const Table& Q,
                                                const Hyper& hp, int ld, int32_t t,
                                                const StepBufs& sb, int long_blocks, int item_blocks,
@@ -653,7 +550,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int n = bv.meta[0];
     const int p = blk * KB + threadIdx.x;
     double acc =
-        p < n ? (double)softplus(-__int_as_float(ldw<PS>(reinterpret_cast<const int32_t*>(xloss) + p))) : 0.0;
+        p < n ? (double)softplus(-__int_as_float(*(reinterpret_cast<const int32_t*>(xloss) + p))) : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);  // fixed butterfly
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -679,9 +576,9 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     float* pw = P.W + (int64_t)u * ld + 4 * sub;
     float4 cur[S], g[S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) cur[k] = ld4p<PS>(pw + 4 * G4 * k);
-    const int32_t su = ldw<PS>(P.stamp + u);
-    sum_rows<G4, S, PS>(g, ugrad, r0.y, r0.z, ld, sub);
+    for (int k = 0; k < S; ++k) cur[k] = ld4(pw + 4 * G4 * k);
+    const int32_t su = *(P.stamp + u);
+    sum_rows<G4, S>(g, ugrad, r0.y, r0.z, ld, sub);
     SSTAMP(1, 2);
     const float f = decay_pow(hp.log2a, t - 1 - su);
 #pragma unroll
@@ -700,7 +597,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int32_t item = r0.x;
     const int beg = r0.y, end = r0.z;
     ItemRow<G4, S, SH> row;
-    if (grp == 0) row.template load<PS>(Q, item, ld, sub);
+    if (grp == 0) row.load(Q, item, ld, sub);
     float4 g[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) g[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -709,11 +606,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
     const int lane0 = (threadIdx.x & 63) - sub;
     for (int base = beg + grp; base < end; base += NG * G4) {
       const int ridx = base + NG * sub;
-#ifdef BPRMF_DIAG_HOTPRE  // diagnostic only (WRONG results): no refs level, as a slot-major layout
-      const int32_t myref = ridx < end ? (int32_t)((ridx % B) << 1) : 0;
-#else
       const int32_t myref = ridx < end ? bv.refs[ridx] : 0;
-#endif
       const int cnt = min(G4, (end - base + NG - 1) / NG);
       constexpr int F = S == 1 ? 16 : 8;  // rows in flight per group (a hot item has ~80 refs)
       for (int m0 = 0; m0 < cnt; m0 += F) {
@@ -722,7 +615,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
 #pragma unroll
         for (int m = 0; m < F; ++m) {
           rf[m] = __shfl(myref, lane0 + ((m0 + m) & (G4 - 1)));
-          if (m0 + m < cnt) load_ref<G4, S, PS>(rows[m], contrib, rf[m], ld, sub);
+          if (m0 + m < cnt) load_ref<G4, S>(rows[m], contrib, rf[m], ld, sub);
         }
 #pragma unroll
         for (int m = 0; m < F; ++m)
@@ -762,17 +655,6 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
   const int s0 = (bid - long_blocks) * NG + grp;
   const int stride = item_blocks * NG;
   const int sc = min(s0, 2 * B - 1);
-#ifdef BPRMF_DIAG_SLOTS
-  float4 pre[4][S];
-  if (!SH) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float* cb = contrib + (int64_t)((sc * 4 + m) % B) * ld + 4 * sub;
-#pragma unroll
-      for (int k = 0; k < S; ++k) pre[m][k] = *reinterpret_cast<const float4*>(cb + 4 * G4 * k);
-    }
-  }
-#endif
   int4 r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[0];
   int4 r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)sc * kRec)[1];
   const int n_iseg = bv.meta[2];
@@ -787,12 +669,7 @@ static __device__ __forceinline__ void k2_body(int blk, BatchView bv, const Tabl
       r0 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[0];
       r1 = reinterpret_cast<const int4*>(bv.irec + (int64_t)s * kRec)[1];
     }
-#ifdef BPRMF_DIAG_SLOTS
-    k2_item_segment<G4, S, SH, WT, PUB, PS>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk,
-                                            (!SH && round == 0) ? pre : nullptr);
-#else
-    k2_item_segment<G4, S, SH, WT, PUB, PS>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
-#endif
+    k2_item_segment<G4, S, SH, WT, PUB>(r0, r1, bv, Q, hp, ld, t, sub, contrib, grads, gr, blk);
   }
 }
 
@@ -801,32 +678,11 @@ __global__ __launch_bounds__(KB) void k_item_step(BatchView bv, Table P, Table Q
                                                   const int32_t* __restrict__ tbase, int step,
                                                   StepBufs sb, int long_blocks, int item_blocks,
                                                   float* __restrict__ grads, double* __restrict__ loss,
-                                                  int64_t bstride, int B, StatusFold sf) {
+                                                  int64_t bstride, int B) {
   CsScope cs_(62);
   if (bstride) bv = bv.shifted((int64_t)(tbase[1] + step) * bstride);
   k2_body<G4, S, SH, KB, WT, false>(blockIdx.x, bv, P, Q, hp, ld, *tbase + step + 1, sb, long_blocks,
                                     item_blocks, grads, loss, B);
-  // the call's status (StatusFold): the loss workgroups come first in the grid, and only their
-  // slots and the error words (set by earlier launches) make the status, so the last loss
-  // workgroup to finish publishes it while item workgroups may still run (later calls, and any
-  // read of the tables, are ordered after this launch on the stream)
-  const int lb = loss && sb.xloss ? (B + KB - 1) / KB : 0;
-  if (sf.cnt && (int)blockIdx.x < lb && threadIdx.x == 0) {
-    const double v = loss[blockIdx.x];  // written by this thread in k2_body (or untouched: dead)
-    __hip_atomic_store(sf.host + 2 + blockIdx.x, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the host slot written before arriving
-    if (__hip_atomic_fetch_add(sf.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lb - 1) {
-      for (int k = lb; k < sf.nslots; ++k)  // slots no loss workgroup owns (zeroed at call start)
-        __hip_atomic_store(sf.host + 2 + k, sf.dstatus[2 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(sf.host, __hip_atomic_load(sf.dstatus, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // the error word
-      __hip_atomic_store(sf.host + 1, sf.dstatus[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(sf.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sf.seq_dst, sf.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
 }
 
 // The fused step: K2 of step t (batch c[1] + step) and K1 of step t + 1 (the next batch) in one
@@ -853,151 +709,8 @@ __global__ __launch_bounds__(KB) void k_fused_step(BatchView bv0, Table P, Table
     k2_body<G4, S, false, KB, true, true>(blockIdx.x, bv0.shifted(kb * bstride), P, Q, hp, ld, t, sb,
                                           long_blocks, item_blocks, nullptr, loss, B);
   else
-  {
-#ifdef BPRMF_DIAG_WAIT
-    const BatchView prev = bv0.shifted(kb * bstride);
-    k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
-                                      hp, ld, t + 1, sb, nullptr, B, err, nullptr, &prev);
-#else
     k1_body<G4, S, false, true, true>(blockIdx.x - k2_blocks, bv0.shifted((kb + 1) * bstride), P, Q,
                                       hp, ld, t + 1, sb, nullptr, B, err);
-#endif
-  }
-}
-
-// ---- the persistent step: a whole chunk in one launch (BPRMF_PERSIST, k_persist_steps) ----
-// Each workgroup keeps one role for the chunk: K2 workgroup b runs K2 of every step, K1
-// workgroup w runs K1 of every step, and the kernel boundary between fused launches becomes two
-// flag gates.  Every workgroup publishes its progress after each step (its stores acknowledged,
-// a workgroup barrier, then an sc1 store of the step number: MI355X_MICROARCH.md "Valid forms",
-// the first table row); f1[w] = the last step K1 workgroup w finished, f2[b] likewise for K2.
-//   K2 of step t starts once every K1 workgroup has finished step t (all contributions, xloss,
-//     ugrad and K1's in-place row updates of step t are in; the step's pend marks too);
-//   K1 of step t starts once every K1 workgroup has finished step t-1 (the marks of step t-1 are
-//     final, so the fused K1's mark-and-stamp protocol applies unchanged) and every K2 workgroup
-//     has finished step t-2 (the contribution / ugrad / xloss half of step t is free again, and
-//     every row update of steps <= t-2 is complete).
-// K2 of step t therefore runs beside K1 of step t+1 exactly as in k_fused_step, without the
-// boundary, the dispatch of ~850 workgroups and their record loads between steps.  Flags hold
-// global step numbers, which only grow, so they are never reset.  All of the launch's workgroups
-// must be resident at once (persist_step checks the occupancy); every wait is bounded (err bit 8
-// after ~10 s, and a raised bit 8 ends every other wait), so a violated assumption fails the call
-// instead of hanging the queue.
-// diagnostic build only (-DBPRMF_PERSIST_STAMPS, tools/ubench_persist_stamps.py): per step k < 32
-// and workgroup, s_memrealtime after its gate, after its step's body, after its arrival
-#ifdef BPRMF_PERSIST_STAMPS
-__device__ uint64_t g_persist_stamps[32][2048][3];
-#define PSTAMP(k, which)                                                             \
-  do {                                                                               \
-    if (threadIdx.x == 0 && (k) < 32 && blk < 2048)                                  \
-      g_persist_stamps[k][blk][which] = __builtin_amdgcn_s_memrealtime();            \
-  } while (0)
-extern "C" int bprmf_debug_persist_stamps(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_persist_stamps), sizeof(g_persist_stamps)) == hipSuccess ? 0 : -3;
-}
-#else
-#define PSTAMP(k, which) \
-  do {                   \
-  } while (0)
-#endif
-// Progress flags: one int32 per workgroup (the step it finished), polled by wave 0 of a waiting
-// workgroup alone, 4 flags per lane per round (two 8-byte sc1 loads).  (Byte flags, 4x fewer
-// lines, measured slower: profiles/r05_persist.)
-static __device__ __forceinline__ bool flags_reached(const int32_t* f, int n, int32_t target, int lane) {
-  bool ok = true;
-  for (int base = 4 * lane; base < n; base += 256) {
-    const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(f + base), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(f + base) + 1, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t v[4] = {(int32_t)a, (int32_t)(a >> 32), (int32_t)b, (int32_t)(b >> 32)};
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (base + q < n) ok &= v[q] >= target;
-  }
-  return ok;
-}
-
-static __device__ __forceinline__ void gate_wait(const int32_t* f, int n, int32_t target,
-                                                 const int32_t* f2, int n2, int32_t target2,
-                                                 int32_t* err) {
-  if (threadIdx.x < 64) {  // wave 0 polls; the others wait at the barrier below
-    const int lane = threadIdx.x;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    int bail = 0;
-    for (uint32_t polls = 1;; ++polls) {
-      const bool ok = flags_reached(f, n, target, lane) && flags_reached(f2, n2, target2, lane);
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(2);
-      PKNOB_SLEEP(2);
-      if ((polls & 127) == 0) {
-        bail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8;
-        if (!bail && __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {  // 100 MHz: 10 s
-          if (lane == 0) atomicOr(err, 8);
-          bail = 1;
-        }
-        if (bail) break;  // uniform over the wave (every lane read the same word and clock); the
-                          // step then runs on whatever it reads, and the call fails on err bit 8
-      }
-    }
-  }
-  __syncthreads();  // every later load of the step sits behind the polling wave's match
-}
-
-static __device__ __forceinline__ void gate_arrive(int32_t* f, int32_t t) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores of the step acknowledged
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(f, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int G4, int S, int KB>
-#ifndef BPRMF_PERSIST_WAVES  // waves per SIMD the persistent kernel is held to (diagnostic builds vary it)
-#define BPRMF_PERSIST_WAVES 4
-#endif
-__global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(BPRMF_PERSIST_WAVES))) void k_persist_steps(BatchView bv0, Table P, Table Q, Hyper hp, int ld,
-                                                      const int32_t* __restrict__ tbase, StepBufs sb,
-                                                      int long_blocks, int item_blocks, int k2_blocks,
-                                                      int k1_blocks, double* __restrict__ loss,
-                                                      int64_t bstride, int B, int n, int32_t* err,
-                                                      int32_t* f1, int32_t* f2) {
-  static_assert(KB == kBlock, "K1 and K2 workgroups share the launch's block size");
-  const int32_t t0 = tbase[0];
-  const int64_t kb0 = tbase[1];
-  const int blk = blockIdx.x;
-  if (blk < k2_blocks) {
-    for (int k = 0; k < n; ++k) {
-      const int32_t t = t0 + k + 1;
-      gate_wait(f1, k1_blocks, t, nullptr, 0, 0, err);
-      PSTAMP(k, 0);
-#ifdef BPRMF_PERSIST_STAMPS
-      if (g_pknob[1] == 1) __builtin_amdgcn_s_setprio(1);
-      if (g_pknob[1] == 2) __builtin_amdgcn_s_setprio(2);
-      if (g_pknob[1] == 3) __builtin_amdgcn_s_setprio(3);
-#endif
-      k2_body<G4, S, false, KB, true, true, true>(blk, bv0.shifted((kb0 + k) * bstride), P, Q, hp, ld, t,
-                                                  sb, long_blocks, item_blocks, nullptr, loss, B);
-      PSTAMP(k, 1);
-      gate_arrive(f2 + blk, t);
-      PSTAMP(k, 2);
-    }
-    return;
-  }
-  const int w = blk - k2_blocks;
-  for (int k = 0; k < n; ++k) {
-    const int32_t t = t0 + k + 1;
-    const BatchView bv = bv0.shifted((kb0 + k) * bstride);
-    if (k == 0) {  // the rows are final since the previous launch: plain loads, no marks to read
-      PSTAMP(k, 0);
-      k1_body<G4, S, false, true, false>(w, bv, P, Q, hp, ld, t, sb, nullptr, B, err);
-    } else {
-      gate_wait(f1, k1_blocks, t - 1, f2, k >= 2 ? k2_blocks : 0, t - 2, err);
-      PSTAMP(k, 0);
-      k1_body<G4, S, false, true, true, true>(w, bv, P, Q, hp, ld, t, sb, nullptr, B, err);
-    }
-    PSTAMP(k, 1);
-    gate_arrive(f1 + w, t);
-    PSTAMP(k, 2);
-  }
 }
 
 // ---- the fused sharded step over the IPC transport (dist.cpp enqueue_steps, two launches/step) ----
@@ -1052,13 +765,6 @@ __global__ __launch_bounds__(kBlock) void k_dist_front(OwnerArgs o, BatchView bv
                                     item_rows, B, nullptr, &all);
 }
 
-// BPRMF_WT=0 turns the write-through row stores off, BPRMF_K2_BLOCK=1024 restores 1024-thread
-// item-step workgroups (A/B of the two choices; read at launch / capture time)
-static bool use_wt() {
-  const char* e = getenv("BPRMF_WT");
-  return !(e && e[0] == '0');
-}
-
 static StepBufs plain_bufs(float* contrib, float* ugrad, float* xloss, const StepBufs* sb) {
   if (sb) return *sb;
   StepBufs b;
@@ -1072,22 +778,17 @@ hipError_t user_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const
                      const int32_t* tbase, int step, float* xloss, float* contrib, float* ugrad,
                      const float* item_rows, hipStream_t s, const PeerWait& pw,
                      int64_t bstride, const StepBufs* sbp) {
-  const bool wt = use_wt();
   const StepBufs sb = plain_bufs(contrib, ugrad, xloss, sbp);
   BPRMF_DISPATCH4(g, ({
+    // every row and contribution store is write-through (sc1): the kernel boundary then has no
+    // dirty-L2 write-back of them to wait for (WT = false builds remain for the template's sake)
     const unsigned blocks = (unsigned)((B + kBlock / G4_ - 1) / (kBlock / G4_));
-    if (item_rows && wt)
+    if (item_rows)
       k_user_step<G4_, S_, true, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
                                                                  item_rows, pw, bstride, B);
-    else if (item_rows)
-      k_user_step<G4_, S_, true, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
-                                                                  item_rows, pw, bstride, B);
-    else if (wt)
+    else
       k_user_step<G4_, S_, false, true><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
                                                                   nullptr, pw, bstride, B);
-    else
-      k_user_step<G4_, S_, false, false><<<blocks, kBlock, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,
-                                                                   nullptr, pw, bstride, B);
   }));
   return hipGetLastError();
 }
@@ -1104,14 +805,8 @@ struct K2Grid {
 // item lane groups of the single-GPU step per 1024 triplets of the batch: K1 finishes the
 // single-reference items, so ~1,000 of a 4,096-triplet batch's ~5,700 distinct items reach K2
 // (ml-20m shape); 384 per 1024 gives those one lane group each, and a lane group loops when a
-// batch has more (BPRMF_K2_ITEM_LG overrides, 0 = one lane group per possible segment, A/B)
-static int k2_item_lg() {
-  static const int lg = [] {
-    const char* e = getenv("BPRMF_K2_ITEM_LG");
-    return e && *e ? atoi(e) : 384;
-  }();
-  return lg;
-}
+// batch has more (round 4 A/B against one lane group per possible segment: DESIGN.md §5)
+constexpr int kK2ItemLg = 384;
 
 template <int G4, int S, int KB>
 static K2Grid k2_grid(int B, bool loss, bool capped = false) {
@@ -1120,10 +815,10 @@ static K2Grid k2_grid(int B, bool loss, bool capped = false) {
   K2Grid k;
   k.long_blocks = item_long_blocks(B);
   k.item_blocks = (int)((2LL * B + NG - 1) / NG);
-  if (R > 1 && capped && k2_item_lg() > 0) {
+  if (R > 1 && capped) {
     const int need = (int)((2LL * B + (int64_t)R * NG - 1) / ((int64_t)R * NG));
     k.item_blocks = std::min<int>(
-        k.item_blocks, std::max<int>(need, (int)(((int64_t)B * k2_item_lg() / 1024 + NG - 1) / NG)));
+        k.item_blocks, std::max<int>(need, (int)(((int64_t)B * kK2ItemLg / 1024 + NG - 1) / NG)));
   }
   // segments K2 finishes span K1 workgroups: at most one per workgroup boundary, and B/2
   const int tpb = kBlock / G4;
@@ -1137,7 +832,7 @@ template <int G4, int S, int KB>
 static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, Table Q,
                                    const Hyper& hp, const int32_t* tbase, int step,
                                    const StepBufs& sb, float* grads, hipStream_t s, double* loss,
-                                   int64_t bstride, bool wt, const StatusFold& sf) {
+                                   int64_t bstride) {
   // single GPU: capped, when the items are many against the batch's 2B references (few items, as
   // at the ml-1m shape, send most of their segments to K2, which the capped grid serialises)
   const K2Grid k = k2_grid<G4, S, KB>(B, loss != nullptr, grads == nullptr && Q.rows >= 2LL * B);
@@ -1145,11 +840,9 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
 #define BPRMF_K2(SH_, WT_)                                                                        \
   k_item_step<G4, S, SH_, KB, WT_><<<blocks, KB, 0, s>>>(bv, P, Q, hp, g.ld, tbase, step, sb,       \
                                                         k.long_blocks, k.item_blocks, grads, loss, \
-                                                        bstride, B, sf)
-  if (grads && wt) BPRMF_K2(true, true);
-  else if (grads) BPRMF_K2(true, false);
-  else if (wt) BPRMF_K2(false, true);
-  else BPRMF_K2(false, false);
+                                                        bstride, B)
+  if (grads) BPRMF_K2(true, true);
+  else BPRMF_K2(false, true);
 #undef BPRMF_K2
   return hipGetLastError();
 }
@@ -1161,20 +854,13 @@ static hipError_t launch_item_step(const Geom& g, BatchView bv, int B, Table P, 
 hipError_t item_step(const Geom& g, BatchView bv, int B, Table P, Table Q, const Hyper& hp,
                      const int32_t* tbase, int step, const float* contrib, const float* ugrad,
                      float* grads, hipStream_t s, const float* xloss, double* loss,
-                     int64_t bstride, const StepBufs* sbp, const StatusFold* sfp) {
+                     int64_t bstride, const StepBufs* sbp) {
   const StepBufs sb = plain_bufs(const_cast<float*>(contrib), const_cast<float*>(ugrad),
                                  const_cast<float*>(xloss), sbp);
   if (!sb.xloss) loss = nullptr;
-  const StatusFold sf = sfp && loss ? *sfp : StatusFold{};
-  const bool wt = use_wt();
-  const char* kb = getenv("BPRMF_K2_BLOCK");
-  const bool big = kb && atoi(kb) == 1024;
   BPRMF_DISPATCH4(g, ({
-    if (big)
-      return launch_item_step<G4_, S_, (S_ == 1 ? 1024 : 512)>(g, bv, B, P, Q, hp, tbase, step, sb,
-                                                               grads, s, loss, bstride, wt, sf);
     return launch_item_step<G4_, S_, 256>(g, bv, B, P, Q, hp, tbase, step, sb, grads, s, loss,
-                                          bstride, wt, sf);
+                                          bstride);
   }));
   return hipGetLastError();
 }
@@ -1190,45 +876,6 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
     k_fused_step<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
         bv0, P, Q, hp, g.ld, tbase, step, sb, k.long_blocks, k.item_blocks, k.total(), loss,
         bstride, B, err);
-  }));
-  return hipGetLastError();
-}
-
-// the persistent step's grid: every workgroup must be resident at once (its waits are on the
-// others); 0 = it does not fit this device at this shape (the caller runs the fused launches)
-int persist_grid(const Geom& g, int B, bool loss, int* k2_blocks, int* k1_blocks) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  int total = 0;
-  BPRMF_DISPATCH4(g, ({
-    // one stripe (d <= 256) only: wider rows need more registers than 4 resident workgroups per
-    // CU leave (the kernel is held to 128 VGPRs, and spills there at S >= 2)
-    if (S_ != 1) return 0;
-    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss, true);
-    *k2_blocks = k.total();
-    *k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_persist_steps<G4_, S_, kBlock>, kBlock, 0) !=
-        hipSuccess)
-      return 0;
-    total = *k2_blocks + *k1_blocks;
-  }));
-  return (int64_t)per_cu * cus >= total ? total : 0;
-}
-
-hipError_t persist_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
-                        const Hyper& hp, const int32_t* tbase, int n, const StepBufs& sb, double* loss,
-                        int32_t* err, int32_t* f1, int32_t* f2, hipStream_t s) {
-  if (!sb.pend_q || !sb.pend_p || !sb.pstride || !bstride || n <= 0) return hipErrorInvalidValue;
-  if (!sb.xloss) loss = nullptr;
-  BPRMF_DISPATCH4(g, ({
-    // the same item-grid cap as the fused launches (Q.rows >= 2B), which persist_grid assumes
-    if (Q.rows < 2LL * B) return hipErrorInvalidValue;
-    const K2Grid k = k2_grid<G4_, S_, kBlock>(B, loss != nullptr, true);
-    const int k1_blocks = (B + kBlock / G4_ - 1) / (kBlock / G4_);
-    k_persist_steps<G4_, S_, kBlock><<<(unsigned)(k.total() + k1_blocks), kBlock, 0, s>>>(
-        bv0, P, Q, hp, g.ld, tbase, sb, k.long_blocks, k.item_blocks, k.total(), k1_blocks, loss,
-        bstride, B, n, err, f1, f2);
   }));
   return hipGetLastError();
 }

@@ -242,13 +242,6 @@ class BPRMF:
         """Leave the batches as a timed-out build would (tests only): the next call fails."""
         _lib.check(self._L.bprmf_debug_fail_build(self._h))
 
-    def debug_persist_grid(self):
-        """The persistent step's workgroup count (0: not resident here, fused launches; -1: not
-        probed yet; tests only)."""
-        v = ctypes.c_int32(0)
-        _lib.check(self._L.bprmf_debug_persist_grid(self._h, ctypes.byref(v)))
-        return v.value
-
     # -- weights -------------------------------------------------------------------------------
     def local_rows(self):
         u, i = ctypes.c_int64(), ctypes.c_int64()

@@ -164,7 +164,7 @@ int main() {
         CHECK((__int128)rg.row_elems == (__int128)W * rg.S * 256);
         CHECK((__int128)rg.id_elems == (__int128)W * 256 * rg.S);
         for (int cap : {0, 1, 63, 64, 65, rg.S})
-          CHECK((__int128)aplan_words(256, W, cap) == (__int128)256 * W * (cap > 0 ? cap : 1) * (3 * W + 1));
+          CHECK((__int128)aplan_words(256, W, cap) == (__int128)256 * W * (cap > 0 ? cap : 1) * (2 * W + 1));
       }
   {
     RunnerGeom rg;

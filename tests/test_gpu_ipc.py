@@ -107,14 +107,13 @@ def _loopback(rl, world, spec, mode, key):
     return out
 
 
-@pytest.mark.parametrize("world,fuse2", [(1, "auto"), (2, "auto"), (3, "auto"), (4, "auto"),
-                                         (2, "1"), (3, "1"), (2, "fuse3"), (3, "fuse3")])
-def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse2):
-    """fuse2 "1": the two-launch step (owner phase beside K1, K2 straight into the owners'
-    landing buffers) forced on although the ranks share the box's one GPU (it is off by default
-    there); "fuse3": the three-launch fused form (owner step, K1 and K2 waiting in-kernel, a push
-    kernel); "auto": the default (ranks sharing one GPU: every exchange a push kernel plus a
-    receive copy into cached buffers)."""
+@pytest.mark.parametrize("world,fuse", [(1, "auto"), (2, "auto"), (3, "auto"), (4, "auto"),
+                                        (2, "1"), (3, "1")])
+def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse):
+    """fuse "1": the fused two-launch step (owner phase beside K1, K2 straight into the owners'
+    landing buffers; the default with one rank per GPU) forced on although the ranks share the
+    box's one GPU; "auto": the shared-device default (every exchange a push kernel plus a receive
+    copy into cached buffers)."""
     U, I, D, GB, steps = 301, 157, 128, 512, 6
     g = np.random.default_rng(11)
     u = g.integers(0, U, (steps, GB)).astype(np.int32)
@@ -125,9 +124,7 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse2)
                 P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
                 Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
     res = _run_workers(tmp_path, spec, "replay", world,
-                       extra_env={"auto": None,
-                                  "fuse3": {"BPRMF_DIST_FUSE": "1", "BPRMF_DIST_FUSE2": "0"}}.get(
-                           fuse2, {"BPRMF_DIST_FUSE2": fuse2}))
+                       extra_env=None if fuse == "auto" else {"BPRMF_DIST_FUSE": fuse})
     sh = rl.sharded
     P = sh.unshard_rows([r["P"] for r in res], U)
     Q = sh.unshard_rows([r["Q"] for r in res], I)

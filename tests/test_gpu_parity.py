@@ -771,66 +771,3 @@ def test_topk_all_after_training_uses_lazy_decay(rl, golden):
         S[u, pos[pos[:, 0] == u, 1]] = -np.inf
     tol = 4e-6 * (np.abs(P).astype(np.float64) @ np.abs(Q.T).astype(np.float64)).max()
     _check_topk_all(items, scores, S, 10, tol)
-
-
-def test_status_folded_into_last_k2_equals_status_launch(rl, golden, monkeypatch):
-    """The call's status (error word, loss slots, sequence number) published by the last loss
-    workgroup of the call's last K2 (StatusFold) instead of a k_status_out
-    launch: every call's loss and the tables bitwise equal to BPRMF_STATUS_FOLD=0's, over calls of
-    1, 2, 7 and 40 steps (one loss workgroup to several), and a failed call still reports."""
-    f = golden("bpr_ml100k_replay.npz")
-    pos = f["positives"].astype(np.int64)
-    U, I = int(f["U"]), int(f["I"])
-    runs = {}
-    for fold in ("1", "0"):
-        monkeypatch.setenv("BPRMF_STATUS_FOLD", fold)
-        m = rl.BPRMF(U, I, 64, lr=0.05, wd=0.001, batch_size=1024, seed=9, device=0)
-        m.set_train(pos)
-        losses, at = [], 0
-        for n in (1, 2, 7, 40, 1, 7):
-            losses.append(m.train_steps(0, at, n)["loss"])
-            at += n
-        runs[fold] = (losses, m.get_weights())
-    assert runs["1"][0] == runs["0"][0]
-    for x, y in zip(runs["1"][1], runs["0"][1]):
-        assert np.array_equal(x, y)
-    monkeypatch.setenv("BPRMF_STATUS_FOLD", "1")
-    m = rl.BPRMF(U, I, 64, batch_size=1024, seed=9, device=0)
-    m.set_train(pos)
-    m.train_steps(0, 0, 2)
-    m.debug_fail_build()  # err bit 16: the folded status must carry it
-    with pytest.raises(rl.BprmfError, match="batch builder"):
-        m.train_steps(0, 2, 3)
-    assert m.train_steps(0, 5, 3)["loss"] > 0
-
-
-@pytest.mark.parametrize("U,I,d,B", [(138493, 26744, 128, 4096), (3000, 9000, 32, 2048),
-                                     (943, 1682, 64, 512), (200, 400, 8, 64)])
-def test_persistent_step_equals_fused_launches_bitwise(rl, monkeypatch, U, I, d, B):
-    """The persistent step (one launch per chunk, K1 / K2 workgroups handing steps over by
-    progress flags, step.hip k_persist_steps) gives the fused launches' result bit for bit: the
-    same K1 / K2 arithmetic, only the schedule differs.  Chunks of 2 .. 300 steps, a second epoch,
-    the call losses equal too; the persistent launch must actually have run."""
-    syn = __import__("importlib").import_module("recommend-lib_amd.synthetic")
-    pos = syn.make_positives(U, I, min(40 * U, 2_000_000), 5)
-    outs = []
-    for persist in ("1", "0"):
-        monkeypatch.setenv("BPRMF_PERSIST", persist)
-        m = _model(rl, U, I, d, B, seed=13)
-        m.set_train(pos)
-        n = m.epoch_size()[1]
-        losses, first = [], 0
-        for c in (2, 3, 20, 1, 64, 300):
-            c = min(c, n - first)
-            if c <= 0:
-                break
-            losses.append(m.train_steps(0, first, c)["loss"])
-            first += c
-        losses.append(m.train_steps(1, 0, min(n, 21))["loss"])
-        if persist == "1":
-            assert m.debug_persist_grid() > 0
-        outs.append((m.get_weights(), losses))
-    (P0, Q0), l0 = outs[0]
-    (P1, Q1), l1 = outs[1]
-    assert np.array_equal(P0, P1) and np.array_equal(Q0, Q1)
-    assert l0 == l1

@@ -84,6 +84,44 @@ def test_stale1_runner_replay_matches_oracle(rl, monkeypatch, world, chunk):
     assert np.abs(Q - Qe).max() > 1e-5
 
 
+@pytest.mark.parametrize("chunk", [0, 3])
+def test_stale1_rccl_transport_world1_matches_oracle(rl, monkeypatch, chunk):
+    """The RCCL transport: at world 1 its exchanges are asynchronous copies on the
+    owner stream, so the owner stream (gradient exchange, apply, gather and row exchange of step
+    k) really runs beside the compute stream's K1 / K2 of step k + 1 -- the loopback transport's
+    host-blocking exchanges never let them overlap.  The hazards of that overlap (row parity k & 1
+    reused for the rows of step k + 2, the gradient parity reused by K2 of step k + 2, the event
+    slots k & 3) are checked against sharded_stale1_serial across chunk boundaries
+    (BPRMF_DIST_CHUNK) with a hot item and i == j triplets, over 12 steps."""
+    import ctypes
+    if chunk:
+        monkeypatch.setenv("BPRMF_DIST_CHUNK", str(chunk))
+    g = np.random.default_rng(700 + chunk)
+    P0 = (0.05 * g.standard_normal((U, D))).astype(np.float32)
+    Q0 = (0.05 * g.standard_normal((I, D))).astype(np.float32)
+    GB, steps, lr, wd = 512, 12, 0.05, 0.01
+    batches = []
+    for _ in range(steps):
+        u, i, j = g.integers(0, U, GB), g.integers(0, I, GB), g.integers(0, I, GB)
+        i[:40] = 7  # a hot item, touched by every step
+        j[40:45] = i[40:45]  # i == j
+        batches.append((u, i, j))
+    m = rl.sharded.HipShard(U, I, D, lr, wd, GB, 4, 0.01, 0, 0, 0, 1, "stale1")
+    m.set_weights(P0, Q0)
+    uid = (ctypes.c_uint8 * 128)()
+    rl._lib.check(rl._lib.load().bprmf_dist_unique_id(ctypes.addressof(uid)))
+    m.runner_rccl(bytes(uid))
+    cat = [np.concatenate([b[k] for b in batches]) for k in range(3)]
+    st = m.runner_train_replay(cat[0], cat[1], cat[2], steps)
+    P, Q = m.get_weights()
+    Pr, Qr = P0.copy(), Q0.copy()
+    losses = O.sharded_stale1_serial(Pr, Qr, batches, lr, wd, chunk or 10**9)
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+    assert st["loss"] == pytest.approx(losses.sum(), rel=1e-5)
+    assert st["steps"] == steps
+
+
 def test_stale1_refuses_per_step_calls_and_single_gpu_path(rl):
     sh = rl.sharded
     pos = np.array([[u, (u * 7 + k) % 13] for u in range(10) for k in range(3)], np.int64)

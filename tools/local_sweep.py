@@ -2,8 +2,8 @@
 shape's 1.5e8 positives are generated and uploaded once): per variant, a warm-up and a timed
 region of whole 128-step periods, step time by the library's live HIP events, algorithmic TB/s
 and the fraction of the 8 TB/s roofline.  Variants are environment settings
-the library reads at every launch (hogwild.hip: BPRMF_HOGWILD_TPW, _NARROW, _WINDOW, _BLOCKS,
-_LOCAL_WX, _PLAIN).
+the library reads at every launch (hogwild.hip: BPRMF_HOGWILD_WINDOW; the other round-4 launch
+knobs were removed in round 6 with their measured settings fixed).
 
   python tools/local_sweep.py [--shape c5|ml20m] [--steps 1024] "NAME:ENV=v,ENV=v" ...
 """

@@ -17,14 +17,15 @@ PHASES = ["loads", "user sort", "user segments", "item keys+sort", "item heads/r
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     b = importlib.import_module("recommend-lib_amd.build")
-    extra = tuple(sys.argv[2:])  # further diagnostic defines
+    extra = tuple(a for a in sys.argv[2:] if a != "--split")  # further diagnostic defines
+    # the step kernels never run on a diagnostic build's batches (some are wrong on purpose),
+    # except in the split builder's form (--split: its batches are the shipped ones)
+    if "--split" not in sys.argv:
+        extra += ("BPRMF_DIAG_BUILD_ONLY",)
     print(b.build(force=True, defines=("BPRMF_BUILD_STAMPS",) + extra, out=LIB))
     sys.exit(0)
 
 os.environ["BPRMF_DIAG_LIB"] = LIB
-# the step kernels never run on a diagnostic build's batches (some are wrong on purpose)
-if "--split" not in sys.argv:
-    os.environ["BPRMF_DIAG_BUILD_ONLY"] = "1"
 import ctypes  # noqa: E402
 
 import numpy as np  # noqa: E402

@@ -5,7 +5,7 @@ from the call's first launch, median over calls (ml-20m shape, d=128, B=4096, th
 
   python tools/ubench_call_stamps.py build     # here: compile tools/libbprmf_cstamps.so
   python tools/ubench_call_stamps.py [calls]   # GPU box
-Env knobs pass through (e.g. BPRMF_SPLIT_SAMPLE=0, BPRMF_K2_ITEM_LG=0) for A/B.
+Env knobs pass through (e.g. BPRMF_SPLIT_SAMPLE=0) for A/B.
 """
 import ctypes
 import importlib

@@ -79,13 +79,13 @@ def summarize(st, k1_blocks, k2_blocks):
 
 
 k1_blocks = B // (256 // 32)
-KB = int(os.environ.get("BPRMF_K2_BLOCK", "256"))
+KB = 256  # K2 workgroup size (step.hip)
 NG = KB // 32
 lb = (B + KB - 1) // KB
 k2_users = min(B // 2, B // 8)
 # the item workgroups as step.hip k2_grid sizes them for the single-GPU step (capped: up to 6
-# segments per lane group; BPRMF_K2_ITEM_LG=0: one lane group per possible segment)
-lg = int(os.environ.get("BPRMF_K2_ITEM_LG", "384"))
+# segments per lane group, kK2ItemLg = 384 lane groups per 1024 triplets)
+lg = 384
 item_blocks = (2 * B + NG - 1) // NG
 if lg > 0:
     need = (2 * B + 6 * NG - 1) // (6 * NG)

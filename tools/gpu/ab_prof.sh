@@ -22,6 +22,6 @@ for r in $(seq 1 "$reps"); do
       timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-relaxed \
         > "$out/bench_${name}_$r.log" 2>&1 ) || { echo "variant $name rep $r failed"; tail -n 5 "$out/prof_${name}_$r.log" "$out/bench_${name}_$r.log"; exit 1; }
     st=$(find "$out/prof_${name}_$r" -name '*kernel_stats.csv' | head -n 1)
-    echo "$name $r $(python3 tools/kstats.py --only k_fused_step,k_user_step,k_build_split,k_persist_steps "$st" | cut -d: -f2-) | bench $(grep '^{' "$out/bench_${name}_$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e8,4), "e8", d["ms_per_step"]*1e3, "us/step", d["roofline"]["avg_us_per_step"])')" | tee -a "$out/summary.txt"
+    echo "$name $r $(python3 tools/kstats.py --only k_fused_step,k_user_step,k_build_split,k_owner_diag "$st" | cut -d: -f2-) | bench $(grep '^{' "$out/bench_${name}_$r.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e8,4), "e8", d["ms_per_step"]*1e3, "us/step", d["roofline"]["avg_us_per_step"])')" | tee -a "$out/summary.txt"
   done
 done

@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libbprmf_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "owner_step.hip", "hogwild.hip", "dist.hip", "topk.hip", "ncf.hip", "capi.cpp", "dist.cpp", "ncf_capi.cpp", "ingest.cpp", "status.cpp", "host_plan.cpp", "node_barrier.cpp", "mf.hip", "mf_capi.cpp", "bprfm.hip", "bprfm_capi.cpp", "sgns.hip", "sgns_capi.cpp")]
+SOURCES = [os.path.join(HERE, "csrc", n) for n in ("kernels.hip", "segment.hip", "step.hip", "hogwild.hip", "dist.hip", "topk.hip", "ncf.hip", "capi.cpp", "dist.cpp", "ncf_capi.cpp", "ingest.cpp", "status.cpp", "host_plan.cpp", "node_barrier.cpp", "mf.hip", "mf_capi.cpp", "bprfm.hip", "bprfm_capi.cpp", "sgns.hip", "sgns_capi.cpp")]
 HEADERS = [os.path.join(HERE, "csrc", n) for n in ("kernels.h", "device_common.h", "handle.h", "ncf_kernels.h", "mf_kernels.h", "bprfm_kernels.h", "sgns_kernels.h", "status.h", "dist_body.h", "host_plan.h")] + [os.path.join(ROOT, "include", n) for n in ("bprmf.h", "ncf.h", "mf.h", "bprfm.h", "sgns.h")]
 ARCH = os.environ.get("BPRMF_OFFLOAD_ARCH", "gfx950")
 

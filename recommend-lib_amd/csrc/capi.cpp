@@ -820,11 +820,6 @@ static int launch_steps(bprmf_handle* h, int64_t nb) {
   const BatchView v0 = BatchBuf{h->d_batch, B}.view(0);
   const int64_t stride = BatchBuf::stride_for(B);
   const StepBufs sb = step_bufs(h);
-#ifdef BPRMF_DIAG_OWNER
-  for (int64_t k = 0; k < nb; ++k)
-    HIPCHK(owner_diag_step(h->geom, v0, stride, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->stream));
-  return 0;
-#endif
   HIPCHK(user_step(h->geom, v0, B, h->P, h->Q, h->hp, h->d_tbase, 0, nullptr, nullptr, nullptr,
                    nullptr, h->stream, PeerWait{}, stride, &sb));
   if (int r = run_units(h, nb - 1, &base)) return r;

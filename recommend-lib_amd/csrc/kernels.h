@@ -249,10 +249,6 @@ hipError_t fused_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Tabl
                       const Hyper& hp, const int32_t* tbase, int step, const StepBufs& sb,
                       double* loss, int32_t* err, hipStream_t s);
 int item_long_blocks(int B);
-#ifdef BPRMF_DIAG_OWNER  // owner_step.hip: timing prototype (WRONG results), one launch per step
-hipError_t owner_diag_step(const Geom& g, BatchView bv0, int64_t bstride, int B, Table P, Table Q,
-                           const Hyper& hp, const int32_t* tbase, int step, hipStream_t s);
-#endif
 // relaxed-synchronisation (Hogwild) steps over n slots (hogwild.hip): triplets from the device
 // sampler (sa != null: slots slot0 .. slot0+n of `epoch`) or replayed device ids tu/ti/tj; slot s
 // belongs to step t0 + 1 + s / B; loss into kSegLossSlots slots

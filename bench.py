@@ -41,6 +41,11 @@ sys.path.insert(0, ROOT)
 
 U_ML20M, I_ML20M, NPOS_ML20M = 138493, 26744, 10_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# what `achieved` / `frac` divide by: this run's own HIP events around the step launches (a
+# process cannot read its own rocprofv3 summary; the same kernel's rocprofv3 averages, which run
+# ~3 % longer than the events, are in profiles/ and DESIGN.md §5)
+FRAC_BASIS = ("events: live HIP-event time per step of this run (rocprofv3 kernel averages of the "
+              "same command: profiles/, DESIGN.md §5)")
 
 
 def bytes_per_triplet(d):
@@ -101,7 +106,7 @@ def load_traffic(cfg_key):
     return e.get("hbm_bytes_per_step"), src
 
 
-def relaxed_local(rl, pos, U, I, d, B, seed, local_steps, steps, warmup):
+def relaxed_local(rl, pos, U, I, d, B, seed, local_steps, steps, warmup, traffic_key=None):
     """The opt-in relaxed mode (semantics="local") on the same workload, as a
     labelled sub-object of the exact line: its own model, warm-up and timed
     region (whole merge periods: `steps` >= 1024), live HIP-event roofline, its own PMC key.  NOT
@@ -135,13 +140,15 @@ def relaxed_local(rl, pos, U, I, d, B, seed, local_steps, steps, warmup):
     if kp and kp["step_graph"]["count"]:
         step_us = kp["step_graph"]["ms"] / kp["step_graph"]["count"] * 1e3
         ach = B * bytes_per_triplet(d) / (step_us * 1e-6) / 1e9
-        traffic, tsrc = (load_traffic(f"ml20m_d{d}_B{B}_local") if (U, I) == (U_ML20M, I_ML20M)
-                         else (None, None))
+        if traffic_key is None and (U, I) == (U_ML20M, I_ML20M):
+            traffic_key = f"ml20m_d{d}_B{B}_local"
+        traffic, tsrc = load_traffic(traffic_key) if traffic_key else (None, None)
         roof = dict(bound="hbm", kernel=("k_hogwild<LOCAL> (in-kernel sampling + gather + dots + "
                                          "sigmoid + SGD scatter, hot items in per-XCD replicas) + "
                                          "k_local_merge every period"),
                     achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
+                    frac=round(ach / HBM_PEAK_GBS, 4), frac_basis=FRAC_BASIS,
+                    traffic=traffic, traffic_source=tsrc,
                     algorithmic_bytes_per_step=B * bytes_per_triplet(d),
                     avg_us_per_step=round(step_us, 3))
     del m
@@ -153,6 +160,28 @@ def relaxed_local(rl, pos, U, I, d, B, seed, local_steps, steps, warmup):
             "timed_region": "one train_steps call per epoch segment, synchronised on both sides",
             "roofline": roof,
             "quality": "HR@10 / NDCG@10 against the exact step: DESIGN.md §5c, tools/hr_modes.py"}
+
+
+# the HBM-resident shape of the relaxed_local_hbm sub-object: tables of
+# (U + I) * d * 4 B = 1.54 GB at d = 128, 6x the 256 MiB Infinity Cache (MALL), so the rows come
+# from HBM rather than from the on-die cache that holds the ml-20m shape's 85 MB of tables
+U_HBM, I_HBM, NPOS_HBM = 2_000_000, 1_000_000, 20_000_000
+
+
+def relaxed_local_hbm(rl, syn, d, B, seed, local_steps, steps, warmup):
+    """relaxed_local at an HBM-resident shape: its own positives (synthetic.make_positives of
+    (U_HBM, I_HBM, NPOS_HBM)), model, warm-up, timed region and event roofline.  NOT the
+    reference step, never the headline."""
+    t0 = time.perf_counter()
+    pos = syn.make_positives(U_HBM, I_HBM, NPOS_HBM, seed + 1)
+    r = relaxed_local(rl, pos, U_HBM, I_HBM, d, B, seed, local_steps, steps, warmup,
+                      traffic_key=f"hbm2m1m_d{d}_B{B}_local")
+    r["config"] = {"users": U_HBM, "items": I_HBM, "positives": int(len(pos)), "factor_num": d,
+                   "batch_size": B, "table_bytes": (U_HBM + I_HBM) * d * 4,
+                   "mall_bytes": 256 << 20,
+                   "why": "tables 6x the 256 MiB Infinity Cache: rows served from HBM"}
+    r["wall_s"] = round(time.perf_counter() - t0, 1)
+    return r
 
 
 def main():
@@ -368,7 +397,7 @@ def main():
                 tsrc = ("none: no rocprofv3 --pmc pass has counted the sharded kernels at this world "
                         "size (a single-GPU figure would describe other kernels)")
             roof = dict(bound="hbm", kernel=what, achieved=round(ach, 1), peak=HBM_PEAK_GBS,
-                        unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                        unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), frac_basis=FRAC_BASIS,
                         traffic=traffic, traffic_source=tsrc,
                         algorithmic_bytes_per_launch=B * bytes_per_triplet(d),
                         avg_us_per_step=round(step_us, 3),
@@ -389,12 +418,14 @@ def main():
                             if not dpi else
                             "grad_bytes: the item-table merges' all-reduce, 2(W-1)/W of the table per "
                             "merge per rank (a ring's volume), averaged per step")}
-        rlx = None
+        rlx = rlx_hbm = None
         if (world == 1 and not sharded and a.semantics == "exact" and a.step == "segmented"
                 and not a.no_relaxed):
             del m  # the exact model's tables and buffers are not needed any more
             rlx = relaxed_local(rl, pos, U, I, d, B, a.seed, a.local_steps or 128,
                                 max(1024, a.relaxed_steps), 256)
+            rlx_hbm = relaxed_local_hbm(rl, syn, d, B, a.seed, a.local_steps or 128,
+                                        max(1024, a.relaxed_steps), 256)
         cpu = None
         if not a.no_cpu_baseline and world == 1 and not sharded:
             cpu = cpu_baseline(pos, U, I, d, B)
@@ -431,6 +462,8 @@ def main():
                "roofline": roof, "cpu_baseline": cpu}
         if rlx is not None:
             out["relaxed_local"] = rlx
+        if rlx_hbm is not None:
+            out["relaxed_local_hbm"] = rlx_hbm
         if sharded:
             out["exchange"] = xch
         print(json.dumps(out), flush=True)

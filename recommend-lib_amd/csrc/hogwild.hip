@@ -40,15 +40,25 @@
 
 namespace bprmf {
 
-// 16-byte row load past this CU's L1: a non-temporal load (global_load_dwordx4 ... nt) is served
-// by the XCD's L2 (MI355X_MICROARCH.md: sc1 / nt loads bypass L1 only), and the L2 drops every
-// line the XCD stores sc1.  A plain load may hit a line this CU cached long ago: a hot row's, or
-// its stamp's, and a stale stamp then decays the row again on every touch.  (A compiler builtin,
-// so the loads stay visible to its wait counting.)
+// 16-byte row load.  NT: past this CU's L1, a non-temporal load (global_load_dwordx4 ... nt)
+// served by the XCD's L2 (MI355X_MICROARCH.md: sc1 / nt loads bypass L1 only; the L2 drops every
+// line the XCD stores sc1); else a plain load, which may hit a line this CU cached a little
+// earlier (a relaxed read; the stamps are always sc1 loads, so a row is never decayed twice).
+// Measured (round 6, tools/gpu/ab_bench.sh, profiles/r06_hogwild_nt_ab.txt): the local mode at the
+// ml-20m shape (tables in the 256 MiB Infinity Cache) 2.62 us per step with plain loads, 3.16
+// with nt; at a 1.5 GB shape (HBM) 2.90 plain, 2.78 nt.  So nt only when the tables exceed the
+// Infinity Cache (hogwild() below).  Rounds 4-5 built one kernel with both forms behind a
+// runtime flag, and the compiler merged them into plain loads: their measurements are the
+// plain form.  (A compiler builtin, so the loads stay visible to its wait counting.)
+template <bool NT>
 static __device__ __forceinline__ float4 hw_ld4(const float* p) {
   typedef float v4f __attribute__((ext_vector_type(4)));
-  const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-  return make_float4(x[0], x[1], x[2], x[3]);
+  if constexpr (NT) {
+    const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(x[0], x[1], x[2], x[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
 }
 static __device__ __forceinline__ int32_t hw_ld_word(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 dword load
@@ -122,7 +132,7 @@ static __device__ __forceinline__ int32_t hot_probe(const LocalArgs& la, int32_t
 }
 
 // issue the round starting at slot k0 of the wave's chunk (ids from the lanes that sampled them)
-template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false>
+template <int G4, int S, int UNR, int GPW, bool SERIAL, bool LOCAL = false, bool NT = false>
 static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int cnt, int32_t mu,
                                                int32_t mi, int32_t mj, const Table& P,
                                                const Table& Q, int ld, int sub, int gw,
@@ -143,9 +153,9 @@ static __device__ __forceinline__ void hw_load(HwRound<S, UNR>& R, int k0, int c
       const float* qj = (LOCAL && R.hj[r] >= 0 ? repx + (int64_t)R.hj[r] * ld : Q.W + (int64_t)R.jj[r] * ld) + 4 * sub;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        R.pu[r][k] = hw_ld4(pr + 4 * G4 * k);
-        R.vi[r][k] = hw_ld4(qi + 4 * G4 * k);
-        R.vj[r][k] = hw_ld4(qj + 4 * G4 * k);
+        R.pu[r][k] = hw_ld4<NT>(pr + 4 * G4 * k);
+        R.vi[r][k] = hw_ld4<NT>(qi + 4 * G4 * k);
+        R.vj[r][k] = hw_ld4<NT>(qj + 4 * G4 * k);
       }
       R.su[r] = hw_ld_word(P.stamp + R.uu[r]);
       // a replica row has no stamp: it is current within its period (the merge applies the
@@ -237,7 +247,7 @@ static __device__ __forceinline__ void hw_apply(HwRound<S, UNR>& R, int64_t base
 // Rounds are double-buffered: round k+1's loads are issued BEFORE round k's stores, so waiting
 // for them does not wait for round k's write-through acknowledgements (gfx9 counts stores in
 // vmcnt, in order with the loads).
-template <int G4, int S, bool SAMPLE, bool SERIAL, bool LOCAL = false>
+template <int G4, int S, bool SAMPLE, bool SERIAL, bool LOCAL = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoch, int64_t slot0,
                                                     const int32_t* __restrict__ tu,
                                                     const int32_t* __restrict__ ti,
@@ -296,21 +306,21 @@ __global__ __launch_bounds__(kBlock) void k_hogwild(SamplerArgs a, uint32_t epoc
     HwRound<S, UNR> A, Bf;
     if (SERIAL) {  // each triplet reads what the one before it stored: no prefetch
       for (int k0 = 0; k0 < cnt; k0 += STEP) {
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL, NT>(A, k0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
         hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, repx);
       }
       continue;
     }
-    hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
+    hw_load<G4, S, UNR, GPW, SERIAL, LOCAL, NT>(A, 0, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi, mhj, repx);
     for (int k0 = 0; k0 < cnt; k0 += 2 * STEP) {
       const bool more1 = k0 + STEP < cnt, more2 = k0 + 2 * STEP < cnt;
       if (more1)
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi,
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL, NT>(Bf, k0 + STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw, mhi,
                                                 mhj, repx);
       hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(A, base, k0, P, Q, hp, ld, t0, B, sub, gw, lacc, repx);
       if (!more1) break;
       if (more2)
-        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw,
+        hw_load<G4, S, UNR, GPW, SERIAL, LOCAL, NT>(A, k0 + 2 * STEP, cnt, mu, mi, mj, P, Q, ld, sub, gw,
                                                 mhi, mhj, repx);
       hw_apply<G4, S, UNR, GPW, SERIAL, LOCAL>(Bf, base, k0 + STEP, P, Q, hp, ld, t0, B, sub, gw, lacc,
                                                repx);
@@ -583,6 +593,8 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
     if (blocks > cap) blocks = cap;
   }
   const unsigned threads = serial ? 64 : kBlock;
+  // the row loads past L1 (nt) only for tables larger than the Infinity Cache (hw_ld4)
+  const bool nt = (P.rows + Q.rows) * (int64_t)g.ld * 4 > (256LL << 20);
   SamplerArgs a{};
   if (sa) a = *sa;
   if (lap) {  // semantics "local": the hot items in per-XCD replicas
@@ -594,6 +606,9 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
       else if (serial)
         k_hogwild<G4_, S_, false, true, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q,
                                                                    hp, g.ld, t0, B, tpw, loss, err, la, uw);
+      else if (sa && nt)
+        k_hogwild<G4_, S_, true, false, true, true><<<(unsigned)blocks, threads, 0, s>>>(
+            a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, la, uw);
       else if (sa)
         k_hogwild<G4_, S_, true, false, true><<<(unsigned)blocks, threads, 0, s>>>(
             a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, la, uw);
@@ -610,6 +625,9 @@ hipError_t hogwild(const Geom& g0, const SamplerArgs* sa, uint32_t epoch, int64_
     else if (serial)
       k_hogwild<G4_, S_, false, true><<<1, threads, 0, s>>>(a, epoch, slot0, tu, ti, tj, n, P, Q, hp,
                                                            g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
+    else if (sa && nt)
+      k_hogwild<G4_, S_, true, false, false, true><<<(unsigned)blocks, threads, 0, s>>>(
+          a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);
     else if (sa)
       k_hogwild<G4_, S_, true, false><<<(unsigned)blocks, threads, 0, s>>>(
           a, epoch, slot0, tu, ti, tj, n, P, Q, hp, g.ld, t0, B, tpw, loss, err, LocalArgs{}, uw);

@@ -251,6 +251,39 @@ def test_parallel_local_trains_ml100k_protocol(rl):
     assert 1.0 < ratio <= 1.5, ratio
 
 
+def test_local_window_moves_along_the_quality_frontier(rl, monkeypatch):
+    """BPRMF_HOGWILD_WINDOW, the knob of DESIGN.md §5c's speed / quality frontier: a smaller
+    in-flight window trains closer to the exact step.  F5 protocol, local mode: the final tables'
+    loss against the exact step's with the default window (min(U, I) = 943 triplets) and with 128
+    triplets in flight (one workgroup)."""
+    with open(os.path.join(GOLDEN, "hr_ndcg_ml100k.json")) as fh:
+        ref = json.load(fh)
+    f = np.load(os.path.join(GOLDEN, "hr_ndcg_ml100k.npz"))
+    p = ref["protocol"]
+    pos = f["positives"].astype(np.int64)
+    U, I = int(f["U"]), int(f["I"])
+    g = np.random.default_rng(8)
+    k = g.integers(0, len(pos), 200_000)
+    u, i, j = pos[k, 0], pos[k, 1], g.integers(0, I, 200_000)
+
+    def fit_loss(semantics, window=None):
+        if window:
+            monkeypatch.setenv("BPRMF_HOGWILD_WINDOW", str(window))
+        else:
+            monkeypatch.delenv("BPRMF_HOGWILD_WINDOW", raising=False)
+        m = rl.BPRMF(U, I, p["factor_num"], lr=p["lr"], wd=p["wd"], batch_size=p["batch_size"],
+                     num_ng=p["num_ng"], seed=11, semantics=semantics)
+        m.fit(pos, epochs=p["epochs"])
+        xs = m.score(u, i).astype(np.float64) - m.score(u, j).astype(np.float64)
+        return float(np.logaddexp(0.0, -xs).mean())
+
+    exact = fit_loss("exact")
+    wide, narrow = fit_loss("local") / exact, fit_loss("local", 128) / exact
+    print("local / exact final-table loss on F5, default window:", wide, "128 in flight:", narrow)
+    assert narrow < wide - 0.05, (narrow, wide)
+    assert narrow < 1.25, narrow
+
+
 def test_local_sharded_handle_holds_every_item(rl):
     """semantics "local" at world > 1 (tests/test_gpu_local_dp.py): the rank keeps
     its users' rows and the whole item table, and trains through the runner only."""

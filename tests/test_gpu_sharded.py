@@ -234,6 +234,37 @@ def test_runner_sampler_matches_python_orchestration_and_is_reproducible(rl, gol
             np.testing.assert_allclose(x, z, rtol=1e-5, atol=1e-6)
 
 
+def test_world1_runner_equals_single_gpu_path(rl, golden, monkeypatch):
+    """At one rank train_steps runs the single-GPU fused step (nothing to exchange);
+    BPRMF_DIST_W1_RUNNER=1 keeps the sharded runner (owner gather, K1 on the gathered rows, K2's
+    per-slot gradients, owner apply), which tools/gpu/stale1_parts.sh measures.  Both take the same
+    steps from the same sampler stream: equal to fp32 summation-order tolerance, losses too."""
+    f = golden("bpr_ml100k_replay.npz")
+    pos = f["positives"].astype(np.int64)
+    Uu, Ii = int(f["U"]), int(f["I"])
+    B, seed, d = 1024, 13, 64
+    sh = rl.sharded
+    outs = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("BPRMF_DIST_W1_RUNNER", env)
+
+        def runner(comm, r, key):
+            m = sh.ShardedBPRMF(Uu, Ii, d, batch_size=B, seed=seed, device=0, comm=comm)
+            S = m.set_train(pos)
+            m.attach_runner("loopback", key=key)
+            a = m.train_steps(0, 0, S)
+            b = m.train_steps(1, 3, 9)
+            return m.get_weights(), a["loss"] + b["loss"]
+
+        key = 4100 + int(env)
+        outs.append(_runner_threads(rl, 1, key, lambda c, r: runner(c, r, key))[0])
+    (Pa, Qa), la = outs[0]
+    (Pb, Qb), lb = outs[1]
+    np.testing.assert_allclose(Pa, Pb, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Qa, Qb, rtol=1e-5, atol=1e-6)
+    assert la == pytest.approx(lb, rel=1e-5)
+
+
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_runner_split_builder_equals_one_workgroup_build(rl, golden, monkeypatch, world):
     """The runner's batches (owner-major item slots, padded per owner) from the split builder (one

@@ -20,7 +20,9 @@ for r in $(seq 1 "$reps"); do
     echo "$name $r $(grep '^{' "$out/bench_${name}_$r.log" | python3 -c '
 import json, sys
 d = json.loads(sys.stdin.read())
-parts = ["exact %.4ge8 %.2f us/step fused %.3f" % (d["value"] / 1e8, d["ms_per_step"] * 1e3, d["roofline"]["avg_us_per_step"])]
+parts = ["exact %.4ge8 %.2f us/step" % (d["value"] / 1e8, d["ms_per_step"] * 1e3)]
+if d.get("roofline"):
+    parts[0] += " kernels %.3f" % d["roofline"]["avg_us_per_step"]
 for k in ("relaxed_local", "relaxed_local_hbm"):
     if k in d:
         parts.append("%s %.4ge9 %.3f us/step frac %.3f" % (k, d[k]["value"] / 1e9, d[k]["ms_per_step"] * 1e3, d[k]["roofline"]["frac"]))

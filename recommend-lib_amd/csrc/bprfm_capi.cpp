@@ -155,15 +155,15 @@ int bprfm_create(const bprfm_config* cfg, bprfm_handle** out) {
 
 int bprfm_destroy(bprfm_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->cfg.device);
-  if (h->stream) hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* ptrs[] = {h->E,  h->acc_E, h->GE,     h->b,    h->acc_b, h->Gb,   h->stamp, h->bn,
                   h->bias_, h->X, h->stats, h->stats2, h->cbuf, h->mask, h->part, h->loss, h->lpart, h->trip};
   for (void* p : ptrs)
-    if (p) hipFree(p);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
-  if (h->stream) hipStreamDestroy(h->stream);
+    if (p) (void)hipFree(p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
 }
@@ -270,7 +270,7 @@ int bprfm_dropout_mask(bprfm_handle* h, int32_t B, float* out) {
   hipError_t e = fm::dropout_mask(args_of(h, B), d, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(out, d, 4 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  hipFree(d);
+  (void)hipFree(d);
   if (e != hipSuccess) return fail(BPRMF_E_HIP, "bprfm_dropout_mask: %s", hipGetErrorString(e));
   return 0;
 }
@@ -287,7 +287,7 @@ int bprfm_predict(bprfm_handle* h, const int32_t* u, const int32_t* x, int64_t n
   float* dout = nullptr;
   HIPCHK(hipMalloc((void**)&d, 8 * (size_t)n));
   if (hipMalloc((void**)&dout, 4 * (size_t)n) != hipSuccess) {
-    hipFree(d);
+    (void)hipFree(d);
     return fail(BPRMF_E_HIP, "hipMalloc failed");
   }
   hipStream_t s = h->stream;
@@ -296,8 +296,8 @@ int bprfm_predict(bprfm_handle* h, const int32_t* u, const int32_t* x, int64_t n
   if (e == hipSuccess) e = fm::predict(args_of(h, 0), d, d + n, n, dout, s);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, 4 * n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  hipFree(d);
-  hipFree(dout);
+  (void)hipFree(d);
+  (void)hipFree(dout);
   if (e != hipSuccess) return fail(BPRMF_E_HIP, "bprfm_predict: %s", hipGetErrorString(e));
   return 0;
 }

@@ -237,10 +237,10 @@ int bprmf_create(const bprmf_config* cfg, bprmf_handle** out) {
 
 int bprmf_destroy(bprmf_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->cfg.device);
-  if (h->own_stream) hipStreamSynchronize(h->own_stream);
+  (void)hipSetDevice(h->cfg.device);
+  if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   // a caller's stream is drained too before anything is freed
-  if (h->stream && h->stream != h->own_stream) hipStreamSynchronize(h->stream);
+  if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   void* ptrs[] = {h->P.W, h->P.G, h->P.stamp, h->Q.W, h->Q.G, h->Q.stamp, h->d_pos_u, h->d_pos_i,
                   h->d_indptr, h->d_indices, h->d_trip, h->d_status,
                   h->d_batch, h->d_contrib, h->d_ugrad, h->d_xloss, h->d_tbase,
@@ -248,12 +248,12 @@ int bprmf_destroy(bprmf_handle* h) {
                   h->d_skeys, h->d_qbase, h->d_qdelta, h->d_qsum, h->d_pos2, h->d_urec,
                   h->d_pos4};
   for (void* p : ptrs)
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
   drop_graphs(h);
   dist_free(h->dist);
-  for (hipEvent_t e : h->prof_pool) hipEventDestroy(e);
-  if (h->h_status) hipHostFree(h->h_status);
-  if (h->own_stream) hipStreamDestroy(h->own_stream);
+  for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
+  if (h->h_status) (void)hipHostFree(h->h_status);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return 0;
 }
@@ -718,7 +718,7 @@ extern "C" {
 // graphs left it.  Shorter chunks launch every unit eagerly.
 static void drop_graphs(bprmf_handle* h) {
   for (auto& ge : h->graphs)
-    if (ge.exec) hipGraphExecDestroy(ge.exec);
+    if (ge.exec) (void)hipGraphExecDestroy(ge.exec);
   h->graphs.clear();
 }
 
@@ -750,13 +750,13 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
   hipGraph_t graph = nullptr;
   const hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
   if (rc || e2 != hipSuccess) {
-    if (graph) hipGraphDestroy(graph);
+    if (graph) (void)hipGraphDestroy(graph);
     return rc ? rc : fail(BPRMF_E_HIP, "step graph capture: %s", hipGetErrorString(e2));
   }
   out->n = n;
   out->advance = advance;
   const hipError_t e = hipGraphInstantiate(&out->exec, graph, nullptr, nullptr, 0);
-  hipGraphDestroy(graph);
+  (void)hipGraphDestroy(graph);
   if (e != hipSuccess) {
     out->exec = nullptr;
     return fail(BPRMF_E_HIP, "step graph instantiate: %s", hipGetErrorString(e));
@@ -764,7 +764,7 @@ static int capture_step_graph(bprmf_handle* h, int64_t n, bool advance, StepGrap
   // the executable graph's device-side setup now (set_train) rather than inside its first replay
   const hipError_t eu = hipGraphUpload(out->exec, h->stream);
   if (eu != hipSuccess) {  // the caller never keeps a failed graph: destroy it here
-    hipGraphExecDestroy(out->exec);
+    (void)hipGraphExecDestroy(out->exec);
     out->exec = nullptr;
     return fail(BPRMF_E_HIP, "step graph upload: %s", hipGetErrorString(eu));
   }
@@ -1092,7 +1092,7 @@ int bprmf_sample(bprmf_handle* h, uint32_t epoch, int64_t first, int64_t n, int3
   if (e == hipSuccess) e = hipMemcpyAsync(j, buf + 2 * n, 4 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "sample: %s", hipGetErrorString(e));
-  hipFree(buf);
+  (void)hipFree(buf);
   if (rc) return rc;
   return check_err_flag(h);
 }
@@ -1163,7 +1163,7 @@ int bprmf_get_rows(bprmf_handle* h, int32_t table, const int32_t* rows, int64_t 
   if (e == hipSuccess) e = hipMemcpy2DAsync(out, D * 4, o, ld * 4, D * 4, n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "get_rows: %s", hipGetErrorString(e));
-  hipFree(buf);
+  (void)hipFree(buf);
   if (rc) return rc;
   return check_err_flag(h);
 }
@@ -1187,7 +1187,7 @@ int bprmf_score(bprmf_handle* h, const int32_t* u, const int32_t* i, int64_t n, 
   if (e == hipSuccess) e = hipMemcpyAsync(out, o, 4 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "score: %s", hipGetErrorString(e));
-  hipFree(buf);
+  (void)hipFree(buf);
   if (rc) return rc;
   return check_err_flag(h);
 }
@@ -1241,7 +1241,7 @@ int bprmf_topk_lists(bprmf_handle* h, const int32_t* users, const int64_t* offse
   if (e == hipSuccess) e = hipMemcpyAsync(out_score, d_score, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "topk_lists: %s", hipGetErrorString(e));
-  hipFree(buf);
+  (void)hipFree(buf);
   if (rc) return rc;
   return check_err_flag(h);
 }
@@ -1276,7 +1276,7 @@ int bprmf_topk_all(bprmf_handle* h, const int32_t* users, int64_t n_users, int32
   if (e == hipSuccess) e = hipMemcpyAsync(out_scores, d_scores, 4 * n_users * (int64_t)k, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "topk_all: %s", hipGetErrorString(e));
-  hipFree(buf);
+  (void)hipFree(buf);
   return rc;
 }
 

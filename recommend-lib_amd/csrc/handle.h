@@ -153,13 +153,13 @@ struct ProfScope {
   int kind;
   hipEvent_t a = nullptr;
   ProfScope(bprmf_handle* hh, int k, bool sampled = true) : h(hh), kind(k) {
-    if (h->prof_on && sampled && (a = prof_event(h))) hipEventRecord(a, h->stream);
+    if (h->prof_on && sampled && (a = prof_event(h))) (void)hipEventRecord(a, h->stream);
   }
   ~ProfScope() {
     if (!a) return;
     hipEvent_t b = prof_event(h);
     if (!b) return;
-    hipEventRecord(b, h->stream);
+    (void)hipEventRecord(b, h->stream);
     h->prof_rec[kind].push_back({a, b});
   }
 };

@@ -170,15 +170,15 @@ int mf_create(const mf_config* cfg, mf_handle** out) {
 
 int mf_destroy(mf_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->cfg.device);
-  if (h->stream) hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* ptrs[] = {h->P,  h->Q,    h->bu,   h->bi,     h->su,   h->si,  h->sr,
                   h->loff, h->d_err, h->Y, h->uoff, h->uitems, h->udup, h->uslot};
   for (void* p : ptrs)
-    if (p) hipFree(p);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
-  if (h->stream) hipStreamDestroy(h->stream);
+    if (p) (void)hipFree(p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
 }
@@ -303,8 +303,8 @@ int mf_predict(mf_handle* h, const int32_t* users, const int32_t* items, int64_t
   double* dout = nullptr;
   int rc = 0;
   if ((rc = malloc_dev(&du, n)) || (rc = malloc_dev(&di, n)) || (rc = malloc_dev(&dout, n))) {
-    hipFree(du);
-    hipFree(di);
+    (void)hipFree(du);
+    (void)hipFree(di);
     return rc;
   }
   hipError_t e = hipMemcpyAsync(du, users, 4 * n, hipMemcpyHostToDevice, h->stream);
@@ -316,12 +316,12 @@ int mf_predict(mf_handle* h, const int32_t* users, const int32_t* items, int64_t
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, 8 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(&bad, h->d_err, 4, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  hipFree(du);
-  hipFree(di);
-  hipFree(dout);
+  (void)hipFree(du);
+  (void)hipFree(di);
+  (void)hipFree(dout);
   if (e != hipSuccess) return fail(BPRMF_E_HIP, "mf_predict: %s", hipGetErrorString(e));
   if (bad) {
-    hipMemset(h->d_err, 0, 4);
+    (void)hipMemset(h->d_err, 0, 4);
     return fail(BPRMF_E_RANGE, "Invalid user or item code");
   }
   return 0;

@@ -76,13 +76,13 @@ struct NcfProf {  // event pair around a launch while profiling
   int kind;
   hipEvent_t a = nullptr;
   NcfProf(ncf_handle* hh, int k) : h(hh), kind(k) {
-    if (h->prof_on && (a = ncf_event(h))) hipEventRecord(a, h->stream);
+    if (h->prof_on && (a = ncf_event(h))) (void)hipEventRecord(a, h->stream);
   }
   ~NcfProf() {
     if (!a) return;
     hipEvent_t b = ncf_event(h);
     if (!b) return;
-    hipEventRecord(b, h->stream);
+    (void)hipEventRecord(b, h->stream);
     h->prof[kind].push_back({a, b});
   }
 };

@@ -159,16 +159,16 @@ int sgns_create(const sgns_config* cfg, sgns_handle** out) {
 
 int sgns_destroy(sgns_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->cfg.device);
-  if (h->stream) hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* ptrs[] = {h->GOp, h->I,  h->O,    h->mI,   h->vI,      h->mO,      h->vO, h->GI, h->GO, h->S,
                   h->IB, h->lbuf, h->cdf, h->touch_i, h->touch_o, h->ex, h->loss};
   for (void* p : ptrs)
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
   if (h->blas) rocblas_destroy_handle(h->blas);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
-  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
 }
@@ -359,7 +359,7 @@ int sgns_negatives(sgns_handle* h, int32_t B, int32_t* out) {
   hipError_t e = sgns::negatives(args_of(h, B), d, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(out, d, 4 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  hipFree(d);
+  (void)hipFree(d);
   if (e != hipSuccess) return fail(BPRMF_E_HIP, "sgns_negatives: %s", hipGetErrorString(e));
   return 0;
 }
@@ -375,15 +375,15 @@ int sgns_lookup(sgns_handle* h, int32_t which, const int32_t* idx, int64_t n, fl
   float* dout = nullptr;
   HIPCHK(hipMalloc((void**)&d, 4 * (size_t)n));
   if (hipMalloc((void**)&dout, 4 * (size_t)n * E) != hipSuccess) {
-    hipFree(d);
+    (void)hipFree(d);
     return fail(BPRMF_E_HIP, "hipMalloc failed");
   }
   hipError_t e = hipMemcpyAsync(d, idx, 4 * n, hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess) e = sgns::lookup(which ? h->O : h->I, h->ld, E, d, n, dout, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, 4 * n * E, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  hipFree(d);
-  hipFree(dout);
+  (void)hipFree(d);
+  (void)hipFree(dout);
   if (e != hipSuccess) return fail(BPRMF_E_HIP, "sgns_lookup: %s", hipGetErrorString(e));
   return 0;
 }

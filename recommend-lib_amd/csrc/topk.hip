@@ -4,19 +4,18 @@
 // forward per candidate, then np.argsort(pred)[::-1][:K]) and the validation protocol
 // (util/metrics.py:46-66: forward of a [gt, negatives] batch, torch.topk).  One workgroup per
 // user: lane groups score the user's candidates into LDS with exactly the arithmetic of k_score
-// (so scores equal BPRMF.score/forward bit for bit), then a block radix sort over 64-bit keys
+// (so scores equal BPRMF.score/forward bit for bit), then a bitonic sort in LDS over 64-bit keys
 // (~orderable(score) << 32 | ~position) takes the top K: score descending, ties by LATER position
 // first, i.e. np.argsort(s)[::-1] on a stable sort.  Lists longer than one pass are handled in
 // passes carrying the current top K.
-#include <rocprim/block/block_radix_sort.hpp>
-
 #include "device_common.h"
 
 namespace bprmf {
 
 constexpr int kTopkThreads = 256;
 constexpr int kTopkIPT = 8;
-constexpr int kTopkPass = kTopkThreads * kTopkIPT;  // keys sorted per pass (carried top K included)
+constexpr int kTopkPass = kTopkThreads * kTopkIPT;  // keys per pass (carried top K included)
+static_assert((kTopkPass & (kTopkPass - 1)) == 0, "bitonic passes: a power of two");
 constexpr int kTopkMaxK = 256;
 
 static __device__ __forceinline__ uint32_t ord_desc(float x) {  // smaller key = larger score
@@ -29,13 +28,31 @@ static __device__ __forceinline__ float from_ord_desc(uint32_t k) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
 
+// ascending bitonic sort of the first N keys in LDS (N a power of two <= kTopkPass, every valid
+// key among them; the rest of s are ~0 padding): log2 N (log2 N + 1) / 2 compare-exchange stages
+// (66 at N = 2048, 28 for a 100-candidate list), each thread taking N / 2 / kTopkThreads pairs
+// per stage.  The keys are distinct (each carries its position), so the order is the one any
+// sort gives: the same top K as the block radix sort over all kTopkPass keys it replaced (round 6).
+static __device__ __forceinline__ void bitonic_sort(uint64_t* s, int N) {
+  for (int k = 2; k <= N; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int q = threadIdx.x; q < N / 2; q += kTopkThreads) {
+        const int i = 2 * q - (q & (j - 1));  // the pair's lower index (bit j clear)
+        const uint64_t a = s[i], b = s[i + j];
+        if ((a > b) == ((i & k) == 0)) {
+          s[i] = b;
+          s[i + j] = a;
+        }
+      }
+      __syncthreads();
+    }
+}
+
 template <int G, int EPL>
 __global__ __launch_bounds__(kTopkThreads) void k_topk_lists(
     const int32_t* __restrict__ users, const int64_t* __restrict__ offs,
     const int32_t* __restrict__ items, int k, Table P, Table Q, Hyper hp, int ld, int32_t T,
     int32_t* __restrict__ out_pos, float* __restrict__ out_score, int32_t* __restrict__ err) {
-  using Sort = rocprim::block_radix_sort<uint64_t, kTopkThreads, kTopkIPT>;
-  __shared__ typename Sort::storage_type ssort;
   __shared__ uint64_t s_key[kTopkPass];
   __shared__ uint64_t s_top[kTopkMaxK];
   constexpr int NG = kTopkThreads / G;
@@ -76,17 +93,10 @@ __global__ __launch_bounds__(kTopkThreads) void k_topk_lists(
     for (int x = m + threadIdx.x; x < kTopkPass; x += kTopkThreads)
       s_key[x] = x - m < carried ? s_top[x - m] : ~0ull;
     __syncthreads();
-    uint64_t key[kTopkIPT];
-#pragma unroll
-    for (int e = 0; e < kTopkIPT; ++e) key[e] = s_key[threadIdx.x * kTopkIPT + e];
-    __syncthreads();
-    Sort().sort(key, ssort);
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < kTopkIPT; ++e) {
-      const int x = threadIdx.x * kTopkIPT + e;
-      if (x < k) s_top[x] = key[e];
-    }
+    int npass = 64;  // the pass's valid keys (this pass's m + the carried top K), rounded up
+    while (npass < m + carried) npass <<= 1;
+    bitonic_sort(s_key, npass);
+    for (int x = threadIdx.x; x < k; x += kTopkThreads) s_top[x] = s_key[x];
     carried = (int)min<int64_t>(k, c0 + m);
     __syncthreads();
     if (n == 0) break;

@@ -67,9 +67,10 @@ int ncf_sample(ncf_handle* h, uint32_t epoch, int64_t first, int64_t n, int32_t*
                float* y);
 /* NCF.forward(user, item) -> prediction logits (NCFRecommender.py:103-124) */
 int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, float* out);
-/* embedding rows Adam steps every step from now on: rows with a nonzero moment (ever touched) */
+/* embedding rows Adam steps every step from now on: rows with a nonzero moment (ever touched).
+ * (Their zero-gradient steps are applied lazily, in closed form, before anything reads them.) */
 int ncf_active_rows(ncf_handle* h, int64_t* users, int64_t* items);
-/* live timing: kinds 0 sample, 1 forward/backward, 2 Adam (bprmf_kprof) */
+/* live timing: kinds 0 sample, 1 forward/backward, 2 Adam, 3 catch-up of the rows read (bprmf_kprof) */
 int ncf_profile(ncf_handle* h, int32_t enable);
 int ncf_profile_read(ncf_handle* h, bprmf_kprof* out);
 

@@ -9,10 +9,12 @@
 //                 dimension of every layer), the prediction and dL/dz, then the tower backward:
 //                 dW partial tiles per workgroup (summed in fixed order by the Adam kernel),
 //                 dX = dPre . W through the transposed weight copies, and the embedding
-//                 gradients as f32 atomics into dense gradient rows (+ a touched-step stamp).
-//   k_ncf_adam_rows  Adam over an embedding table: a row never touched has m = v = 0 and no
-//                 update (skipped); every other row is stepped with g = its gradient row (this
-//                 step) or 0 — torch's dense Adam exactly, HBM-bound (p, m, v read + written).
+//                 gradients as f32 atomics into dense gradient rows.
+//   k_ncf_catch_up / k_ncf_adam_rows  torch's dense Adam over the embedding tables, done lazily:
+//                 every row with a nonzero moment moves every step, but a step with g = 0 has a
+//                 closed form, so a row is brought up to date only when something reads it (the
+//                 step that gathers it, a predict, a parameter copy) and Adam proper runs on the
+//                 batch's rows alone.  Equal to the dense sweep up to f32 rounding.
 //   k_ncf_adam_flat  Adam over the tower + predict layer, g = sum of the workgroups' partials in
 //                 workgroup order; weights also written transposed for the next backward.
 #include <algorithm>
@@ -87,6 +89,18 @@ static __device__ __forceinline__ f32x4 tile_xwt(const float* X, int ldx, const 
   return acc;
 }
 
+// BPRMF_NCF_PHASES (diagnostic builds only): workgroup 0 of step 100 prints its phase times
+#ifdef BPRMF_NCF_PHASES
+#define NCF_PH(k)                                 \
+  do {                                            \
+    if (threadIdx.x == 0) s_ph[k] = wall_clock64(); \
+  } while (0)
+#else
+#define NCF_PH(k) \
+  do {            \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
                                                      const int32_t* __restrict__ us,
                                                      const int32_t* __restrict__ is,
@@ -96,6 +110,11 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
                                                      int32_t* __restrict__ err,
                                                      float* __restrict__ zout) {
   extern __shared__ float sm[];
+#ifdef BPRMF_NCF_PHASES
+  __shared__ uint64_t s_ph[24];
+  if (threadIdx.x < 24) s_ph[threadIdx.x] = 0;
+  NCF_PH(0);
+#endif
   const Lds Lp = lds_plan(D);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = 16;
@@ -125,6 +144,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
     sy[tid] = y;
   }
   __syncthreads();
+  NCF_PH(1);
   // 2. gathers (float4): GMF rows and the tower input [Pm[u], Qm[i]]
   if (gmf) {
     const int q = d / 4;
@@ -152,6 +172,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
     }
   }
   __syncthreads();
+  NCF_PH(2);
   // 3. tower forward: h_l = relu(h_{l-1} W_l^T + b_l)
   if (mlp) {
     for (int l = 0; l < D.L; ++l) {
@@ -171,6 +192,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
         }
       }
       __syncthreads();
+      NCF_PH(3 + l);
     }
   }
   // 4. prediction z = [gmf, h_L] . wp + bp and dL/dz of the mean BCE-with-logits loss
@@ -201,6 +223,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
     }
   }
   __syncthreads();
+  NCF_PH(7);
   if (zout) return;  // forward only (ncf_predict)
   // 5. predict-layer gradients (workgroup partials, samples in order) and dX of the predictor
   float* part = partial + (int64_t)blockIdx.x * D.flat_n;
@@ -222,6 +245,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
     }
   }
   __syncthreads();  // hL (read above as x) is overwritten below by dPre_L
+  NCF_PH(8);
   if (gmf) {  // dPg[u] += dz wp_k Qg[i]_k ; dQg[i] += dz wp_k Pg[u]_k
     for (int x = tid; x < kSamples * d; x += blockDim.x) {
       const int s = x / d, k = x % d;
@@ -241,6 +265,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
       hw[s * ldL + k] = h > 0.f ? sz[s] * P.wp[(gmf ? d : 0) + k] : 0.f;
     }
     __syncthreads();
+    NCF_PH(9);
     for (int l = D.L - 1; l >= 0; --l) {
       const int K = D.nin[l], N = D.nout[l];
       const float* dP = sm + Lp.h[l + 1];  // dPre_l [16 x N]
@@ -275,6 +300,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
         part[D.off_b[l] + nn] = acc;
       }
       __syncthreads();
+      NCF_PH(10 + 2 * (D.L - 1 - l));
       // (b) dX [16 x K] = dPre . W_l  (B operand from the transposed copy WT_l [K x N])
       for (int tile = wave; 16 * tile < K; tile += NW) {
         const f32x4 acc = tile_xwt(dP, ldp, P.WT[l], N, 16 * tile, K, lane);
@@ -290,6 +316,7 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
         }
       }
       __syncthreads();
+      NCF_PH(11 + 2 * (D.L - 1 - l));
     }
     // embedding gradients of the tower input: dPm[u] += dX0[:E], dQm[i] += dX0[E:]
     const float* X0 = sm + Lp.h[0];
@@ -304,10 +331,13 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
         atomicAdd(G.Qm + (int64_t)i * E + (k - E), v);
     }
   }
-  if (tid < kSamples && su[tid] >= 0) {
-    G.touch_u[su[tid]] = t;
-    G.touch_i[si[tid]] = t;
-  }
+#ifdef BPRMF_NCF_PHASES
+  __syncthreads();
+  NCF_PH(20);
+  if (threadIdx.x == 0 && blockIdx.x == 0 && t == 100)
+    for (int k = 1; k <= 20; ++k)
+      if (s_ph[k]) printf("ncf phase %d: %.2f us\n", k, (double)(s_ph[k] - s_ph[0]) * 1e-2);
+#endif
 }
 
 // torch Adam (single-tensor form): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
@@ -318,32 +348,99 @@ static __device__ __forceinline__ void adam1(float& p, float& m, float& v, float
   p = p - a.step_size * (m / (sqrtf(v) / a.bc2_sqrt + a.eps));
 }
 
-__global__ __launch_bounds__(256) void k_ncf_adam_rows(float* __restrict__ W, float* __restrict__ M,
-                                                       float* __restrict__ V, float* __restrict__ Gr,
-                                                       const int32_t* __restrict__ touch,
-                                                       int64_t rows, int dim, int32_t t, AdamArgs a) {
-  const int q = dim / 4;
-  const int64_t total = rows * q;
-  const bool narrow = total < (1LL << 31);  // 32-bit row division (a 64-bit one costs ~40 VALU)
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-       x += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = narrow ? (int64_t)((uint32_t)x / (uint32_t)q) : x / q;
-    const int32_t st = touch[r];
-    if (st < 0) continue;  // never touched: m = v = 0, torch's step leaves it unchanged
-    const int64_t e = r * dim + 4 * (x - r * q);
-    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (st == t) {
-      g = ld4(Gr + e);
-      *reinterpret_cast<float4*>(Gr + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+// ---- lazy row Adam ---------------------------------------------------------------------------
+// Steps s = c+1 .. e with g = 0 from a row's state (p, m, v) at step c (j = s - c):
+//   m_s = b1^j m,  v_s = b2^j v,
+//   p_e = p - m * sum_j a_j / (sqrt(v) w_j + eps),  a_j = step_size(s) b1^j,  w_j = b2^(j/2) / bc2_sqrt(s)
+// (torch's step_size(s) = lr / (1 - b1^s), bc2_sqrt(s) = sqrt(1 - b2^s)).  A term is at most
+// (b1 / sqrt(b2))^j (1 / bc2_sqrt(c+1)) times the first (0.9005^j x <= 32 at the defaults), so
+// the sum stops after kCatchTerms terms: 32 x 0.9005^192 < 6e-8 of the first term.  The per-step
+// and per-term factors come from tables built once on the host (in double).
+
+// one workgroup per (sample, side): thread 0 claims the row (cur: c -> target by CAS, so a row
+// repeated in the batch is caught up once); row = blockIdx.x when the sides carry no ids
+static __device__ __forceinline__ int64_t side_row(const RowSides& R, int side) {
+  const int64_t x = blockIdx.x;
+  if (!R.ids[0]) return x < R.side[side].rows ? x : -1;
+  const int32_t u = R.ids[0][x], i = R.ids[1][x];
+  if ((uint64_t)u >= (uint64_t)R.U || (uint64_t)i >= (uint64_t)R.I) return -1;  // no gradient
+  return side ? i : u;
+}
+
+__global__ __launch_bounds__(1024) void k_ncf_catch_up(RowSides R, CatchArgs c) {
+  __shared__ float2 s_term[kCatchTerms];
+  __shared__ int64_t s_row;
+  __shared__ int32_t s_from;
+
+  const int side = blockIdx.y;
+  const RowSide S = side ? R.side[1] : R.side[0];  // no dynamic index into the kernel arguments
+  if (threadIdx.x == 0) {
+    const int64_t r = side_row(R, side);
+    int32_t from = -1;
+    if (r >= 0) {
+      const int32_t old = S.cur[r];
+      if (old >= 0 && old < c.target && atomicCAS(S.cur + r, old, c.target) == old) from = old;
     }
-    float4 p = ld4(W + e), m = ld4(M + e), v = ld4(V + e);
-    adam1(p.x, m.x, v.x, g.x, a);
-    adam1(p.y, m.y, v.y, g.y, a);
-    adam1(p.z, m.z, v.z, g.z, a);
-    adam1(p.w, m.w, v.w, g.w, a);
-    *reinterpret_cast<float4*>(W + e) = p;
-    *reinterpret_cast<float4*>(M + e) = m;
-    *reinterpret_cast<float4*>(V + e) = v;
+    s_row = r;
+    s_from = from;
+  }
+  __syncthreads();
+  const int32_t from = s_from;
+  if (from < 0) return;
+  const int J = min(c.target - from, kCatchTerms);
+  for (int j = threadIdx.x + 1; j <= J; j += blockDim.x) {
+    const int64_t s = (int64_t)from + j;
+    const float2 st = s <= c.nstep ? c.step[s - 1] : make_float2(c.lr, 1.f), pw = c.pw[j - 1];
+    s_term[j - 1] = make_float2(st.x * pw.x, pw.y * st.y);
+  }
+  __syncthreads();
+  const int64_t r = s_row;
+  const float k = (float)(c.target - from);
+  const float dm = exp2f(k * c.log2_b1), dv = exp2f(k * c.log2_b2), eps = c.eps;
+  for (int e = threadIdx.x; e < S.cols[0] + S.cols[1]; e += blockDim.x) {
+    const int tb = e >= S.cols[0];
+    const int64_t x = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
+    const float m = S.M[tb][x], v = S.V[tb][x], sv = sqrtf(v);
+    float acc0 = 0.f, acc1 = 0.f;
+    int j = 0;
+    for (; j + 1 < J; j += 2) {
+      const float2 q0 = s_term[j], q1 = s_term[j + 1];
+      acc0 = fmaf(q0.x, __builtin_amdgcn_rcpf(fmaf(sv, q0.y, eps)), acc0);
+      acc1 = fmaf(q1.x, __builtin_amdgcn_rcpf(fmaf(sv, q1.y, eps)), acc1);
+    }
+    if (j < J) acc0 = fmaf(s_term[j].x, __builtin_amdgcn_rcpf(fmaf(sv, s_term[j].y, eps)), acc0);
+    S.W[tb][x] -= m * (acc0 + acc1);
+    S.M[tb][x] = m * dm;
+    S.V[tb][x] = v * dv;
+  }
+}
+
+// Adam step t on the batch's rows (the rows are at step t - 1 or never touched): g = the
+// gradient row (zeroed for the next step), cur = t; a row repeated in the batch is stepped once
+__global__ __launch_bounds__(1024) void k_ncf_adam_rows(RowSides R, int32_t t, AdamArgs a) {
+  __shared__ int64_t s_row;
+  const int side = blockIdx.y;
+  const RowSide S = side ? R.side[1] : R.side[0];  // no dynamic index into the kernel arguments
+  if (threadIdx.x == 0) {
+    int64_t r = side_row(R, side);
+    if (r >= 0) {
+      const int32_t old = S.cur[r];
+      if (old == t || atomicCAS(S.cur + r, old, t) != old) r = -1;
+    }
+    s_row = r;
+  }
+  __syncthreads();
+  const int64_t r = s_row;
+  if (r < 0) return;
+  for (int e = threadIdx.x; e < S.cols[0] + S.cols[1]; e += blockDim.x) {
+    const int tb = e >= S.cols[0];
+    const int64_t x = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
+    float p = S.W[tb][x], m = S.M[tb][x], v = S.V[tb][x];
+    adam1(p, m, v, S.G[tb][x], a);
+    S.G[tb][x] = 0.f;
+    S.W[tb][x] = p;
+    S.M[tb][x] = m;
+    S.V[tb][x] = v;
   }
 }
 
@@ -473,10 +570,23 @@ hipError_t forward(const Dims& D, const Params& P, const int32_t* u, const int32
   return hipGetLastError();
 }
 
-hipError_t adam_rows(float* W, float* M, float* V, float* Gr, const int32_t* touch, int64_t rows,
-                     int dim, int32_t t, const AdamArgs& a, hipStream_t s) {
-  if (rows <= 0) return hipSuccess;
-  k_ncf_adam_rows<<<grid1(rows * (dim / 4)), 256, 0, s>>>(W, M, V, Gr, touch, rows, dim, t, a);
+static dim3 rows_grid(const RowSides& R, int64_t n) {
+  return dim3((unsigned)(R.ids[0] ? n : std::max(R.side[0].rows, R.side[1].rows)), 2);
+}
+static unsigned rows_block(const RowSides& R) {
+  const int w = std::max(R.side[0].cols[0] + R.side[0].cols[1], R.side[1].cols[0] + R.side[1].cols[1]);
+  return (unsigned)std::min(1024, std::max(64, (w + 63) / 64 * 64));
+}
+
+hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_t s) {
+  if (c.target <= 0 || (R.ids[0] && n <= 0)) return hipSuccess;
+  k_ncf_catch_up<<<rows_grid(R, n), rows_block(R), 0, s>>>(R, c);
+  return hipGetLastError();
+}
+
+hipError_t adam_rows(const RowSides& R, int64_t n, int32_t t, const AdamArgs& a, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_ncf_adam_rows<<<rows_grid(R, n), rows_block(R), 0, s>>>(R, t, a);
   return hipGetLastError();
 }
 

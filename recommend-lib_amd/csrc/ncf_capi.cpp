@@ -2,11 +2,14 @@
 //
 // One handle = one GPU.  It owns, in HBM: the four embedding tables and the flat tower+predict
 // block (the reference's parameters), their Adam moments m and v, the dense embedding gradient
-// rows and per-row touched-step stamps, the transposed tower weights, the per-workgroup gradient
+// rows and per-row current-step stamps, the transposed tower weights, the per-workgroup gradient
 // partials, the training positives and their sorted CSR (the sampler's rejection set).
-// A step (NCFRecommender.py:278-285): one k_ncf_fwdbwd launch over the batch (16 samples per
-// workgroup), then Adam over the flat block (k_ncf_adam_flat) and the used embedding tables
-// (k_ncf_adam_rows).
+// A step (NCFRecommender.py:278-285): the batch's embedding rows are brought up to step t - 1
+// (k_ncf_catch_up: the zero-gradient Adam steps they missed, in closed form), one k_ncf_fwdbwd
+// launch over the batch (16 samples per workgroup), then Adam over the flat block
+// (k_ncf_adam_flat) and over the batch's embedding rows (k_ncf_adam_rows).  Every read of the
+// tables from outside a step (predict, get / set_param) first brings the rows it reads to the
+// current step, so every observable value is torch's dense Adam.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -52,10 +55,14 @@ struct ncf_handle {
   double* d_loss = nullptr;
   int32_t* d_err = nullptr;
   int32_t t = 0;  // Adam steps taken
+  int32_t *cur_u = nullptr, *cur_i = nullptr;  // step each row's p, m, v are current at (-1: never touched)
+  int32_t flushed = 0;                         // every row is current at this step
+  float2 *d_step = nullptr, *d_pw = nullptr;   // catch-up tables (CatchArgs)
+  int32_t nstep = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool prof_on = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[3];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[4];
   std::vector<hipEvent_t> pool;
 };
 
@@ -130,6 +137,75 @@ static bool param_at(ncf_handle* h, int idx, float** p, int64_t* rows, int64_t* 
   return false;
 }
 
+// the embedding rows of the used tables, per side; ids: the samples' (user, item) or null (all rows)
+static RowSides row_sides(const ncf_handle* h, const int32_t* u, const int32_t* i) {
+  RowSides R{};
+  for (int side = 0; side < 2; ++side) {
+    RowSide& S = R.side[side];
+    for (int k = 0; k < 2; ++k) {
+      const int tb = 2 * k + side;  // Pg, Qg, Pm, Qm
+      if (!uses_table(h, tb)) continue;
+      S.W[k] = h->emb[tb];
+      S.M[k] = h->emb_m[tb];
+      S.V[k] = h->emb_v[tb];
+      S.G[k] = tb == 0 ? h->G.Pg : tb == 1 ? h->G.Qg : tb == 2 ? h->G.Pm : h->G.Qm;
+      S.cols[k] = (int)h->emb_cols[tb];
+    }
+    S.cur = side ? h->cur_i : h->cur_u;
+    S.rows = side ? h->D.I : h->D.U;
+  }
+  R.ids[0] = u;
+  R.ids[1] = i;
+  R.U = h->D.U;
+  R.I = h->D.I;
+  return R;
+}
+
+static CatchArgs catch_args(const ncf_handle* h, int32_t target) {
+  CatchArgs c;
+  c.step = h->d_step;
+  c.pw = h->d_pw;
+  c.nstep = h->nstep;
+  c.lr = h->cfg.lr;
+  c.eps = h->cfg.eps;
+  c.log2_b1 = (float)std::log2((double)h->cfg.beta1);
+  c.log2_b2 = (float)std::log2((double)h->cfg.beta2);
+  c.target = target;
+  return c;
+}
+
+// the catch-up's tables, in double as the step's own AdamArgs: torch's step_size(s) and
+// 1 / bc2_sqrt(s) for every step whose bias corrections f32 tells from 1 (then lr and 1), and
+// b1^j, b2^(j/2) for the terms
+static int catch_tables(ncf_handle* h) {
+  const double b1 = h->cfg.beta1, b2 = h->cfg.beta2, lr = h->cfg.lr;
+  int64_t n = 1;
+  while (n < (1 << 22) && (std::pow(b1, (double)n) > 0x1p-26 || std::pow(b2, (double)n) > 0x1p-26)) n *= 2;
+  std::vector<float2> st((size_t)n), pw(kCatchTerms);
+  for (int64_t s = 1; s <= n; ++s)
+    st[s - 1] = make_float2((float)(lr / (1.0 - std::pow(b1, (double)s))),
+                            (float)(1.0 / std::sqrt(1.0 - std::pow(b2, (double)s))));
+  for (int j = 1; j <= kCatchTerms; ++j)
+    pw[j - 1] = make_float2((float)std::pow(b1, (double)j), (float)std::pow(b2, 0.5 * j));
+  if (int r = dalloc(&h->d_step, n)) return r;
+  if (int r = dalloc(&h->d_pw, kCatchTerms)) return r;
+  HIPCHK(hipMemcpy(h->d_step, st.data(), sizeof(float2) * n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_pw, pw.data(), sizeof(float2) * kCatchTerms, hipMemcpyHostToDevice));
+  h->nstep = (int32_t)n;
+  return 0;
+}
+
+// every embedding row brought to the current step (before the tables are read or written whole)
+static int ncf_flush(ncf_handle* h) {
+  if (h->flushed == h->t) return 0;
+  {
+    NcfProf ps(h, 3);
+    HIPCHK(catch_up(row_sides(h, nullptr, nullptr), 0, catch_args(h, h->t), h->stream));
+  }
+  h->flushed = h->t;
+  return 0;
+}
+
 static SamplerArgs ncf_sampler(ncf_handle* h) {
   SamplerArgs a{};
   a.pos_u = h->d_pos_u;
@@ -164,6 +240,11 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   const int32_t t = ++h->t;
   const int nb = (n + kSamples - 1) / kSamples;
+  const RowSides R = row_sides(h, u, i);
+  {
+    NcfProf ps(h, 3);
+    HIPCHK(catch_up(R, n, catch_args(h, t - 1), h->stream));
+  }
   {
     NcfProf ps(h, 1);
     HIPCHK(fwdbwd(h->D, h->P, h->G, u, i, y, n, t, h->partial, h->d_loss, h->d_err, h->stream));
@@ -179,13 +260,7 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   NcfProf ps(h, 2);
   const int lo = h->D.model == kGMF ? h->D.off_wp : 0;  // GMF: the tower has no gradient
   HIPCHK(adam_flat(h->D, h->P, h->F, h->Fm, h->Fv, h->partial, nb, lo, h->D.flat_n, a, h->stream));
-  for (int tb = 0; tb < 4; ++tb) {
-    if (!uses_table(h, tb)) continue;
-    float* g = tb == 0 ? h->G.Pg : tb == 1 ? h->G.Qg : tb == 2 ? h->G.Pm : h->G.Qm;
-    const int32_t* touch = (tb % 2 == 0) ? h->G.touch_u : h->G.touch_i;
-    HIPCHK(adam_rows(h->emb[tb], h->emb_m[tb], h->emb_v[tb], g, touch, h->emb_rows[tb],
-                     (int)h->emb_cols[tb], t, a, h->stream));
-  }
+  HIPCHK(adam_rows(R, n, t, a, h->stream));
   return 0;
 }
 
@@ -319,10 +394,11 @@ int ncf_create(const ncf_config* cfg, ncf_handle** out) {
   TRY(memz(h->G.Qg, 4 * D.I * D.d));
   TRY(memz(h->G.Pm, 4 * D.U * D.E));
   TRY(memz(h->G.Qm, 4 * D.I * D.E));
-  TRY(dalloc(&h->G.touch_u, D.U));
-  TRY(dalloc(&h->G.touch_i, D.I));
-  HIPCHK(hipMemsetAsync(h->G.touch_u, 0xFF, 4 * D.U, h->stream));  // -1: never touched
-  HIPCHK(hipMemsetAsync(h->G.touch_i, 0xFF, 4 * D.I, h->stream));
+  TRY(catch_tables(h));
+  TRY(dalloc(&h->cur_u, D.U));
+  TRY(dalloc(&h->cur_i, D.I));
+  HIPCHK(hipMemsetAsync(h->cur_u, 0xFF, 4 * D.U, h->stream));  // -1: never touched
+  HIPCHK(hipMemsetAsync(h->cur_i, 0xFF, 4 * D.I, h->stream));
   TRY(dalloc(&h->F, D.flat_n));
   TRY(dalloc(&h->Fm, D.flat_n));
   TRY(dalloc(&h->Fv, D.flat_n));
@@ -378,7 +454,7 @@ int ncf_destroy(ncf_handle* h) {
     for (void* x : p)
       if (x) (void)!hipFree(x);
   }
-  void* ptrs[] = {h->G.Pg, h->G.Qg, h->G.Pm, h->G.Qm, h->G.touch_u, h->G.touch_i, h->F, h->Fm,
+  void* ptrs[] = {h->G.Pg, h->G.Qg, h->G.Pm, h->G.Qm, h->cur_u, h->cur_i, h->d_step, h->d_pw, h->F, h->Fm,
                   h->Fv, h->WT, h->partial, h->d_pos_u, h->d_pos_i, h->d_indices, h->d_indptr,
                   h->d_u, h->d_i, h->d_y, h->d_loss, h->d_err};
   for (void* x : ptrs)
@@ -410,6 +486,8 @@ int ncf_set_param(ncf_handle* h, int32_t index, const float* data) {
   int64_t r, c;
   if (!param_at(h, index, &p, &r, &c)) return fail(BPRMF_E_RANGE, "no parameter %d", index);
   if (int rc = ncf_dev(h)) return rc;
+  if (index < 4)  // the moments of the rows keep counting from the current step
+    if (int rc = ncf_flush(h)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(p, data, 4 * r * c, hipMemcpyHostToDevice));
   HIPCHK(transpose(h->D, h->P, h->stream));
@@ -423,6 +501,8 @@ int ncf_get_param(ncf_handle* h, int32_t index, float* data) {
   int64_t r, c;
   if (!param_at(h, index, &p, &r, &c)) return fail(BPRMF_E_RANGE, "no parameter %d", index);
   if (int rc = ncf_dev(h)) return rc;
+  if (index < 4)
+    if (int rc = ncf_flush(h)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(data, p, 4 * r * c, hipMemcpyDeviceToHost));
   return 0;
@@ -554,12 +634,18 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
   }
   if (n == 0) return 0;
   if (int r = ncf_dev(h)) return r;
+  // the rows read are brought to the current step: the requested ones, or every row for a long request
+  const bool whole = 2 * n >= h->D.U + h->D.I;
+  if (whole)
+    if (int r = ncf_flush(h)) return r;
   int32_t* buf = nullptr;
   if (int r = dalloc(&buf, 3 * n)) return r;
   float* z = reinterpret_cast<float*>(buf + 2 * n);
   int rc = 0;
   hipError_t e = hipMemcpyAsync(buf, u, 4 * n, hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(buf + n, i, 4 * n, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess && !whole && h->flushed != h->t)
+    e = catch_up(row_sides(h, buf, buf + n), n, catch_args(h, h->t), h->stream);
   for (int64_t off = 0; off < n && e == hipSuccess; off += (1 << 30))
     e = forward(h->D, h->P, buf + off, buf + n + off, (int)std::min<int64_t>(n - off, 1 << 30), z + off,
                 h->d_err, h->stream);
@@ -576,8 +662,8 @@ int ncf_active_rows(ncf_handle* h, int64_t* users, int64_t* items) {
   if (int r = ncf_dev(h)) return r;
   HIPCHK(hipStreamSynchronize(h->stream));
   std::vector<int32_t> tu(h->D.U), ti(h->D.I);
-  HIPCHK(hipMemcpy(tu.data(), h->G.touch_u, 4 * h->D.U, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(ti.data(), h->G.touch_i, 4 * h->D.I, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(tu.data(), h->cur_u, 4 * h->D.U, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ti.data(), h->cur_i, 4 * h->D.I, hipMemcpyDeviceToHost));
   *users = std::count_if(tu.begin(), tu.end(), [](int32_t x) { return x >= 0; });
   *items = std::count_if(ti.begin(), ti.end(), [](int32_t x) { return x >= 0; });
   return 0;
@@ -599,7 +685,7 @@ int ncf_profile_read(ncf_handle* h, bprmf_kprof* out) {
   if (int r = ncf_dev(h)) return r;
   HIPCHK(hipStreamSynchronize(h->stream));
   memset(out, 0, sizeof *out);
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 4; ++k) {
     double tot = 0;
     for (auto& pr : h->prof[k]) {
       float ms = 0;

@@ -29,9 +29,33 @@ struct Params {
   float *wp, *bp;                      // predict_layer.weight [pred] / bias [1]
 };
 
-struct Grads {  // dense gradient rows of the embedding tables + the step each row was touched
+struct Grads {  // dense gradient rows of the embedding tables (zeroed again by the row Adam)
   float *Pg, *Qg, *Pm, *Qm;
-  int32_t *touch_u, *touch_i;
+};
+
+// The embedding rows of one side (users or items): its GMF and MLP tables (cols 0 for a table the
+// model does not use) and the step through which each row's p, m, v are current (cur, -1: never
+// touched, m = v = 0).
+struct RowSide {
+  float *W[2], *M[2], *V[2], *G[2];
+  int cols[2];
+  int32_t* cur;
+  int64_t rows;
+};
+struct RowSides {
+  RowSide side[2];           // users, items
+  const int32_t* ids[2];     // the batch's (user, item) samples; nullptr: every row of the side
+  int64_t U, I;              // id bounds (a sample with an id out of range has no gradient)
+};
+
+constexpr int kCatchTerms = 192;  // terms of a catch-up's sum (k_ncf_catch_up)
+
+struct CatchArgs {  // zero-gradient Adam steps up to step `target`
+  const float2* step;  // (step_size(s), 1 / bc2_sqrt(s)) for s = 1 .. nstep; beyond, (lr, 1)
+  const float2* pw;    // (b1^j, b2^(j/2)) for j = 1 .. kCatchTerms
+  int32_t nstep;
+  float lr, eps, log2_b1, log2_b2;
+  int32_t target;
 };
 
 struct AdamArgs {
@@ -44,8 +68,10 @@ hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const int32_t*
                   double* loss, int32_t* err, hipStream_t s);
 hipError_t forward(const Dims& D, const Params& P, const int32_t* u, const int32_t* i, int n,
                    float* z, int32_t* err, hipStream_t s);
-hipError_t adam_rows(float* W, float* M, float* V, float* Gr, const int32_t* touch, int64_t rows,
-                     int dim, int32_t t, const AdamArgs& a, hipStream_t s);
+// rows of the samples (or every row when ids are null) brought to c.target; cur = c.target
+hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_t s);
+// step t of Adam on the rows of the samples (g = the gradient row, then zeroed); cur = t
+hipError_t adam_rows(const RowSides& R, int64_t n, int32_t t, const AdamArgs& a, hipStream_t s);
 hipError_t adam_flat(const Dims& D, const Params& P, float* F, float* M, float* V,
                      const float* partial, int nparts, int lo, int hi, const AdamArgs& a,
                      hipStream_t s);

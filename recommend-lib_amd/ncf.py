@@ -198,7 +198,7 @@ class NCF:
         kp = _lib.KProf()
         _lib.check(self._L.ncf_profile_read(self._h, ctypes.byref(kp)))
         return {k: dict(count=int(kp.count[n]), ms=float(kp.ms[n]))
-                for n, k in enumerate(("sample", "fwd_bwd", "adam"))}
+                for n, k in enumerate(("sample", "fwd_bwd", "adam", "catch_up"))}
 
 
 class NCFData:

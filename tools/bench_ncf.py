@@ -104,6 +104,7 @@ def main():
     adam_bytes = 24 * (au * (d + E) + ai * (d + E))
     adam_s = kp["adam"]["ms"] / kp["adam"]["count"] * 1e-3
     fb_s = kp["fwd_bwd"]["ms"] / kp["fwd_bwd"]["count"] * 1e-3
+    cu_s = kp["catch_up"]["ms"] / max(1, kp["catch_up"]["count"]) * 1e-3
     ach = adam_bytes / adam_s / 1e9
     out = {"metric": "NCF NeuMF-end training samples/s, ml-20m shape, factor 64 (config C4)",
            "value": round(a.steps * B / st["seconds"], 1), "unit": "samples/s", "n_gpus": 1,
@@ -112,7 +113,8 @@ def main():
            "config": {"users": U, "items": I, "factor_num": d, "num_layers": L, "batch_size": B,
                       "num_ng": 4, "optimizer": "Adam(lr=0.001), dense over all parameters",
                       "active_rows": [au, ai]},
-           "kernels_us": {"fwd_bwd": round(fb_s * 1e6, 2), "adam_all": round(adam_s * 1e6, 2)},
+           "kernels_us": {"catch_up": round(cu_s * 1e6, 2), "fwd_bwd": round(fb_s * 1e6, 2),
+                          "adam_all": round(adam_s * 1e6, 2)},
            "roofline": {"bound": "hbm", "kernel": "Adam sweep (p, m, v of every active parameter)",
                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": adam_bytes},

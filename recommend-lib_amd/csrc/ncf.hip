@@ -4,19 +4,16 @@
 // parameter with dense gradients), util/data_loader.py:931-972 (NCFData: positives, then num_ng
 // negatives per positive, shuffled).
 //
-//   k_ncf_fwdbwd  one 1024-thread workgroup per 16 samples: embedding gathers into LDS, the MLP
-//                 tower forward on f32 MFMA (v_mfma_f32_16x16x4_f32: the 16 samples are the M
-//                 dimension of every layer), the prediction and dL/dz, then the tower backward:
-//                 dW partial tiles per workgroup (summed in fixed order by the Adam kernel),
-//                 dX = dPre . W through the transposed weight copies, and the embedding
-//                 gradients as f32 atomics into dense gradient rows.
+//   k_ncf_front / k_ncf_mid / k_ncf_back  the forward and backward on f32 MFMA
+//                 (v_mfma_f32_16x16x4_f32; 16 samples are the M dimension of the per-sample
+//                 layers), torch's Adam on the tower and predict layer fused into the weight-
+//                 gradient tiles, the embedding gradients as f32 atomics into dense gradient rows
+//                 (see "forward / backward" below).
 //   k_ncf_catch_up / k_ncf_adam_rows  torch's dense Adam over the embedding tables, done lazily:
 //                 every row with a nonzero moment moves every step, but a step with g = 0 has a
 //                 closed form, so a row is brought up to date only when something reads it (the
 //                 step that gathers it, a predict, a parameter copy) and Adam proper runs on the
 //                 batch's rows alone.  Equal to the dense sweep up to f32 rounding.
-//   k_ncf_adam_flat  Adam over the tower + predict layer, g = sum of the workgroups' partials in
-//                 workgroup order; weights also written transposed for the next backward.
 #include <algorithm>
 
 #include "device_common.h"
@@ -29,10 +26,26 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// LDS plan of k_ncf_fwdbwd (floats): sample ids / labels / z / dz, GMF rows, tower activations
+// ---- forward / backward ----------------------------------------------------------------------
+// A step's tower runs in three launches, so that no kernel streams every weight through one CU:
+//   k_ncf_front  layer 0 (the widest): one workgroup per (16 samples, 64 output columns); gathers
+//                the tower input [Pm[u], Qm[i]] and writes h_1 (and the input itself, X0, for
+//                the weight gradient).
+//   k_ncf_mid    one workgroup per 16 samples: layers 1 .. L-1, the prediction, BCE and dL/dz,
+//                the GMF embedding gradients, then the tower backward down to dPre_0 (the
+//                gradient of layer 0's pre-activation).  Activations and pre-activation
+//                gradients go to global memory (Acts) for the next launch.
+//   k_ncf_back   jobs over the whole batch: every weight-gradient tile dW_l = dPre_l^T . h_l, bias
+//                and predict-layer gradient as a contraction over the batch's samples (MFMA,
+//                fixed order: deterministic), each followed by torch's Adam on its elements (and
+//                the transposed copy W^T); and the tower input's gradient dX_0 = dPre_0 . W_0
+//                per (16 samples, 16 columns) into the MLP embedding gradient rows (f32 atomics).
+
+// LDS plan of k_ncf_mid (floats): sample ids / labels / z / dz, GMF rows, activations h_1 .. h_L
 struct Lds {
   int eu, ei, h[kMaxLayers + 1], misc, total;
   int ldh[kMaxLayers + 1];
+  int hL, ldL;  // h[L], ldh[L]
 };
 static __host__ __device__ inline Lds lds_plan(const Dims& D) {
   Lds p{};
@@ -43,19 +56,25 @@ static __host__ __device__ inline Lds lds_plan(const Dims& D) {
   off += kSamples * (D.d + 4);
   p.ei = off;
   off += kSamples * (D.d + 4);
-  for (int l = 0; l <= D.L; ++l) {
-    const int n = l == 0 ? D.nin[0] : D.nout[l - 1];
-    p.ldh[l] = n + 4;  // row stride: +4 floats keeps float4 reads of 16 rows conflict-free
+#pragma unroll
+  for (int l = 1; l <= kMaxLayers; ++l) {  // constant indices: no scratch copy of the arrays
+    if (l > D.L) break;
+    p.ldh[l] = D.nout[l - 1] + 4;  // row stride: +4 floats keeps float4 reads of 16 rows conflict-free
     p.h[l] = off;
     off += kSamples * p.ldh[l];
+    p.hL = p.h[l];
+    p.ldL = p.ldh[l];
   }
   p.total = off;
   return p;
 }
+static __host__ __device__ inline int front_ld(const Dims& D) { return 2 * D.E + 4; }
 
-size_t fwdbwd_lds_bytes(const Dims& D) { return sizeof(float) * (size_t)lds_plan(D).total; }
+size_t fwdbwd_lds_bytes(const Dims& D) {
+  return sizeof(float) * (size_t)std::max(lds_plan(D).total, kSamples * front_ld(D));
+}
 
-// y[16 x 16 tile] = X[16 x K] (LDS, stride ldx) . W[n0.., :]^T (global, W[n][k], stride K):
+// y[16 x 16 tile] = X[16 x K] (stride ldx) . W[n0.., :]^T (global, W[n][k], stride K):
 // 16x16x4 f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (K % 4 == 0).  The W rows
 // come from L2/HBM: eight k-steps of loads are issued before their 32 MFMAs, so one latency is
 // paid per eight steps, not per step.
@@ -89,32 +108,73 @@ static __device__ __forceinline__ f32x4 tile_xwt(const float* X, int ldx, const 
   return acc;
 }
 
-// BPRMF_NCF_PHASES (diagnostic builds only): workgroup 0 of step 100 prints its phase times
-#ifdef BPRMF_NCF_PHASES
-#define NCF_PH(k)                                 \
-  do {                                            \
-    if (threadIdx.x == 0) s_ph[k] = wall_clock64(); \
-  } while (0)
-#else
-#define NCF_PH(k) \
-  do {            \
-  } while (0)
-#endif
+// a[i] for a run-time i without a dynamic index into the array (which would go through scratch)
+template <typename T, int N>
+static __device__ __forceinline__ T pick(const T (&a)[N], int i) {
+  T r = a[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k)
+    if (i == k) r = a[k];
+  return r;
+}
 
-__global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
-                                                     const int32_t* __restrict__ us,
-                                                     const int32_t* __restrict__ is,
-                                                     const float* __restrict__ ys, int n,
-                                                     int32_t t, float* __restrict__ partial,
-                                                     double* __restrict__ loss,
-                                                     int32_t* __restrict__ err,
-                                                     float* __restrict__ zout) {
+// a sample's ids, or -1 / -1 past n or out of range (the error flag is raised by k_ncf_mid)
+static __device__ __forceinline__ void sample_ids(const Dims& D, const int32_t* us, const int32_t* is,
+                                                  int s, int n, int32_t& u, int32_t& i) {
+  u = i = -1;
+  if (s >= n) return;
+  const int32_t a = us[s], b = is[s];
+  if ((uint64_t)a < (uint64_t)D.U && (uint64_t)b < (uint64_t)D.I) {
+    u = a;
+    i = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
+                                                   const int32_t* __restrict__ us,
+                                                   const int32_t* __restrict__ is, int n) {
   extern __shared__ float sm[];
-#ifdef BPRMF_NCF_PHASES
-  __shared__ uint64_t s_ph[24];
-  if (threadIdx.x < 24) s_ph[threadIdx.x] = 0;
-  NCF_PH(0);
-#endif
+  __shared__ int32_t su[kSamples], si[kSamples];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int s0 = blockIdx.x * kSamples, E = D.E, K = 2 * E, N = D.nout[0], ld = front_ld(D);
+  if (tid < kSamples) sample_ids(D, us, is, s0 + tid, n, su[tid], si[tid]);
+  __syncthreads();
+  const bool keep = A.X0 && blockIdx.y == 0;  // one workgroup per sample group stores X0
+  const int q = K / 4;
+  for (int x = tid; x < kSamples * q; x += blockDim.x) {
+    const int s = x / q, c = 4 * (x % q);
+    const int32_t u = su[s], i = si[s];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < E) {
+      if (u >= 0) v = ld4(P.Pm + (int64_t)u * E + c);
+    } else if (i >= 0) {
+      v = ld4(P.Qm + (int64_t)i * E + (c - E));
+    }
+    *reinterpret_cast<float4*>(sm + s * ld + c) = v;
+    if (keep && s0 + s < n) *reinterpret_cast<float4*>(A.X0 + (int64_t)(s0 + s) * K + c) = v;
+  }
+  __syncthreads();
+  const int tile = 4 * blockIdx.y + wave;
+  if (16 * tile >= N) return;
+  const f32x4 acc = tile_xwt(sm, ld, P.W[0], K, 16 * tile, N, lane);
+  const int nn = 16 * tile + (lane & 15);
+  if (nn >= N) return;
+  const float bias = P.b[0][nn];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int s = 4 * (lane >> 4) + r;
+    if (s0 + s < n) A.H[1][(int64_t)(s0 + s) * A.ldH[1] + nn] = fmaxf(acc[r] + bias, 0.f);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Acts A,
+                                                  const int32_t* __restrict__ us,
+                                                  const int32_t* __restrict__ is,
+                                                  const float* __restrict__ ys, int n,
+                                                  double* __restrict__ loss,
+                                                  int32_t* __restrict__ err,
+                                                  float* __restrict__ zout) {
+  extern __shared__ float sm[];
   const Lds Lp = lds_plan(D);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = 16;
@@ -124,28 +184,24 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
   float* sy = sm + Lp.misc + 2 * kSamples;
   float* sz = sm + Lp.misc + 3 * kSamples;
   const bool gmf = D.model != kMLP, mlp = D.model != kGMF;
-  const int d = D.d, E = D.E;
+  const int d = D.d, L = D.L;
+  const int rows = min(kSamples, n - s0);  // valid rows of this group in the Acts buffers
   // 1. samples
   if (tid < kSamples) {
     const int s = s0 + tid;
     int32_t u = -1, i = -1;
     float y = 0.f;
     if (s < n) {
-      u = us[s];
-      i = is[s];
       y = ys ? ys[s] : 0.f;
-      if ((uint64_t)u >= (uint64_t)D.U || (uint64_t)i >= (uint64_t)D.I) {
-        atomicOr(err, 1);
-        u = i = -1;
-      }
+      if ((uint64_t)us[s] >= (uint64_t)D.U || (uint64_t)is[s] >= (uint64_t)D.I) atomicOr(err, 1);
+      sample_ids(D, us, is, s, n, u, i);
     }
     su[tid] = u;
     si[tid] = i;
     sy[tid] = y;
   }
   __syncthreads();
-  NCF_PH(1);
-  // 2. gathers (float4): GMF rows and the tower input [Pm[u], Qm[i]]
+  // 2. GMF rows and h_1 (k_ncf_front's output)
   if (gmf) {
     const int q = d / 4;
     for (int x = tid; x < kSamples * q; x += blockDim.x) {
@@ -158,24 +214,19 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
     }
   }
   if (mlp) {
-    const int q = 2 * E / 4;
+    const int q = D.nout[0] / 4;
     for (int x = tid; x < kSamples * q; x += blockDim.x) {
       const int s = x / q, c = 4 * (x % q);
-      const int32_t u = su[s], i = si[s];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (c < E) {
-        if (u >= 0) v = ld4(P.Pm + (int64_t)u * E + c);
-      } else if (i >= 0) {
-        v = ld4(P.Qm + (int64_t)i * E + (c - E));
-      }
-      *reinterpret_cast<float4*>(sm + Lp.h[0] + s * Lp.ldh[0] + c) = v;
+      const float4 v = s < rows ? ld4(A.H[1] + (int64_t)(s0 + s) * A.ldH[1] + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(sm + Lp.h[1] + s * Lp.ldh[1] + c) = v;
     }
   }
   __syncthreads();
-  NCF_PH(2);
-  // 3. tower forward: h_l = relu(h_{l-1} W_l^T + b_l)
+  // 3. tower forward, layers 1 .. L-1: h_{l+1} = relu(h_l W_l^T + b_l), also to global (not h_1)
   if (mlp) {
-    for (int l = 0; l < D.L; ++l) {
+#pragma unroll
+    for (int l = 1; l < kMaxLayers; ++l) {
+      if (l >= L) break;
       const int K = D.nin[l], N = D.nout[l];
       const float* X = sm + Lp.h[l];
       float* Y = sm + Lp.h[l + 1];
@@ -187,26 +238,29 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int s = 4 * (lane >> 4) + r;
-            Y[s * Lp.ldh[l + 1] + nn] = fmaxf(acc[r] + bias, 0.f);
+            const float h = fmaxf(acc[r] + bias, 0.f);
+            Y[s * Lp.ldh[l + 1] + nn] = h;
+            if (!zout && s < rows) A.H[l + 1][(int64_t)(s0 + s) * A.ldH[l + 1] + nn] = h;
           }
         }
       }
       __syncthreads();
-      NCF_PH(3 + l);
     }
   }
   // 4. prediction z = [gmf, h_L] . wp + bp and dL/dz of the mean BCE-with-logits loss
-  const float* hL = sm + Lp.h[D.L];
-  const int ldL = Lp.ldh[D.L];
+  const float* hL = sm + Lp.hL;
+  const int ldL = Lp.ldL;
   if (wave < kSamples) {
     const int s = wave;
     float acc = 0.f;
     for (int k = lane; k < D.pred; k += 64) {
       float x;
-      if (gmf && k < d)
+      if (gmf && k < d) {
         x = sm[Lp.eu + s * (d + 4) + k] * sm[Lp.ei + s * (d + 4) + k];
-      else
+        if (!zout && s < rows) A.Xp[(int64_t)(s0 + s) * D.pred + k] = x;
+      } else {
         x = hL[s * ldL + (k - (gmf ? d : 0))];
+      }
       acc = fmaf(x, P.wp[k], acc);
     }
 #pragma unroll
@@ -216,36 +270,16 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
       const float z = acc + P.bp[0];
       if (zout && s0 + s < n) zout[s0 + s] = z;
       const float y = sy[s];
-      sz[s] = ok ? (1.0f / (1.0f + expf(-z)) - y) / (float)n : 0.f;  // dz
+      const float dz = ok ? (1.0f / (1.0f + expf(-z)) - y) / (float)n : 0.f;
+      sz[s] = dz;
+      if (!zout && s < rows) A.dz[s0 + s] = dz;
       if (ok && loss)  // this sample's share of the step's mean loss
         atomicAdd(&loss[blockIdx.x & (kLossSlotsNcf - 1)],
                   (double)(fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)))) / (double)n);
     }
   }
   __syncthreads();
-  NCF_PH(7);
   if (zout) return;  // forward only (ncf_predict)
-  // 5. predict-layer gradients (workgroup partials, samples in order) and dX of the predictor
-  float* part = partial + (int64_t)blockIdx.x * D.flat_n;
-  for (int k = tid; k <= D.pred; k += blockDim.x) {
-    float acc = 0.f;
-    if (k < D.pred) {
-      for (int s = 0; s < kSamples; ++s) {
-        float x;
-        if (gmf && k < d)
-          x = sm[Lp.eu + s * (d + 4) + k] * sm[Lp.ei + s * (d + 4) + k];
-        else
-          x = hL[s * ldL + (k - (gmf ? d : 0))];
-        acc = fmaf(sz[s], x, acc);
-      }
-      part[D.off_wp + k] = acc;
-    } else {
-      for (int s = 0; s < kSamples; ++s) acc += sz[s];
-      part[D.off_bp] = acc;
-    }
-  }
-  __syncthreads();  // hL (read above as x) is overwritten below by dPre_L
-  NCF_PH(8);
   if (gmf) {  // dPg[u] += dz wp_k Qg[i]_k ; dQg[i] += dz wp_k Pg[u]_k
     for (int x = tid; x < kSamples * d; x += blockDim.x) {
       const int s = x / d, k = x % d;
@@ -256,88 +290,41 @@ __global__ __launch_bounds__(1024) void k_ncf_fwdbwd(Dims D, Params P, Grads G,
       atomicAdd(G.Qg + (int64_t)i * d + k, gk * sm[Lp.eu + s * (d + 4) + k]);
     }
   }
-  if (mlp) {
-    // dPre_L = dz wp[tower part] * (h_L > 0), in place of h_L
-    float* hw = sm + Lp.h[D.L];
-    for (int x = tid; x < kSamples * d; x += blockDim.x) {
-      const int s = x / d, k = x % d;
-      const float h = hw[s * ldL + k];
-      hw[s * ldL + k] = h > 0.f ? sz[s] * P.wp[(gmf ? d : 0) + k] : 0.f;
+  if (!mlp) return;
+  // 5. dPre_{L-1} = dz wp[tower part] * (h_L > 0), in place of h_L
+  float* hw = sm + Lp.hL;
+  float* dPreL = pick(A.dPre, L - 1);
+  for (int x = tid; x < kSamples * d; x += blockDim.x) {
+    const int s = x / d, k = x % d;
+    const float h = hw[s * ldL + k];
+    const float g = h > 0.f ? sz[s] * P.wp[(gmf ? d : 0) + k] : 0.f;
+    hw[s * ldL + k] = g;
+    if (s < rows) dPreL[(int64_t)(s0 + s) * d + k] = g;
+  }
+  __syncthreads();
+  // 6. dPre_{l-1} = (dPre_l . W_l) * (h_l > 0) for l = L-1 .. 1 (B operand: W_l^T), in place of h_l
+#pragma unroll
+  for (int l = kMaxLayers - 1; l >= 1; --l) {
+    if (l > L - 1) continue;
+    const int K = D.nin[l], N = D.nout[l];
+    const float* dP = sm + Lp.h[l + 1];
+    float* H = sm + Lp.h[l];
+    const int ldp = Lp.ldh[l + 1], ldx = Lp.ldh[l];
+    for (int tile = wave; 16 * tile < K; tile += NW) {
+      const f32x4 acc = tile_xwt(dP, ldp, P.WT[l], N, 16 * tile, K, lane);
+      const int kk = 16 * tile + (lane & 15);
+      if (kk < K) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = 4 * (lane >> 4) + r;
+          const float g = H[s * ldx + kk] > 0.f ? acc[r] : 0.f;
+          H[s * ldx + kk] = g;
+          if (s < rows) A.dPre[l - 1][(int64_t)(s0 + s) * K + kk] = g;
+        }
+      }
     }
     __syncthreads();
-    NCF_PH(9);
-    for (int l = D.L - 1; l >= 0; --l) {
-      const int K = D.nin[l], N = D.nout[l];
-      const float* dP = sm + Lp.h[l + 1];  // dPre_l [16 x N]
-      const int ldp = Lp.ldh[l + 1];
-      float* H = sm + Lp.h[l];  // h_{l-1} [16 x K], becomes dPre_{l-1} (or dX_0)
-      const int ldx = Lp.ldh[l];
-      // (a) dW_l partial [N x K] = dPre^T . H (contraction over the 16 samples), db_l
-      const int tn = (N + 15) / 16, tk = (K + 15) / 16;
-      for (int tile = wave; tile < tn * tk; tile += NW) {
-        const int n0 = 16 * (tile / tk), k0 = 16 * (tile % tk);
-        const int r = lane & 15, g = lane >> 4;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int s = 4 * e + g;
-          const float a = n0 + r < N ? dP[s * ldp + n0 + r] : 0.f;
-          const float b = k0 + r < K ? H[s * ldx + k0 + r] : 0.f;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        }
-        const int kk = k0 + r;
-        if (kk < K) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int nn = n0 + 4 * g + q;
-            if (nn < N) part[D.off_W[l] + (int64_t)nn * K + kk] = acc[q];
-          }
-        }
-      }
-      for (int nn = tid; nn < N; nn += blockDim.x) {
-        float acc = 0.f;
-        for (int s = 0; s < kSamples; ++s) acc += dP[s * ldp + nn];
-        part[D.off_b[l] + nn] = acc;
-      }
-      __syncthreads();
-      NCF_PH(10 + 2 * (D.L - 1 - l));
-      // (b) dX [16 x K] = dPre . W_l  (B operand from the transposed copy WT_l [K x N])
-      for (int tile = wave; 16 * tile < K; tile += NW) {
-        const f32x4 acc = tile_xwt(dP, ldp, P.WT[l], N, 16 * tile, K, lane);
-        const int kk = 16 * tile + (lane & 15);
-        if (kk < K) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int s = 4 * (lane >> 4) + r;
-            float v = acc[r];
-            if (l > 0) v = H[s * ldx + kk] > 0.f ? v : 0.f;  // relu' of h_{l-1}
-            H[s * ldx + kk] = v;
-          }
-        }
-      }
-      __syncthreads();
-      NCF_PH(11 + 2 * (D.L - 1 - l));
-    }
-    // embedding gradients of the tower input: dPm[u] += dX0[:E], dQm[i] += dX0[E:]
-    const float* X0 = sm + Lp.h[0];
-    for (int x = tid; x < kSamples * 2 * E; x += blockDim.x) {
-      const int s = x / (2 * E), k = x % (2 * E);
-      const int32_t u = su[s], i = si[s];
-      if (u < 0) continue;
-      const float v = X0[s * Lp.ldh[0] + k];
-      if (k < E)
-        atomicAdd(G.Pm + (int64_t)u * E + k, v);
-      else
-        atomicAdd(G.Qm + (int64_t)i * E + (k - E), v);
-    }
   }
-#ifdef BPRMF_NCF_PHASES
-  __syncthreads();
-  NCF_PH(20);
-  if (threadIdx.x == 0 && blockIdx.x == 0 && t == 100)
-    for (int k = 1; k <= 20; ++k)
-      if (s_ph[k]) printf("ncf phase %d: %.2f us\n", k, (double)(s_ph[k] - s_ph[0]) * 1e-2);
-#endif
 }
 
 // torch Adam (single-tensor form): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
@@ -444,26 +431,69 @@ __global__ __launch_bounds__(1024) void k_ncf_adam_rows(RowSides R, int32_t t, A
   }
 }
 
-// flat region [lo, hi) of the tower+predict parameters; weights of layer l also to WT_l
-__global__ __launch_bounds__(256) void k_ncf_adam_flat(Dims D, Params P, float* __restrict__ F,
-                                                       float* __restrict__ M, float* __restrict__ V,
-                                                       const float* __restrict__ partial, int nparts,
-                                                       int lo, int hi, AdamArgs a) {
-  for (int j = lo + blockIdx.x * blockDim.x + threadIdx.x; j < hi; j += gridDim.x * blockDim.x) {
-    float g = 0.f;
-    for (int b = 0; b < nparts; ++b) g += partial[(int64_t)b * D.flat_n + j];
-    float p = F[j], m = M[j], v = V[j];
-    adam1(p, m, v, g, a);
-    F[j] = p;
+// k_ncf_back: one job per wave (NcfJob, built once per handle).  Reads the step's weights at
+// Fcur / P.WT and writes the Adam-updated ones to Fnext / WTnext (double-buffered: the dX_0 jobs
+// of the same launch still read the old W_0).
+__global__ __launch_bounds__(256) void k_ncf_back(Dims D, Params P, Grads G, const NcfJob* __restrict__ jobs,
+                                                  int njobs, const int32_t* __restrict__ us,
+                                                  const int32_t* __restrict__ is, int n,
+                                                  const float* __restrict__ Fcur, float* __restrict__ Fnext,
+                                                  float* __restrict__ WTnext, float* __restrict__ M,
+                                                  float* __restrict__ V, AdamArgs a) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int jx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (jx >= njobs) return;
+  const NcfJob J = jobs[jx];
+  if (J.kind == kJobDx0) {  // dX_0 [16 samples x 16 columns] = dPre_0 . W_0 -> dPm[u], dQm[i]
+    if (J.m0 >= n) return;
+    const f32x4 acc = tile_xwt(J.A + (int64_t)J.m0 * J.lda, J.lda, P.WT[0], J.lda, J.k0, J.K, lane);
+    const int kk = J.k0 + r, E = D.E;
+    if (kk >= J.K) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int32_t u, i;
+      sample_ids(D, us, is, J.m0 + 4 * g + q, n, u, i);
+      if (u < 0) continue;
+      if (kk < E)
+        atomicAdd(G.Pm + (int64_t)u * E + kk, acc[q]);
+      else
+        atomicAdd(G.Qm + (int64_t)i * E + (kk - E), acc[q]);
+    }
+    return;
+  }
+  // C[16 x 16] = sum_s A[s][m0 + m] B[s][k0 + k] (B[s] for a vector job), the samples in order
+  const bool vec = J.kind == kJobVec;
+  const bool mok = J.m0 + r < J.M, kok = vec || J.k0 + r < J.K;
+  const float* pa = J.A + J.m0 + r;
+  const float* pb = vec ? J.B : J.B + J.k0 + r;
+  const int ldb = vec ? 1 : J.ldb;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 16;  // samples 4U per round of loads
+  for (int s4 = 0; s4 < n; s4 += 4 * U) {
+    float av[U], bv[U];
+#pragma unroll
+    for (int e = 0; e < U; ++e) {
+      const int s = s4 + 4 * e + g;
+      av[e] = (s < n && mok) ? pa[(int64_t)s * J.lda] : 0.f;
+      bv[e] = (s < n && kok) ? pb[(int64_t)s * ldb] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < U; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
+  }
+  if (vec && r != 0) return;  // a vector job's 16 columns are equal
+  const int kk = J.k0 + r;
+  if (!vec && kk >= J.K) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int mm = J.m0 + 4 * g + q;
+    if (mm >= J.M) continue;
+    const int j = vec ? J.flat + mm : J.flat + mm * J.K + kk;
+    float p = Fcur[j], m = M[j], v = V[j];
+    adam1(p, m, v, acc[q], a);
+    Fnext[j] = p;
     M[j] = m;
     V[j] = v;
-    for (int l = 0; l < D.L; ++l) {
-      const int w0 = D.off_W[l], K = D.nin[l], N = D.nout[l];
-      if (j >= w0 && j < w0 + N * K) {
-        const int nn = (j - w0) / K, kk = (j - w0) % K;
-        P.WT[l][(int64_t)kk * N + nn] = p;
-      }
-    }
+    if (J.layer >= 0) WTnext[J.wt + (int64_t)kk * J.M + mm] = p;
   }
 }
 
@@ -540,33 +570,45 @@ static unsigned grid1(int64_t n) {
 }
 
 // dynamic LDS beyond the default 64 KB window (up to the CU's 160 KB) must be opted into
-static hipError_t allow_lds(size_t bytes) {
-  static size_t allowed = 64 * 1024;
-  if (bytes <= allowed) return hipSuccess;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_ncf_fwdbwd),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess) allowed = bytes;
-  return e;
+template <typename K>
+static hipError_t allow_lds(K* kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const int32_t* u,
-                  const int32_t* i, const float* y, int n, int32_t t, float* partial,
-                  double* loss, int32_t* err, hipStream_t s) {
+static hipError_t front_mid(const Dims& D, const Params& P, const Grads& G, const Acts& A,
+                            const int32_t* u, const int32_t* i, const float* y, int n, double* loss,
+                            int32_t* err, float* z, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (hipError_t e = allow_lds(fwdbwd_lds_bytes(D))) return e;
-  const unsigned blocks = (unsigned)((n + kSamples - 1) / kSamples);
-  k_ncf_fwdbwd<<<blocks, 1024, fwdbwd_lds_bytes(D), s>>>(D, P, G, u, i, y, n, t, partial, loss, err,
-                                                         nullptr);
+  const unsigned groups = (unsigned)((n + kSamples - 1) / kSamples);
+  if (D.model != kGMF) {
+    const size_t fb = sizeof(float) * (size_t)kSamples * front_ld(D);
+    if (hipError_t e = allow_lds(k_ncf_front, fb)) return e;
+    k_ncf_front<<<dim3(groups, (unsigned)((D.nout[0] + 63) / 64)), 256, fb, s>>>(D, P, A, u, i, n);
+  }
+  const size_t mb = sizeof(float) * (size_t)lds_plan(D).total;
+  if (hipError_t e = allow_lds(k_ncf_mid, mb)) return e;
+  k_ncf_mid<<<groups, 1024, mb, s>>>(D, P, G, A, u, i, y, n, loss, err, z);
   return hipGetLastError();
 }
 
-hipError_t forward(const Dims& D, const Params& P, const int32_t* u, const int32_t* i, int n,
-                   float* z, int32_t* err, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  if (hipError_t e = allow_lds(fwdbwd_lds_bytes(D))) return e;
-  const unsigned blocks = (unsigned)((n + kSamples - 1) / kSamples);
-  k_ncf_fwdbwd<<<blocks, 1024, fwdbwd_lds_bytes(D), s>>>(D, P, Grads{}, u, i, nullptr, n, 0,
-                                                         nullptr, nullptr, err, z);
+hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
+                  const int32_t* i, const float* y, int n, double* loss, int32_t* err, hipStream_t s) {
+  return front_mid(D, P, G, A, u, i, y, n, loss, err, nullptr, s);
+}
+
+hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
+                   int n, float* z, int32_t* err, hipStream_t s) {
+  return front_mid(D, P, Grads{}, A, u, i, nullptr, n, nullptr, err, z, s);
+}
+
+hipError_t back(const Dims& D, const Params& P, const Grads& G, const NcfJob* jobs, int njobs,
+                const int32_t* u, const int32_t* i, int n, const float* Fcur, float* Fnext,
+                float* WTnext, float* M, float* V, const AdamArgs& a, hipStream_t s) {
+  if (n <= 0 || njobs <= 0) return hipSuccess;
+  k_ncf_back<<<(unsigned)((njobs + 3) / 4), 256, 0, s>>>(D, P, G, jobs, njobs, u, i, n, Fcur, Fnext,
+                                                         WTnext, M, V, a);
   return hipGetLastError();
 }
 
@@ -587,14 +629,6 @@ hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_
 hipError_t adam_rows(const RowSides& R, int64_t n, int32_t t, const AdamArgs& a, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   k_ncf_adam_rows<<<rows_grid(R, n), rows_block(R), 0, s>>>(R, t, a);
-  return hipGetLastError();
-}
-
-hipError_t adam_flat(const Dims& D, const Params& P, float* F, float* M, float* V,
-                     const float* partial, int nparts, int lo, int hi, const AdamArgs& a,
-                     hipStream_t s) {
-  if (hi <= lo) return hipSuccess;
-  k_ncf_adam_flat<<<grid1(hi - lo), 256, 0, s>>>(D, P, F, M, V, partial, nparts, lo, hi, a);
   return hipGetLastError();
 }
 

@@ -2,12 +2,14 @@
 //
 // One handle = one GPU.  It owns, in HBM: the four embedding tables and the flat tower+predict
 // block (the reference's parameters), their Adam moments m and v, the dense embedding gradient
-// rows and per-row current-step stamps, the transposed tower weights, the per-workgroup gradient
-// partials, the training positives and their sorted CSR (the sampler's rejection set).
+// rows and per-row current-step stamps, the tower + predict block and its transposed weights
+// (double-buffered: a step reads one copy and writes the other), the per-sample activations
+// between the step's launches (Acts) and the backward's job list, the training positives and
+// their sorted CSR (the sampler's rejection set).
 // A step (NCFRecommender.py:278-285): the batch's embedding rows are brought up to step t - 1
-// (k_ncf_catch_up: the zero-gradient Adam steps they missed, in closed form), one k_ncf_fwdbwd
-// launch over the batch (16 samples per workgroup), then Adam over the flat block
-// (k_ncf_adam_flat) and over the batch's embedding rows (k_ncf_adam_rows).  Every read of the
+// (k_ncf_catch_up: the zero-gradient Adam steps they missed, in closed form), the forward and
+// backward (k_ncf_front, k_ncf_mid, then k_ncf_back with the tower + predict layer's Adam), then
+// Adam over the batch's embedding rows (k_ncf_adam_rows).  Every read of the
 // tables from outside a step (predict, get / set_param) first brings the rows it reads to the
 // current step, so every observable value is torch's dense Adam.
 #include <hip/hip_runtime.h>
@@ -38,10 +40,15 @@ struct ncf_handle {
   float* emb_m[4] = {};
   float* emb_v[4] = {};
   int64_t emb_rows[4] = {}, emb_cols[4] = {};
-  float *F = nullptr, *Fm = nullptr, *Fv = nullptr;  // flat tower + predict block
-  float* WT = nullptr;
-  float* partial = nullptr;
+  float *F = nullptr, *Fm = nullptr, *Fv = nullptr;  // flat tower + predict block (current copy)
+  float* WT = nullptr;                                // its transposed tower weights (current copy)
+  float *Fo = nullptr, *WTo = nullptr;                // the other copies (the next step's)
+  int wt_n = 0;                                       // floats of the W^T block
   int64_t max_blocks = 0;
+  Acts A{};                                           // training activations, max_blocks * 16 rows
+  float* acts = nullptr;
+  NcfJob* d_jobs = nullptr;
+  int njobs = 0;
   // training data
   int64_t npos = 0;
   int32_t *d_pos_u = nullptr, *d_pos_i = nullptr, *d_indices = nullptr;
@@ -206,6 +213,96 @@ static int ncf_flush(ncf_handle* h) {
   return 0;
 }
 
+// Params' tower / predict pointers into the current copy of the flat block
+static void point_params(ncf_handle* h) {
+  const Dims& D = h->D;
+  int wo = 0;
+  for (int l = 0; l < D.L; ++l) {
+    h->P.W[l] = h->F + D.off_W[l];
+    h->P.b[l] = h->F + D.off_b[l];
+    h->P.WT[l] = h->WT + wo;
+    wo += D.nin[l] * D.nout[l];
+  }
+  h->P.wp = h->F + D.off_wp;
+  h->P.bp = h->F + D.off_bp;
+}
+
+// W^T from W in the current copy, then the other copy made equal (after init / set_param)
+static int sync_copies(ncf_handle* h) {
+  HIPCHK(transpose(h->D, h->P, h->stream));
+  HIPCHK(hipMemcpyAsync(h->Fo, h->F, 4 * (size_t)h->D.flat_n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->WTo, h->WT, 4 * (size_t)h->wt_n, hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
+// Acts carved from one buffer of `rows` sample rows (base null: the floats needed)
+static int64_t carve_acts(const Dims& D, int64_t rows, bool train, float* base, Acts* A) {
+  int64_t off = 0;
+  auto take = [&](int64_t n) {
+    float* p = base ? base + off : nullptr;
+    off += (n + 15) & ~(int64_t)15;
+    return p;
+  };
+  Acts a{};
+  if (train) a.X0 = take(rows * 2 * D.E);
+  a.Xp = take(rows * D.pred);
+  for (int l = 1; l < D.L; ++l) {
+    a.H[l] = take(rows * D.nin[l]);
+    a.ldH[l] = D.nin[l];
+  }
+  a.H[D.L] = a.Xp ? a.Xp + (D.model == kNeuMF ? D.d : 0) : nullptr;
+  a.ldH[D.L] = D.pred;
+  a.dz = take(rows);
+  if (train) {
+    for (int l = 0; l < D.L; ++l) a.dPre[l] = take(rows * D.nout[l]);
+    a.ones = take(rows);
+  }
+  if (A) *A = a;
+  return off;
+}
+
+// k_ncf_back's jobs: dX_0 tiles (the longest, first), weight-gradient tiles, bias and predict
+// vectors; every element of the model's tower + predict block belongs to exactly one job
+static std::vector<NcfJob> make_jobs(const ncf_handle* h) {
+  const Dims& D = h->D;
+  const Acts& A = h->A;
+  std::vector<NcfJob> v;
+  auto job = [&](int kind, const float* a, int lda, const float* b, int ldb, int m0, int k0, int M, int K,
+                 int flat, int layer, int wt) {
+    NcfJob j;
+    j.A = a;
+    j.B = b;
+    j.lda = lda;
+    j.ldb = ldb;
+    j.m0 = m0;
+    j.k0 = k0;
+    j.M = M;
+    j.K = K;
+    j.flat = flat;
+    j.kind = kind;
+    j.layer = layer;
+    j.wt = wt;
+    v.push_back(j);
+  };
+  if (D.model != kGMF) {
+    for (int64_t s0 = 0; s0 < h->max_blocks * kSamples; s0 += kSamples)
+      for (int k0 = 0; k0 < 2 * D.E; k0 += 16)
+        job(kJobDx0, A.dPre[0], D.nout[0], nullptr, 0, (int)s0, k0, kSamples, 2 * D.E, 0, -1, 0);
+    int wo = 0;
+    for (int l = 0; l < D.L; ++l) {
+      const int M = D.nout[l], K = D.nin[l];
+      const float* H = l == 0 ? A.X0 : A.H[l];
+      for (int m0 = 0; m0 < M; m0 += 16)
+        for (int k0 = 0; k0 < K; k0 += 16) job(kJobTile, A.dPre[l], M, H, K, m0, k0, M, K, D.off_W[l], l, wo);
+      for (int m0 = 0; m0 < M; m0 += 16) job(kJobVec, A.dPre[l], M, A.ones, 1, m0, 0, M, 1, D.off_b[l], -1, 0);
+      wo += M * K;
+    }
+  }
+  for (int m0 = 0; m0 < D.pred; m0 += 16) job(kJobVec, A.Xp, D.pred, A.dz, 1, m0, 0, D.pred, 1, D.off_wp, -1, 0);
+  job(kJobVec, A.ones, 1, A.dz, 1, 0, 0, 1, 1, D.off_bp, -1, 0);
+  return v;
+}
+
 static SamplerArgs ncf_sampler(ncf_handle* h) {
   SamplerArgs a{};
   a.pos_u = h->d_pos_u;
@@ -239,15 +336,10 @@ static int ncf_check_err(ncf_handle* h) {
 static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const float* y, int n) {
   if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   const int32_t t = ++h->t;
-  const int nb = (n + kSamples - 1) / kSamples;
   const RowSides R = row_sides(h, u, i);
   {
     NcfProf ps(h, 3);
     HIPCHK(catch_up(R, n, catch_args(h, t - 1), h->stream));
-  }
-  {
-    NcfProf ps(h, 1);
-    HIPCHK(fwdbwd(h->D, h->P, h->G, u, i, y, n, t, h->partial, h->d_loss, h->d_err, h->stream));
   }
   const double b1 = h->cfg.beta1, b2 = h->cfg.beta2;
   AdamArgs a;
@@ -257,9 +349,16 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   a.eps = h->cfg.eps;
   a.step_size = (float)((double)h->cfg.lr / (1.0 - std::pow(b1, (double)t)));
   a.bc2_sqrt = (float)std::sqrt(1.0 - std::pow(b2, (double)t));
+  {
+    NcfProf ps(h, 1);
+    HIPCHK(fwdbwd(h->D, h->P, h->G, h->A, u, i, y, n, h->d_loss, h->d_err, h->stream));
+    HIPCHK(back(h->D, h->P, h->G, h->d_jobs, h->njobs, u, i, n, h->F, h->Fo, h->WTo, h->Fm, h->Fv, a,
+                h->stream));
+  }
+  std::swap(h->F, h->Fo);  // the updated tower / predict weights are the current copy
+  std::swap(h->WT, h->WTo);
+  point_params(h);
   NcfProf ps(h, 2);
-  const int lo = h->D.model == kGMF ? h->D.off_wp : 0;  // GMF: the tower has no gradient
-  HIPCHK(adam_flat(h->D, h->P, h->F, h->Fm, h->Fv, h->partial, nb, lo, h->D.flat_n, a, h->stream));
   HIPCHK(adam_rows(R, n, t, a, h->stream));
   return 0;
 }
@@ -400,14 +499,26 @@ int ncf_create(const ncf_config* cfg, ncf_handle** out) {
   HIPCHK(hipMemsetAsync(h->cur_u, 0xFF, 4 * D.U, h->stream));  // -1: never touched
   HIPCHK(hipMemsetAsync(h->cur_i, 0xFF, 4 * D.I, h->stream));
   TRY(dalloc(&h->F, D.flat_n));
+  TRY(dalloc(&h->Fo, D.flat_n));
   TRY(dalloc(&h->Fm, D.flat_n));
   TRY(dalloc(&h->Fv, D.flat_n));
   TRY(memz(h->Fm, 4 * D.flat_n));
   TRY(memz(h->Fv, 4 * D.flat_n));
   int wt = 0;
   for (int l = 0; l < D.L; ++l) wt += D.nin[l] * D.nout[l];
-  TRY(dalloc(&h->WT, std::max(wt, 1)));
-  TRY(dalloc(&h->partial, h->max_blocks * D.flat_n));
+  h->wt_n = std::max(wt, 1);
+  TRY(dalloc(&h->WT, h->wt_n));
+  TRY(dalloc(&h->WTo, h->wt_n));
+  {
+    const int64_t rows = h->max_blocks * kSamples;
+    TRY(dalloc(&h->acts, carve_acts(D, rows, true, nullptr, nullptr)));
+    carve_acts(D, rows, true, h->acts, &h->A);
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->A.ones), 0x3F800000, rows, h->stream));
+    const std::vector<NcfJob> jobs = make_jobs(h);
+    h->njobs = (int)jobs.size();
+    TRY(dalloc(&h->d_jobs, h->njobs));
+    HIPCHK(hipMemcpy(h->d_jobs, jobs.data(), sizeof(NcfJob) * jobs.size(), hipMemcpyHostToDevice));
+  }
   TRY(dalloc(&h->d_loss, kLossSlotsNcf));
   TRY(dalloc(&h->d_err, 1));
   TRY(memz(h->d_err, 4));
@@ -415,15 +526,7 @@ int ncf_create(const ncf_config* cfg, ncf_handle** out) {
   h->P.Qg = h->emb[1];
   h->P.Pm = h->emb[2];
   h->P.Qm = h->emb[3];
-  int wo = 0;
-  for (int l = 0; l < D.L; ++l) {
-    h->P.W[l] = h->F + D.off_W[l];
-    h->P.b[l] = h->F + D.off_b[l];
-    h->P.WT[l] = h->WT + wo;
-    wo += D.nin[l] * D.nout[l];
-  }
-  h->P.wp = h->F + D.off_wp;
-  h->P.bp = h->F + D.off_bp;
+  point_params(h);
   // NCF._init_weight_ (NCFRecommender.py:65-82): normal(0.01) embeddings, xavier_uniform tower,
   // kaiming_uniform(a=1, 'sigmoid') predictor, zero biases
   hipError_t e = hipSuccess;
@@ -434,7 +537,7 @@ int ncf_create(const ncf_config* cfg, ncf_handle** out) {
     e = init(h->P.W[l], (int64_t)D.nin[l] * D.nout[l], 1,
              (float)std::sqrt(6.0 / (D.nin[l] + D.nout[l])), h->k0, h->k1, 16u + l, h->stream);
   if (e == hipSuccess) e = init(h->P.wp, D.pred, 1, (float)std::sqrt(3.0 / D.pred), h->k0, h->k1, 32u, h->stream);
-  if (e == hipSuccess) e = transpose(D, h->P, h->stream);
+  if (e == hipSuccess && sync_copies(h)) e = hipErrorUnknown;
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) {
     ncf_destroy(h);
@@ -455,7 +558,7 @@ int ncf_destroy(ncf_handle* h) {
       if (x) (void)!hipFree(x);
   }
   void* ptrs[] = {h->G.Pg, h->G.Qg, h->G.Pm, h->G.Qm, h->cur_u, h->cur_i, h->d_step, h->d_pw, h->F, h->Fm,
-                  h->Fv, h->WT, h->partial, h->d_pos_u, h->d_pos_i, h->d_indices, h->d_indptr,
+                  h->Fv, h->WT, h->Fo, h->WTo, h->acts, h->d_jobs, h->d_pos_u, h->d_pos_i, h->d_indices, h->d_indptr,
                   h->d_u, h->d_i, h->d_y, h->d_loss, h->d_err};
   for (void* x : ptrs)
     if (x) (void)!hipFree(x);
@@ -490,7 +593,7 @@ int ncf_set_param(ncf_handle* h, int32_t index, const float* data) {
     if (int rc = ncf_flush(h)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(p, data, 4 * r * c, hipMemcpyHostToDevice));
-  HIPCHK(transpose(h->D, h->P, h->stream));
+  if (int rc = sync_copies(h)) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -638,17 +741,23 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
   const bool whole = 2 * n >= h->D.U + h->D.I;
   if (whole)
     if (int r = ncf_flush(h)) return r;
+  // ids, logits and the forward's activations for chunks of up to 64k samples
+  const int64_t chunk = std::min<int64_t>((n + kSamples - 1) / kSamples * kSamples, 1 << 16);
+  const int64_t act_n = carve_acts(h->D, chunk, false, nullptr, nullptr);
   int32_t* buf = nullptr;
-  if (int r = dalloc(&buf, 3 * n)) return r;
+  const int64_t act_off = (3 * n + 15) & ~(int64_t)15;  // float4-aligned activations
+  if (int r = dalloc(&buf, act_off + act_n)) return r;
   float* z = reinterpret_cast<float*>(buf + 2 * n);
+  Acts A;
+  carve_acts(h->D, chunk, false, reinterpret_cast<float*>(buf + act_off), &A);
   int rc = 0;
   hipError_t e = hipMemcpyAsync(buf, u, 4 * n, hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(buf + n, i, 4 * n, hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess && !whole && h->flushed != h->t)
     e = catch_up(row_sides(h, buf, buf + n), n, catch_args(h, h->t), h->stream);
-  for (int64_t off = 0; off < n && e == hipSuccess; off += (1 << 30))
-    e = forward(h->D, h->P, buf + off, buf + n + off, (int)std::min<int64_t>(n - off, 1 << 30), z + off,
-                h->d_err, h->stream);
+  for (int64_t off = 0; off < n && e == hipSuccess; off += chunk)
+    e = forward(h->D, h->P, A, buf + off, buf + n + off, (int)std::min(n - off, chunk), z + off, h->d_err,
+                h->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(out, z, 4 * n, hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) rc = fail(BPRMF_E_HIP, "ncf_predict: %s", hipGetErrorString(e));

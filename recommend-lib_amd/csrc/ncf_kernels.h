@@ -58,23 +58,49 @@ struct CatchArgs {  // zero-gradient Adam steps up to step `target`
   int32_t target;
 };
 
+// Per-sample activations and gradients between the step's launches (rows = samples).
+struct Acts {
+  float* X0;                  // [rows x 2E] tower input [Pm[u], Qm[i]] (training only)
+  float* H[kMaxLayers + 1];   // H[l], l = 1 .. L: h_l, layer l-1's output; H[L] is Xp's tower part
+  int ldH[kMaxLayers + 1];
+  float* Xp;                  // [rows x pred] predict-layer input [Pg[u] * Qg[i], h_L]
+  float* dz;                  // [rows] dL/dz
+  float* dPre[kMaxLayers];    // [rows x nout[l]] gradient of layer l's pre-activation (training only)
+  float* ones;                // [rows] 1.0: bias gradients as contractions (training only)
+};
+
+// One wave of k_ncf_back: a [16 x 16] tile of sum_s A[s][m] B[s][k] (weight gradient, then Adam
+// on its elements), a vector sum_s A[s][m] B[s] (bias / predict layer, then Adam), or a
+// [16 samples x 16 columns] tile of dX_0 = dPre_0 . W_0 (into the MLP embedding gradients).
+enum { kJobTile = 0, kJobVec = 1, kJobDx0 = 2 };
+struct NcfJob {
+  const float* A;
+  const float* B;
+  int lda, ldb, m0, k0, M, K;
+  int flat;   // flat-block index of element (m, k): flat + m K + k (vector: flat + m)
+  int kind;
+  int layer;  // tiles: the W^T copy refreshed (its offset wt in the W^T block); else -1
+  int wt;
+};
+
 struct AdamArgs {
   float one_minus_b1, b2, one_minus_b2, eps, step_size, bc2_sqrt;
 };
 
 size_t fwdbwd_lds_bytes(const Dims& D);
-hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const int32_t* u,
-                  const int32_t* i, const float* y, int n, int32_t t, float* partial,
-                  double* loss, int32_t* err, hipStream_t s);
-hipError_t forward(const Dims& D, const Params& P, const int32_t* u, const int32_t* i, int n,
-                   float* z, int32_t* err, hipStream_t s);
+// k_ncf_front + k_ncf_mid (training: activations and gradients into A, loss, embedding GMF grads)
+hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
+                  const int32_t* i, const float* y, int n, double* loss, int32_t* err, hipStream_t s);
+hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
+                   int n, float* z, int32_t* err, hipStream_t s);
+// k_ncf_back: the step's jobs; the tower / predict weights from Fcur (and P) to Fnext / WTnext
+hipError_t back(const Dims& D, const Params& P, const Grads& G, const NcfJob* jobs, int njobs,
+                const int32_t* u, const int32_t* i, int n, const float* Fcur, float* Fnext,
+                float* WTnext, float* M, float* V, const AdamArgs& a, hipStream_t s);
 // rows of the samples (or every row when ids are null) brought to c.target; cur = c.target
 hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_t s);
 // step t of Adam on the rows of the samples (g = the gradient row, then zeroed); cur = t
 hipError_t adam_rows(const RowSides& R, int64_t n, int32_t t, const AdamArgs& a, hipStream_t s);
-hipError_t adam_flat(const Dims& D, const Params& P, float* F, float* M, float* V,
-                     const float* partial, int nparts, int lo, int hi, const AdamArgs& a,
-                     hipStream_t s);
 hipError_t transpose(const Dims& D, const Params& P, hipStream_t s);
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* u,
                   int32_t* i, float* y, int32_t* err, hipStream_t s);

@@ -28,9 +28,9 @@ static __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpr
 
 // ---- forward / backward ----------------------------------------------------------------------
 // A step's tower runs in three launches, so that no kernel streams every weight through one CU:
-//   k_ncf_front  layer 0 (the widest): one workgroup per (16 samples, 64 output columns); gathers
-//                the tower input [Pm[u], Qm[i]] and writes h_1 (and the input itself, X0, for
-//                the weight gradient).
+//   k_ncf_front  layer 0 (the widest): one workgroup per (16 samples, 16 output columns), K split
+//                over its waves, reading the tower input [Pm[u], Qm[i]] straight from the rows;
+//                writes h_1 (and the input itself, X0, for the weight gradient).
 //   k_ncf_mid    one workgroup per 16 samples: layers 1 .. L-1, the prediction, BCE and dL/dz,
 //                the GMF embedding gradients, then the tower backward down to dPre_0 (the
 //                gradient of layer 0's pre-activation).  Activations and pre-activation
@@ -68,34 +68,30 @@ static __host__ __device__ inline Lds lds_plan(const Dims& D) {
   p.total = off;
   return p;
 }
-static __host__ __device__ inline int front_ld(const Dims& D) { return 2 * D.E + 4; }
+size_t fwdbwd_lds_bytes(const Dims& D) { return sizeof(float) * (size_t)lds_plan(D).total; }
 
-size_t fwdbwd_lds_bytes(const Dims& D) {
-  return sizeof(float) * (size_t)std::max(lds_plan(D).total, kSamples * front_ld(D));
-}
-
-// y[16 x 16 tile] = X[16 x K] (stride ldx) . W[n0.., :]^T (global, W[n][k], stride K):
-// 16x16x4 f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (K % 4 == 0).  The W rows
-// come from L2/HBM: eight k-steps of loads are issued before their 32 MFMAs, so one latency is
-// paid per eight steps, not per step.
-static __device__ __forceinline__ f32x4 tile_xwt(const float* X, int ldx, const float* W, int K,
-                                                 int n0, int nmax, int lane) {
+// y[16 x 16 tile] = X[16 x kc] . W[n0.., 0 .. kc)^T (global, W[n][k], row stride ldw): 16x16x4
+// f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (kc % 4 == 0); lane l supplies
+// row l & 15 of X from xr (0 where !xok).  The W rows come from L2/HBM: eight k-steps of loads
+// are issued before their 32 MFMAs, so one latency is paid per eight steps, not per step.
+static __device__ __forceinline__ f32x4 tile_xwt(const float* xr, bool xok, const float* W, int ldw,
+                                                 int kc, int n0, int nmax, int lane) {
   constexpr int U = 8;
   const int r = lane & 15, g = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const bool nok = n0 + r < nmax;
-  const float* wr = W + (int64_t)(n0 + r) * K;
-  for (int t0 = 0; 16 * t0 < K; t0 += U) {
+  const float* wr = W + (int64_t)(n0 + r) * ldw;
+  for (int t0 = 0; 16 * t0 < kc; t0 += U) {
     float4 a[U], b[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int k = 16 * (t0 + q) + 4 * g;
-      b[q] = (nok && k < K) ? ld4(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      b[q] = (nok && k < kc) ? ld4(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int k = 16 * (t0 + q) + 4 * g;
-      a[q] = k < K ? *reinterpret_cast<const float4*>(X + r * ldx + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[q] = (xok && k < kc) ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
@@ -130,47 +126,55 @@ static __device__ __forceinline__ void sample_ids(const Dims& D, const int32_t* 
   }
 }
 
+// one workgroup per (16 samples, 16 output columns); wave w of the ks parts of K = 2E takes
+// k in [w K/ks, (w+1) K/ks) straight from the embedding rows (the first half from Pm[u], the
+// second from Qm[i]), the parts summed in wave order through LDS.  The y = 0 workgroups also
+// store the tower input rows (X0) for the weight gradient.
 __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
                                                    const int32_t* __restrict__ us,
                                                    const int32_t* __restrict__ is, int n) {
-  extern __shared__ float sm[];
-  __shared__ int32_t su[kSamples], si[kSamples];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int s0 = blockIdx.x * kSamples, E = D.E, K = 2 * E, N = D.nout[0], ld = front_ld(D);
-  if (tid < kSamples) sample_ids(D, us, is, s0 + tid, n, su[tid], si[tid]);
-  __syncthreads();
-  const bool keep = A.X0 && blockIdx.y == 0;  // one workgroup per sample group stores X0
-  const int q = K / 4;
-  for (int x = tid; x < kSamples * q; x += blockDim.x) {
-    const int s = x / q, c = 4 * (x % q);
-    const int32_t u = su[s], i = si[s];
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < E) {
-      if (u >= 0) v = ld4(P.Pm + (int64_t)u * E + c);
-    } else if (i >= 0) {
-      v = ld4(P.Qm + (int64_t)i * E + (c - E));
+  __shared__ f32x4 s_acc[3][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15;
+  const int s0 = blockIdx.x * kSamples, E = D.E, K = 2 * E, N = D.nout[0], n0 = 16 * blockIdx.y;
+  const int ks = E % 8 == 0 ? 4 : 2, kq = K / ks;  // parts of K, each a multiple of 4 floats
+  if (A.X0 && blockIdx.y == 0) {
+    const int q = K / 4;
+    for (int x = tid; x < kSamples * q; x += blockDim.x) {
+      const int s = x / q, c = 4 * (x % q);
+      int32_t u, i;
+      sample_ids(D, us, is, s0 + s, n, u, i);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u >= 0) v = c < E ? ld4(P.Pm + (int64_t)u * E + c) : ld4(P.Qm + (int64_t)i * E + (c - E));
+      if (s0 + s < n) *reinterpret_cast<float4*>(A.X0 + (int64_t)(s0 + s) * K + c) = v;
     }
-    *reinterpret_cast<float4*>(sm + s * ld + c) = v;
-    if (keep && s0 + s < n) *reinterpret_cast<float4*>(A.X0 + (int64_t)(s0 + s) * K + c) = v;
   }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (wave < ks) {
+    int32_t u, i;
+    sample_ids(D, us, is, s0 + r, n, u, i);
+    const int kb = wave * kq;  // this part's first k; < E: the user's row
+    const float* xr = kb < E ? P.Pm + (int64_t)max(u, 0) * E + kb : P.Qm + (int64_t)max(i, 0) * E + (kb - E);
+    acc = tile_xwt(xr, u >= 0, P.W[0] + kb, K, kq, n0, N, lane);
+  }
+  if (wave > 0) s_acc[wave - 1][lane] = acc;
   __syncthreads();
-  const int tile = 4 * blockIdx.y + wave;
-  if (16 * tile >= N) return;
-  const f32x4 acc = tile_xwt(sm, ld, P.W[0], K, 16 * tile, N, lane);
-  const int nn = 16 * tile + (lane & 15);
+  if (wave > 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) acc += s_acc[w][lane];
+  const int nn = n0 + r;
   if (nn >= N) return;
   const float bias = P.b[0][nn];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int s = 4 * (lane >> 4) + r;
-    if (s0 + s < n) A.H[1][(int64_t)(s0 + s) * A.ldH[1] + nn] = fmaxf(acc[r] + bias, 0.f);
+  for (int q = 0; q < 4; ++q) {
+    const int s = 4 * (lane >> 4) + q;
+    if (s0 + s < n) A.H[1][(int64_t)(s0 + s) * A.ldH[1] + nn] = fmaxf(acc[q] + bias, 0.f);
   }
 }
 
 __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Acts A,
                                                   const int32_t* __restrict__ us,
                                                   const int32_t* __restrict__ is,
-                                                  const float* __restrict__ ys, int n,
+                                                  const float* __restrict__ ys, int n, int32_t t,
                                                   double* __restrict__ loss,
                                                   int32_t* __restrict__ err,
                                                   float* __restrict__ zout) {
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Act
       const float* X = sm + Lp.h[l];
       float* Y = sm + Lp.h[l + 1];
       for (int tile = wave; 16 * tile < N; tile += NW) {
-        const f32x4 acc = tile_xwt(X, Lp.ldh[l], P.W[l], K, 16 * tile, N, lane);
+        const f32x4 acc = tile_xwt(X + (lane & 15) * Lp.ldh[l], true, P.W[l], K, K, 16 * tile, N, lane);
         const int nn = 16 * tile + (lane & 15);
         if (nn < N) {
           const float bias = P.b[l][nn];
@@ -290,6 +294,10 @@ __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Act
       atomicAdd(G.Qg + (int64_t)i * d + k, gk * sm[Lp.eu + s * (d + 4) + k]);
     }
   }
+  if (tid < kSamples && su[tid] >= 0) {  // the rows this step's row Adam will move
+    G.touch_u[su[tid]] = t;
+    G.touch_i[si[tid]] = t;
+  }
   if (!mlp) return;
   // 5. dPre_{L-1} = dz wp[tower part] * (h_L > 0), in place of h_L
   float* hw = sm + Lp.hL;
@@ -311,7 +319,7 @@ __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Act
     float* H = sm + Lp.h[l];
     const int ldp = Lp.ldh[l + 1], ldx = Lp.ldh[l];
     for (int tile = wave; 16 * tile < K; tile += NW) {
-      const f32x4 acc = tile_xwt(dP, ldp, P.WT[l], N, 16 * tile, K, lane);
+      const f32x4 acc = tile_xwt(dP + (lane & 15) * ldp, true, P.WT[l], N, N, 16 * tile, K, lane);
       const int kk = 16 * tile + (lane & 15);
       if (kk < K) {
 #pragma unroll
@@ -345,26 +353,26 @@ static __device__ __forceinline__ void adam1(float& p, float& m, float& v, float
 // and per-term factors come from tables built once on the host (in double).
 
 // one workgroup per (sample, side): thread 0 claims the row (cur: c -> target by CAS, so a row
-// repeated in the batch is caught up once); row = blockIdx.x when the sides carry no ids
-static __device__ __forceinline__ int64_t side_row(const RowSides& R, int side) {
-  const int64_t x = blockIdx.x;
+// repeated in the batch is caught up once); row = x when the sides carry no ids
+static __device__ __forceinline__ int64_t side_row(const RowSides& R, int64_t x, int side) {
   if (!R.ids[0]) return x < R.side[side].rows ? x : -1;
   const int32_t u = R.ids[0][x], i = R.ids[1][x];
   if ((uint64_t)u >= (uint64_t)R.U || (uint64_t)i >= (uint64_t)R.I) return -1;  // no gradient
   return side ? i : u;
 }
 
-__global__ __launch_bounds__(1024) void k_ncf_catch_up(RowSides R, CatchArgs c) {
+// row x of side `side` brought to c.target; a row touched at step `skip` (>= 0) is left to that
+// step's Adam (k_ncf_rows: it runs in the same launch and brings the row to c.target itself)
+static __device__ __forceinline__ void catch_row(const RowSides& R, int64_t x, int side, const CatchArgs& c,
+                                                 int32_t skip) {
   __shared__ float2 s_term[kCatchTerms];
   __shared__ int64_t s_row;
   __shared__ int32_t s_from;
-
-  const int side = blockIdx.y;
   const RowSide S = side ? R.side[1] : R.side[0];  // no dynamic index into the kernel arguments
   if (threadIdx.x == 0) {
-    const int64_t r = side_row(R, side);
+    const int64_t r = side_row(R, x, side);
     int32_t from = -1;
-    if (r >= 0) {
+    if (r >= 0 && (skip < 0 || S.touch[r] != skip)) {
       const int32_t old = S.cur[r];
       if (old >= 0 && old < c.target && atomicCAS(S.cur + r, old, c.target) == old) from = old;
     }
@@ -386,8 +394,8 @@ __global__ __launch_bounds__(1024) void k_ncf_catch_up(RowSides R, CatchArgs c) 
   const float dm = exp2f(k * c.log2_b1), dv = exp2f(k * c.log2_b2), eps = c.eps;
   for (int e = threadIdx.x; e < S.cols[0] + S.cols[1]; e += blockDim.x) {
     const int tb = e >= S.cols[0];
-    const int64_t x = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
-    const float m = S.M[tb][x], v = S.V[tb][x], sv = sqrtf(v);
+    const int64_t o = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
+    const float m = S.M[tb][o], v = S.V[tb][o], sv = sqrtf(v);
     float acc0 = 0.f, acc1 = 0.f;
     int j = 0;
     for (; j + 1 < J; j += 2) {
@@ -396,20 +404,20 @@ __global__ __launch_bounds__(1024) void k_ncf_catch_up(RowSides R, CatchArgs c) 
       acc1 = fmaf(q1.x, __builtin_amdgcn_rcpf(fmaf(sv, q1.y, eps)), acc1);
     }
     if (j < J) acc0 = fmaf(s_term[j].x, __builtin_amdgcn_rcpf(fmaf(sv, s_term[j].y, eps)), acc0);
-    S.W[tb][x] -= m * (acc0 + acc1);
-    S.M[tb][x] = m * dm;
-    S.V[tb][x] = v * dv;
+    S.W[tb][o] -= m * (acc0 + acc1);
+    S.M[tb][o] = m * dm;
+    S.V[tb][o] = v * dv;
   }
 }
 
-// Adam step t on the batch's rows (the rows are at step t - 1 or never touched): g = the
+// Adam step t on row x of side `side` (the row is at step t - 1 or never touched): g = the
 // gradient row (zeroed for the next step), cur = t; a row repeated in the batch is stepped once
-__global__ __launch_bounds__(1024) void k_ncf_adam_rows(RowSides R, int32_t t, AdamArgs a) {
+static __device__ __forceinline__ void adam_row(const RowSides& R, int64_t x, int side, int32_t t,
+                                                const AdamArgs& a) {
   __shared__ int64_t s_row;
-  const int side = blockIdx.y;
-  const RowSide S = side ? R.side[1] : R.side[0];  // no dynamic index into the kernel arguments
+  const RowSide S = side ? R.side[1] : R.side[0];
   if (threadIdx.x == 0) {
-    int64_t r = side_row(R, side);
+    int64_t r = side_row(R, x, side);
     if (r >= 0) {
       const int32_t old = S.cur[r];
       if (old == t || atomicCAS(S.cur + r, old, t) != old) r = -1;
@@ -421,14 +429,31 @@ __global__ __launch_bounds__(1024) void k_ncf_adam_rows(RowSides R, int32_t t, A
   if (r < 0) return;
   for (int e = threadIdx.x; e < S.cols[0] + S.cols[1]; e += blockDim.x) {
     const int tb = e >= S.cols[0];
-    const int64_t x = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
-    float p = S.W[tb][x], m = S.M[tb][x], v = S.V[tb][x];
-    adam1(p, m, v, S.G[tb][x], a);
-    S.G[tb][x] = 0.f;
-    S.W[tb][x] = p;
-    S.M[tb][x] = m;
-    S.V[tb][x] = v;
+    const int64_t o = r * S.cols[tb] + (tb ? e - S.cols[0] : e);
+    float p = S.W[tb][o], m = S.M[tb][o], v = S.V[tb][o];
+    adam1(p, m, v, S.G[tb][o], a);
+    S.G[tb][o] = 0.f;
+    S.W[tb][o] = p;
+    S.M[tb][o] = m;
+    S.V[tb][o] = v;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_ncf_catch_up(RowSides R, CatchArgs c) {
+  catch_row(R, blockIdx.x, blockIdx.y, c, -1);
+}
+
+__global__ __launch_bounds__(1024) void k_ncf_adam_rows(RowSides R, int32_t t, AdamArgs a) {
+  adam_row(R, blockIdx.x, blockIdx.y, t, a);
+}
+
+// the previous step's row Adam (samples [0, np) of Rp, step c.target) and this step's catch-up
+// (samples of Rc) in one launch
+__global__ __launch_bounds__(1024) void k_ncf_rows(RowSides Rp, int np, AdamArgs a, RowSides Rc, CatchArgs c) {
+  if ((int)blockIdx.x < np)
+    adam_row(Rp, blockIdx.x, blockIdx.y, c.target, a);
+  else
+    catch_row(Rc, blockIdx.x - np, blockIdx.y, c, c.target);
 }
 
 // k_ncf_back: one job per wave (NcfJob, built once per handle).  Reads the step's weights at
@@ -446,7 +471,8 @@ __global__ __launch_bounds__(256) void k_ncf_back(Dims D, Params P, Grads G, con
   const NcfJob J = jobs[jx];
   if (J.kind == kJobDx0) {  // dX_0 [16 samples x 16 columns] = dPre_0 . W_0 -> dPm[u], dQm[i]
     if (J.m0 >= n) return;
-    const f32x4 acc = tile_xwt(J.A + (int64_t)J.m0 * J.lda, J.lda, P.WT[0], J.lda, J.k0, J.K, lane);
+    const f32x4 acc = tile_xwt(J.A + (int64_t)(J.m0 + (lane & 15)) * J.lda, true, P.WT[0], J.lda, J.lda,
+                               J.k0, J.K, lane);
     const int kk = J.k0 + r, E = D.E;
     if (kk >= J.K) return;
 #pragma unroll
@@ -468,7 +494,7 @@ __global__ __launch_bounds__(256) void k_ncf_back(Dims D, Params P, Grads G, con
   const float* pb = vec ? J.B : J.B + J.k0 + r;
   const int ldb = vec ? 1 : J.ldb;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr int U = 16;  // samples 4U per round of loads
+  constexpr int U = 32;  // samples 4U per round of loads
   for (int s4 = 0; s4 < n; s4 += 4 * U) {
     float av[U], bv[U];
 #pragma unroll
@@ -578,29 +604,27 @@ static hipError_t allow_lds(K* kernel, size_t bytes) {
 }
 
 static hipError_t front_mid(const Dims& D, const Params& P, const Grads& G, const Acts& A,
-                            const int32_t* u, const int32_t* i, const float* y, int n, double* loss,
+                            const int32_t* u, const int32_t* i, const float* y, int n, int32_t t, double* loss,
                             int32_t* err, float* z, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned groups = (unsigned)((n + kSamples - 1) / kSamples);
-  if (D.model != kGMF) {
-    const size_t fb = sizeof(float) * (size_t)kSamples * front_ld(D);
-    if (hipError_t e = allow_lds(k_ncf_front, fb)) return e;
-    k_ncf_front<<<dim3(groups, (unsigned)((D.nout[0] + 63) / 64)), 256, fb, s>>>(D, P, A, u, i, n);
-  }
+  if (D.model != kGMF)
+    k_ncf_front<<<dim3(groups, (unsigned)((D.nout[0] + 15) / 16)), 256, 0, s>>>(D, P, A, u, i, n);
   const size_t mb = sizeof(float) * (size_t)lds_plan(D).total;
   if (hipError_t e = allow_lds(k_ncf_mid, mb)) return e;
-  k_ncf_mid<<<groups, 1024, mb, s>>>(D, P, G, A, u, i, y, n, loss, err, z);
+  k_ncf_mid<<<groups, 1024, mb, s>>>(D, P, G, A, u, i, y, n, t, loss, err, z);
   return hipGetLastError();
 }
 
 hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
-                  const int32_t* i, const float* y, int n, double* loss, int32_t* err, hipStream_t s) {
-  return front_mid(D, P, G, A, u, i, y, n, loss, err, nullptr, s);
+                  const int32_t* i, const float* y, int n, int32_t t, double* loss, int32_t* err,
+                  hipStream_t s) {
+  return front_mid(D, P, G, A, u, i, y, n, t, loss, err, nullptr, s);
 }
 
 hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
                    int n, float* z, int32_t* err, hipStream_t s) {
-  return front_mid(D, P, Grads{}, A, u, i, nullptr, n, nullptr, err, z, s);
+  return front_mid(D, P, Grads{}, A, u, i, nullptr, n, 0, nullptr, err, z, s);
 }
 
 hipError_t back(const Dims& D, const Params& P, const Grads& G, const NcfJob* jobs, int njobs,
@@ -623,6 +647,13 @@ static unsigned rows_block(const RowSides& R) {
 hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_t s) {
   if (c.target <= 0 || (R.ids[0] && n <= 0)) return hipSuccess;
   k_ncf_catch_up<<<rows_grid(R, n), rows_block(R), 0, s>>>(R, c);
+  return hipGetLastError();
+}
+
+hipError_t rows(const RowSides& Rp, int np, const AdamArgs& a, const RowSides& Rc, int nc,
+                const CatchArgs& c, hipStream_t s) {
+  if (np <= 0) return catch_up(Rc, nc, c, s);
+  k_ncf_rows<<<dim3((unsigned)(np + nc), 2), rows_block(Rc), 0, s>>>(Rp, np, a, Rc, c);
   return hipGetLastError();
 }
 

@@ -9,7 +9,8 @@
 // A step (NCFRecommender.py:278-285): the batch's embedding rows are brought up to step t - 1
 // (k_ncf_catch_up: the zero-gradient Adam steps they missed, in closed form), the forward and
 // backward (k_ncf_front, k_ncf_mid, then k_ncf_back with the tower + predict layer's Adam), then
-// Adam over the batch's embedding rows (k_ncf_adam_rows).  Every read of the
+// Adam over the batch's embedding rows, which runs with the next step's catch-up in one launch
+// (k_ncf_rows; the last step of a call runs it alone, k_ncf_adam_rows).  Every read of the
 // tables from outside a step (predict, get / set_param) first brings the rows it reads to the
 // current step, so every observable value is torch's dense Adam.
 #include <hip/hip_runtime.h>
@@ -64,6 +65,11 @@ struct ncf_handle {
   int32_t t = 0;  // Adam steps taken
   int32_t *cur_u = nullptr, *cur_i = nullptr;  // step each row's p, m, v are current at (-1: never touched)
   int32_t flushed = 0;                         // every row is current at this step
+  struct {                                     // step t's row Adam, run with step t + 1's catch-up
+    const int32_t *u = nullptr, *i = nullptr;
+    int n = 0;
+    AdamArgs a{};
+  } pend;
   float2 *d_step = nullptr, *d_pw = nullptr;   // catch-up tables (CatchArgs)
   int32_t nstep = 0;
   hipStream_t stream = nullptr;
@@ -159,6 +165,7 @@ static RowSides row_sides(const ncf_handle* h, const int32_t* u, const int32_t* 
       S.cols[k] = (int)h->emb_cols[tb];
     }
     S.cur = side ? h->cur_i : h->cur_u;
+    S.touch = side ? h->G.touch_i : h->G.touch_u;
     S.rows = side ? h->D.I : h->D.U;
   }
   R.ids[0] = u;
@@ -202,8 +209,19 @@ static int catch_tables(ncf_handle* h) {
   return 0;
 }
 
+// the last step's row Adam, when it is still pending (before anything reads the rows or the
+// sample buffers it points into are refilled)
+static int flush_pending(ncf_handle* h) {
+  if (!h->pend.n) return 0;
+  NcfProf ps(h, 2);
+  HIPCHK(adam_rows(row_sides(h, h->pend.u, h->pend.i), h->pend.n, h->t, h->pend.a, h->stream));
+  h->pend.n = 0;
+  return 0;
+}
+
 // every embedding row brought to the current step (before the tables are read or written whole)
 static int ncf_flush(ncf_handle* h) {
+  if (int r = flush_pending(h)) return r;
   if (h->flushed == h->t) return 0;
   {
     NcfProf ps(h, 3);
@@ -337,9 +355,11 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   const int32_t t = ++h->t;
   const RowSides R = row_sides(h, u, i);
-  {
+  {  // step t - 1's row Adam (pending) and this step's catch-up to t - 1
     NcfProf ps(h, 3);
-    HIPCHK(catch_up(R, n, catch_args(h, t - 1), h->stream));
+    HIPCHK(rows(row_sides(h, h->pend.u, h->pend.i), h->pend.n, h->pend.a, R, n, catch_args(h, t - 1),
+                h->stream));
+    h->pend.n = 0;
   }
   const double b1 = h->cfg.beta1, b2 = h->cfg.beta2;
   AdamArgs a;
@@ -351,26 +371,30 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   a.bc2_sqrt = (float)std::sqrt(1.0 - std::pow(b2, (double)t));
   {
     NcfProf ps(h, 1);
-    HIPCHK(fwdbwd(h->D, h->P, h->G, h->A, u, i, y, n, h->d_loss, h->d_err, h->stream));
+    HIPCHK(fwdbwd(h->D, h->P, h->G, h->A, u, i, y, n, t, h->d_loss, h->d_err, h->stream));
     HIPCHK(back(h->D, h->P, h->G, h->d_jobs, h->njobs, u, i, n, h->F, h->Fo, h->WTo, h->Fm, h->Fv, a,
                 h->stream));
   }
   std::swap(h->F, h->Fo);  // the updated tower / predict weights are the current copy
   std::swap(h->WT, h->WTo);
   point_params(h);
-  NcfProf ps(h, 2);
-  HIPCHK(adam_rows(R, n, t, a, h->stream));
+  h->pend.u = u;
+  h->pend.i = i;
+  h->pend.n = n;
+  h->pend.a = a;
   return 0;
 }
 
 static int ncf_begin(ncf_handle* h) {
   if (int r = ncf_dev(h)) return r;
+  if (int r = flush_pending(h)) return r;
   HIPCHK(hipMemsetAsync(h->d_loss, 0, sizeof(double) * kLossSlotsNcf, h->stream));
   HIPCHK(hipEventRecord(h->ev0, h->stream));
   return 0;
 }
 
 static int ncf_end(ncf_handle* h, bprmf_stats* st, int64_t samples, int64_t steps) {
+  if (int r = flush_pending(h)) return r;
   HIPCHK(hipEventRecord(h->ev1, h->stream));
   std::vector<double> slots(kLossSlotsNcf);
   HIPCHK(hipMemcpyAsync(slots.data(), h->d_loss, sizeof(double) * kLossSlotsNcf, hipMemcpyDeviceToHost,
@@ -498,6 +522,10 @@ int ncf_create(const ncf_config* cfg, ncf_handle** out) {
   TRY(dalloc(&h->cur_i, D.I));
   HIPCHK(hipMemsetAsync(h->cur_u, 0xFF, 4 * D.U, h->stream));  // -1: never touched
   HIPCHK(hipMemsetAsync(h->cur_i, 0xFF, 4 * D.I, h->stream));
+  TRY(dalloc(&h->G.touch_u, D.U));
+  TRY(dalloc(&h->G.touch_i, D.I));
+  HIPCHK(hipMemsetAsync(h->G.touch_u, 0xFF, 4 * D.U, h->stream));
+  HIPCHK(hipMemsetAsync(h->G.touch_i, 0xFF, 4 * D.I, h->stream));
   TRY(dalloc(&h->F, D.flat_n));
   TRY(dalloc(&h->Fo, D.flat_n));
   TRY(dalloc(&h->Fm, D.flat_n));
@@ -557,7 +585,7 @@ int ncf_destroy(ncf_handle* h) {
     for (void* x : p)
       if (x) (void)!hipFree(x);
   }
-  void* ptrs[] = {h->G.Pg, h->G.Qg, h->G.Pm, h->G.Qm, h->cur_u, h->cur_i, h->d_step, h->d_pw, h->F, h->Fm,
+  void* ptrs[] = {h->G.Pg, h->G.Qg, h->G.Pm, h->G.Qm, h->cur_u, h->cur_i, h->G.touch_u, h->G.touch_i, h->d_step, h->d_pw, h->F, h->Fm,
                   h->Fv, h->WT, h->Fo, h->WTo, h->acts, h->d_jobs, h->d_pos_u, h->d_pos_i, h->d_indices, h->d_indptr,
                   h->d_u, h->d_i, h->d_y, h->d_loss, h->d_err};
   for (void* x : ptrs)
@@ -672,6 +700,7 @@ int ncf_train_samples(ncf_handle* h, const int32_t* u, const int32_t* i, const f
   int64_t steps = 0;
   for (int64_t off = 0; off < n; off += chunk) {
     const int64_t m = std::min(chunk, n - off);
+    if (int r = flush_pending(h)) return r;  // it points into the buffers refilled here
     HIPCHK(hipMemcpyAsync(h->d_u, u + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_i, i + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_y, y + off, 4 * m, hipMemcpyHostToDevice, h->stream));
@@ -696,6 +725,7 @@ int ncf_train_steps(ncf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
   int64_t steps = 0;
   for (int64_t off = beg; off < end; off += chunk) {
     const int64_t m = std::min(chunk, end - off);
+    if (int r = flush_pending(h)) return r;  // it points into the buffers refilled here
     {
       NcfProf ps(h, 0);
       HIPCHK(ncf::sample(ncf_sampler(h), epoch, off, m, h->d_u, h->d_i, h->d_y, h->d_err, h->stream));
@@ -737,6 +767,7 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
   }
   if (n == 0) return 0;
   if (int r = ncf_dev(h)) return r;
+  if (int r = flush_pending(h)) return r;
   // the rows read are brought to the current step: the requested ones, or every row for a long request
   const bool whole = 2 * n >= h->D.U + h->D.I;
   if (whole)
@@ -769,6 +800,7 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
 int ncf_active_rows(ncf_handle* h, int64_t* users, int64_t* items) {
   if (!h || !users || !items) return fail(BPRMF_E_INVALID, "null argument");
   if (int r = ncf_dev(h)) return r;
+  if (int r = flush_pending(h)) return r;
   HIPCHK(hipStreamSynchronize(h->stream));
   std::vector<int32_t> tu(h->D.U), ti(h->D.I);
   HIPCHK(hipMemcpy(tu.data(), h->cur_u, 4 * h->D.U, hipMemcpyDeviceToHost));

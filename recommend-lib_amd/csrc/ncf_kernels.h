@@ -31,6 +31,7 @@ struct Params {
 
 struct Grads {  // dense gradient rows of the embedding tables (zeroed again by the row Adam)
   float *Pg, *Qg, *Pm, *Qm;
+  int32_t *touch_u, *touch_i;  // the last step that gathered each row (-1: none)
 };
 
 // The embedding rows of one side (users or items): its GMF and MLP tables (cols 0 for a table the
@@ -40,6 +41,7 @@ struct RowSide {
   float *W[2], *M[2], *V[2], *G[2];
   int cols[2];
   int32_t* cur;
+  const int32_t* touch;
   int64_t rows;
 };
 struct RowSides {
@@ -90,7 +92,8 @@ struct AdamArgs {
 size_t fwdbwd_lds_bytes(const Dims& D);
 // k_ncf_front + k_ncf_mid (training: activations and gradients into A, loss, embedding GMF grads)
 hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
-                  const int32_t* i, const float* y, int n, double* loss, int32_t* err, hipStream_t s);
+                  const int32_t* i, const float* y, int n, int32_t t, double* loss, int32_t* err,
+                  hipStream_t s);
 hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
                    int n, float* z, int32_t* err, hipStream_t s);
 // k_ncf_back: the step's jobs; the tower / predict weights from Fcur (and P) to Fnext / WTnext
@@ -101,6 +104,10 @@ hipError_t back(const Dims& D, const Params& P, const Grads& G, const NcfJob* jo
 hipError_t catch_up(const RowSides& R, int64_t n, const CatchArgs& c, hipStream_t s);
 // step t of Adam on the rows of the samples (g = the gradient row, then zeroed); cur = t
 hipError_t adam_rows(const RowSides& R, int64_t n, int32_t t, const AdamArgs& a, hipStream_t s);
+// adam_rows of the previous step (np samples of Rp, step c.target) + catch_up of this step's
+// nc samples of Rc to c.target, in one launch (rows touched at c.target are left to the Adam)
+hipError_t rows(const RowSides& Rp, int np, const AdamArgs& a, const RowSides& Rc, int nc,
+                const CatchArgs& c, hipStream_t s);
 hipError_t transpose(const Dims& D, const Params& P, hipStream_t s);
 hipError_t sample(const SamplerArgs& a, uint32_t epoch, int64_t first, int64_t count, int32_t* u,
                   int32_t* i, float* y, int32_t* err, hipStream_t s);

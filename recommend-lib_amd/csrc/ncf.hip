@@ -148,6 +148,8 @@ __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
       if (s0 + s < n) *reinterpret_cast<float4*>(A.X0 + (int64_t)(s0 + s) * K + c) = v;
     }
   }
+  const int nn = n0 + r;
+  const float bias = wave == 0 && nn < N ? P.b[0][nn] : 0.f;  // issued before the MFMAs
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (wave < ks) {
     int32_t u, i;
@@ -161,9 +163,7 @@ __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
   if (wave > 0) return;
 #pragma unroll
   for (int w = 0; w < 3; ++w) acc += s_acc[w][lane];
-  const int nn = n0 + r;
   if (nn >= N) return;
-  const float bias = P.b[0][nn];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int s = 4 * (lane >> 4) + q;

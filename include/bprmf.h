@@ -42,12 +42,13 @@ typedef enum {
  * of a row may overwrite each other), weight decay still once per row per step; staleness is
  * bounded by the launch's in-flight window.  Single-GPU handles only. */
 enum { BPRMF_SEM_EXACT = 0, BPRMF_SEM_HOGWILD = 1, BPRMF_SEM_LOCAL = 2, BPRMF_SEM_STALE1 = 3 };
-/* STALE1 (opt-in, the sharded runner only: bprmf_dist_train_*, transports rccl / loopback): the
- * exact sharded step with the item rows one step stale.  Step k's gradient exchange and the
- * owners' apply run on a second stream beside step k+1's compute, so the rows step t reads are
- * the table after step t-2 brought to step t-1 by weight decay alone (they miss step t-1's
- * gradients); users stay exact; the first step of every runner chunk reads the current table.
- * Spec: oracle/bpr_oracle.py sharded_stale1_serial. */
+/* STALE1 (opt-in, the sharded runner only: bprmf_dist_train_*): the exact sharded step with the
+ * item rows one step stale.  Step k's gradient exchange and the owners' apply run beside step
+ * k+1's compute (transports rccl / loopback: on a second stream; ipc, one rank per GPU or
+ * BPRMF_DIST_FUSE=1: inside the next step's launch, ordered by device flags), so the rows step t
+ * reads are the table after step t-2 brought to step t-1 by weight decay alone (they miss step
+ * t-1's gradients); users stay exact; the first step of every runner chunk reads the current
+ * table.  Spec: oracle/bpr_oracle.py sharded_stale1_serial. */
 /* LOCAL (bounded staleness, opt-in): HOGWILD for users and for all but the most popular items;
  * the hot items (the top min(I, 4096) by positive count) are trained in one replica per XCD of the
  * GPU (each XCD's waves see their own XCD's updates at once, the other XCDs' only at the next

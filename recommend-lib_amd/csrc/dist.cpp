@@ -564,10 +564,14 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   d->nmax = rg.nmax;
   const int64_t rows = rg.row_elems;
   const int64_t ids = rg.id_elems;
+  auto* ipc = dynamic_cast<IpcTransport*>(tr);
+  const bool stale1 = h->semantics == BPRMF_SEM_STALE1;
+  // stale-1 over IPC (enqueue_stale1_ipc): the row and gradient landing buffers in two parities
+  const int64_t land = stale1 && ipc ? 2 * rows : rows;
   void* p = nullptr;
-  if (int r = tr->alloc_shared(h, X_ROWS, sizeof(float) * rows, &p)) return r;
+  if (int r = tr->alloc_shared(h, X_ROWS, sizeof(float) * land, &p)) return r;
   d->rows_recv = static_cast<float*>(p);
-  if (int r = tr->alloc_shared(h, X_GRADS, sizeof(float) * rows, &p)) return r;
+  if (int r = tr->alloc_shared(h, X_GRADS, sizeof(float) * land, &p)) return r;
   d->grads_recv = static_cast<float*>(p);
   if (int r = tr->alloc_shared(h, X_IDS, sizeof(int32_t) * 2 * ids, &p)) return r;
   d->ids_recv = static_cast<int32_t*>(p);
@@ -582,14 +586,13 @@ static int dist_attach(bprmf_handle* h, Transport* tr) {
   // chunk ever reallocates one inside a call (a free synchronises the device)
   for (int par = 0; par < 2; ++par)
     if (int r = ensure_aplan(h, par, d->nmax, d->S)) return r;
-  if (h->semantics == BPRMF_SEM_STALE1) {  // enqueue_stale1's second parities, stream, events
-    if (dynamic_cast<IpcTransport*>(tr))
-      return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics: attach the rccl or loopback transport "
-                                       "(the IPC transport's step kernels wait on their own flags)");
-    if (int r = dalloc(&d->rows_recv1, rows)) return r;
+  if (stale1) {  // the second parities; enqueue_stale1's stream and events
     if (int r = dalloc(&d->grads_send1, rows)) return r;
-    HIPCHK(hipMemsetAsync(d->rows_recv1, 0, sizeof(float) * rows, h->stream));
     HIPCHK(hipMemsetAsync(d->grads_send1, 0, sizeof(float) * rows, h->stream));
+  }
+  if (stale1 && !ipc) {
+    if (int r = dalloc(&d->rows_recv1, rows)) return r;
+    HIPCHK(hipMemsetAsync(d->rows_recv1, 0, sizeof(float) * rows, h->stream));
     HIPCHK(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
     for (hipEvent_t* e : {&d->ev_rows[0], &d->ev_rows[1], &d->ev_rows[2], &d->ev_rows[3], &d->ev_k2[0],
                           &d->ev_k2[1], &d->ev_k2[2], &d->ev_k2[3], &d->ev_fork, &d->ev_join})
@@ -700,11 +703,115 @@ static int enqueue_stale1(bprmf_handle* h, int64_t n, int cap, const int32_t* id
   return 0;
 }
 
+// Stale-1 over the IPC transport (the device-flag form): two launches per step on
+// one stream, no cross-stream events.
+//   front(k): owner phase [k = 0: gather steps 0 and 1 from the current table; k > 0: wait for
+//             the gradients of step k-1, apply them, gather step k+1 (rows of the table after step
+//             k-1, decayed to step k+1's t-1; none past the chunk)] beside K1(k), which waits for
+//             the row flags of step k (pushed by front(k-1), so it never waits on its own launch's
+//             owner workgroups except at k = 0);
+//   back(k):  K2(k), its gradients straight into the owners' landing buffers;
+//   after the chunk: the apply of step n-1.
+// Rows and gradients land in two parities (step k: parity k & 1).  Hazards: rows(k+2) can land
+// in parity k & 1 only after its owner applied step k, which needs this rank's gradients of step
+// k, pushed by back(k) after K1(k) read parity k & 1; gradients(k+2) can land in parity k & 1
+// only after their sender's K1(k+2) saw the row flags of step k+2, which every owner raises after
+// applying step k (the gradients in parity k & 1).  Flags and boards carry step numbers, so the
+// single flag word per peer serves both parities.
+static int enqueue_stale1_ipc(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
+                              const int32_t* aplan, bool prof_kernels) {
+  DistState* d = h->dist;
+  auto* ipc = dynamic_cast<IpcTransport*>(d->tr);
+  const int B = h->cfg.batch_size, W = h->cfg.world;
+  const int ld = h->geom.ld;
+  const BatchBuf bb{h->d_batch, B};
+  const int64_t R = h->cfg.rank;
+  const int64_t par_rows = (int64_t)W * d->S * ld;  // floats of one landing parity
+  float* rows_land[2] = {ipc->landing(X_ROWS), ipc->landing(X_ROWS) + par_rows};
+  float* grads_land[2] = {d->grads_recv, d->grads_recv + par_rows};
+  float* grads_own[2] = {d->grads_send, d->grads_send1};
+  auto row_dst = [&](int par) {  // where the owners' gather puts the rows of a step of parity par
+    PushArgs gd{};
+    for (int p = 0; p < W; ++p) {
+      if (p == R) {
+        gd.dst[p] = rows_land[par] + R * d->S * ld;
+        gd.flag[p] = const_cast<int32_t*>(ipc->my_flags(X_ROWS)) + R;  // K1 waits on its own too
+      } else {
+        gd.dst[p] = static_cast<float*>(ipc->peer_landing(X_ROWS, p)) + par * par_rows + R * d->S * ld;
+        gd.flag[p] = ipc->peer_flag(X_ROWS, p);
+      }
+    }
+    return gd;
+  };
+  const PeerWait pw{ipc->my_flags(X_ROWS), W, (int)R, h->d_err};
+  const int64_t WC0 = (int64_t)W * cap;
+  OwnerArgs oa;
+  oa.ids_recv = ids_recv;
+  oa.aplan = aplan;
+  oa.gdep = aplan + n * WC0 * W;
+  oa.gfree = oa.gdep + n * WC0 * W;
+  oa.n = n;
+  oa.world = W;
+  oa.cap = cap;
+  oa.self = (int)R;
+  oa.wait_flags = ipc->my_flags(X_GRADS);
+  oa.mark = ipc->board(IpcTransport::kBoardOwner);
+  oa.max_blocks = ipc->owner_blocks();
+  oa.lag = 2;
+  GradRoute gr[2];
+  for (int par = 0; par < 2; ++par) {
+    for (int p = 0; p < W; ++p) {
+      gr[par].dst[p] = p == R ? grads_own[par] + R * d->S * ld
+                              : static_cast<float*>(ipc->peer_landing(X_GRADS, p)) + par * par_rows +
+                                    R * (int64_t)cap * ld;
+      gr[par].flag[p] = p == R ? nullptr : ipc->peer_flag(X_GRADS, p);
+    }
+    gr[par].S = d->S;
+    gr[par].world = W;
+    gr[par].mark = ipc->board(IpcTransport::kBoardK2);
+    gr[par].err = h->d_err;
+  }
+  for (int64_t k = 0; k < n; ++k) {
+    const BatchView v = bb.view(k);
+    const bool sampled = prof_kernels && ((h->t + k) % kProfStride) == 0;
+    const int pk = (int)(k & 1), pa = (int)((k + 1) & 1);  // this step's parity, the other one
+    oa.dst = row_dst(k == 0 ? 0 : pa);
+    oa.dst1 = row_dst(1);
+    oa.grads_recv = grads_land[pa];  // step k-1's gradients (k > 0)
+    oa.self_grads = grads_own[pa] + R * d->S * ld;
+    {
+      ProfScope ps(h, BPRMF_KPROF_FWD_SCATTER, sampled);
+      HIPCHK(dist_front(h->geom, oa, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                        h->d_ugrad, h->d_xloss, rows_land[pk], pw, h->stream));
+    }
+    {
+      ProfScope ps(h, BPRMF_KPROF_APPLY, sampled);
+      HIPCHK(item_step_push(h->geom, v, B, h->P, h->Q, h->hp, h->d_tbase, (int)k, h->d_contrib,
+                            h->d_ugrad, h->d_xloss, h->d_loss, gr[pk], h->stream));
+    }
+  }
+  const int pl = (int)((n - 1) & 1);
+  ProfScope ps(h, BPRMF_KPROF_OWNER, prof_kernels && ((h->t + n - 1) % kProfStride) == 0);
+  HIPCHK(dist_owner_apply(h->geom, h->Q, ids_recv, aplan, n, W, cap, (int)(n - 1), h->hp, h->d_tbase,
+                          grads_land[pl], (int)R, grads_own[pl] + R * d->S * ld, ipc->my_flags(X_GRADS),
+                          h->d_err, h->stream));
+  return 0;
+}
+
 // The per-step launches and exchanges of a chunk of n steps (plan of `cap` rows per peer):
 // enqueued eagerly or captured into a hipGraph by dist_chunk.
 static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids_recv,
                          const int32_t* aplan, bool prof_kernels) {
-  if (h->semantics == BPRMF_SEM_STALE1) return enqueue_stale1(h, n, cap, ids_recv, aplan);
+  if (h->semantics == BPRMF_SEM_STALE1) {
+    auto* ipc = dynamic_cast<IpcTransport*>(h->dist->tr);
+    if (!ipc) return enqueue_stale1(h, n, cap, ids_recv, aplan);
+    if (!ipc->fused())
+      return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics over the IPC transport run the device-flag form, "
+                                       "which needs one rank per GPU (or BPRMF_DIST_FUSE=1); attach the "
+                                       "rccl or loopback transport");
+    // (a chunk with nothing to exchange reads no item row: the exact launch sequence below is it)
+    if (cap > 0) return enqueue_stale1_ipc(h, n, cap, ids_recv, aplan, prof_kernels);
+  }
   DistState* d = h->dist;
   const int B = h->cfg.batch_size, W = h->cfg.world;
   const int ld = h->geom.ld;
@@ -979,7 +1086,8 @@ static int dist_chunk(bprmf_handle* h, uint32_t epoch, int64_t first_step, int64
                                           nullptr, 0, seq});
     d->tr->self_exchange = se;
     if (r) return r;
-    HIPCHK(dist_owner_plan(ids_recv, n, W, cap, aplan, aplan + n * W * (int64_t)cap * W,
+    HIPCHK(dist_owner_plan(ids_recv, n, W, cap, h->semantics == BPRMF_SEM_STALE1 ? 2 : 1, aplan,
+                           aplan + n * W * (int64_t)cap * W,
                            aplan + 2 * n * W * (int64_t)cap * W, h->stream));
   }
   hipEvent_t ea = h->prof_on ? prof_event(h) : nullptr;

@@ -69,18 +69,19 @@ static __device__ __forceinline__ int find_row(const int32_t* __restrict__ list,
 // apply plan: aplan[k][p][idx][q] = q*cap + (position of row in peer q's list of step k), -1 if q
 // does not request it; a position whose row an earlier peer also requests (or a pad) gets
 // aplan[..][0] = -2 (not a leader: skipped by k_owner_apply).
-// Gather plan of the fused owner step (k_owner_step: apply step k, then gather step k+1):
-// gdep[k][p][idx][q] = position of the leader's row in peer q's list of step k+1, -1 if q does not
-// request it then (the leader serves those positions from the row it just wrote); gfree[k][p][idx]
-// = 1 when position (p, idx) of step k holds a row that step k-1 did not apply (k = 0: every row),
-// gathered on its own.
+// Gather plan of the fused owner step (k_owner_step: apply step k, then gather step k+lag; lag 1
+// for the exact step, 2 for the stale-1 step, whose rows of step k+2 are read after step k's
+// apply): gdep[k][p][idx][q] = position of the leader's row in peer q's list of step k+lag, -1 if
+// q does not request it then (the leader serves those positions from the row it just wrote);
+// gfree[k][p][idx] = 1 when position (p, idx) of step k holds a row that step k-lag did not apply
+// (k < lag: every row), gathered on its own.
 // One lane per (position, peer q): a group of G = next_pow2(world) lanes per position does its W
-// searches side by side (three binary searches a lane: step k-1, k and k+1 of peer q's list, one
-// dependent chain each) instead of one thread walking ~3W searches in sequence; the group's "any
+// searches side by side (three binary searches a lane: step k-lag, k and k+lag of peer q's list,
+// one dependent chain each) instead of one thread walking ~3W searches in sequence; the group's "any
 // peer" answers (the row was applied last step; a lower peer requests it too) are ballots.
 __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, int world, int cap,
-                             int gshift, int32_t* __restrict__ aplan, int32_t* __restrict__ gdep,
-                             int32_t* __restrict__ gfree) {
+                             int gshift, int lag, int32_t* __restrict__ aplan,
+                             int32_t* __restrict__ gdep, int32_t* __restrict__ gfree) {
   const int G = 1 << gshift;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t x = t >> gshift;
@@ -96,9 +97,9 @@ __global__ void k_owner_plan(const int32_t* __restrict__ ids_recv, int64_t n, in
     row = ids_recv[((int64_t)p * n + k) * cap + idx];
   }
   const bool qv = live && q < world && row >= 0;
-  const bool prev = qv && k > 0 && find_row(ids_recv + ((int64_t)q * n + k - 1) * cap, cap, (uint32_t)row) >= 0;
+  const bool prev = qv && k >= lag && find_row(ids_recv + ((int64_t)q * n + k - lag) * cap, cap, (uint32_t)row) >= 0;
   const int cur = !qv ? -1 : q == p ? idx : find_row(ids_recv + ((int64_t)q * n + k) * cap, cap, (uint32_t)row);
-  const int nxt = qv && k + 1 < n ? find_row(ids_recv + ((int64_t)q * n + k + 1) * cap, cap, (uint32_t)row) : -1;
+  const int nxt = qv && k + lag < n ? find_row(ids_recv + ((int64_t)q * n + k + lag) * cap, cap, (uint32_t)row) : -1;
   // every lane of the wave takes part in the ballots (groups never straddle a wave: G <= 16)
   const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
   const uint64_t gmask = (G >= 64 ? ~0ull : ((1ull << G) - 1)) << gbase;
@@ -365,13 +366,13 @@ hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* id
   return hipGetLastError();
 }
 
-hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
-                           int32_t* gdep, int32_t* gfree, hipStream_t s) {
+hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int lag,
+                           int32_t* aplan, int32_t* gdep, int32_t* gfree, hipStream_t s) {
   if (n <= 0 || cap <= 0) return hipSuccess;
   int gshift = 0;
   while ((1 << gshift) < world) ++gshift;  // world <= kMaxWorld = 16
   k_owner_plan<<<blocks_for((n * world * (int64_t)cap) << gshift), kBlock, 0, s>>>(
-      ids_recv, n, world, cap, gshift, aplan, gdep, gfree);
+      ids_recv, n, world, cap, gshift, lag, aplan, gdep, gfree);
   return hipGetLastError();
 }
 

@@ -45,12 +45,14 @@ static __device__ __forceinline__ void owner_gather_body(int blk, int nblk, cons
   if (mark) board_mark(mark, blk, t);
 }
 
-// Fused owner step: apply step k (as k_owner_apply) and gather step k+1 (as k_owner_gather) in one
-// launch.  A row step k applies is served to step k+1's requesters by its leader, from the value
-// it just stored (gdep); rows step k does not apply are gathered by their own groups (gfree).  No
-// row is both read by a free gather and written by an apply, so the groups are independent.
-// With mark set (IPC), each workgroup marks its completion board entry (step k+1) once its stores
-// are acknowledged; a finisher workgroup raises the peers' row flags.
+// Fused owner step: apply step k (as k_owner_apply) and gather step k+lag (as k_owner_gather) in
+// one launch (lag 1: the exact step; 2: the stale-1 step, whose rows of step k+2 are the table
+// after step k brought to step t+1 by decay).  A row step k applies is served to step k+lag's
+// requesters by its leader, from the value it just stored (gdep); rows step k does not apply are
+// gathered by their own groups (gfree).  No row is both read by a free gather and written by an
+// apply, so the groups are independent.  Past the chunk's last step there is nothing to gather.
+// With mark set (IPC), each workgroup marks its completion board entry (step k+lag) once its
+// stores are acknowledged; a finisher workgroup raises the peers' row flags.
 template <int G4, int S>
 static __device__ __forceinline__ void owner_step_body(
     int blk, int nblk, const Table& Q, const int32_t* __restrict__ ids_recv,
@@ -58,14 +60,16 @@ static __device__ __forceinline__ void owner_step_body(
     const int32_t* __restrict__ gfree, int64_t n, int world, int cap, int k, const Hyper& hp, int ld,
     const int32_t* __restrict__ tbase, const float* __restrict__ grads_recv, int self,
     const float* __restrict__ self_grads, const int32_t* __restrict__ wait_flags,
-    int32_t* __restrict__ err, const PushArgs& dst, int32_t* __restrict__ mark) {
+    int32_t* __restrict__ err, const PushArgs& dst, int32_t* __restrict__ mark, int lag = 1) {
   constexpr int NG = kBlock / G4;
   const int sub = threadIdx.x & (G4 - 1);
   const int32_t t = *tbase + k + 1;
   wait_peer_flags(wait_flags, world, self, t, err);  // IPC: the peers' gradients of step k
   const int64_t WC = (int64_t)world * cap;
   const float lr = hp.lr, wd = hp.wd;
-  for (int64_t x = blk * (int64_t)NG + threadIdx.x / G4; x < 2 * WC; x += (int64_t)nblk * NG) {
+  const int64_t nx = k + lag < n ? 2 * WC : WC;  // applies, then the gathers of step k+lag
+  const float f_dep = lag > 1 ? decay_pow(hp.log2a, lag - 1) : 1.f;  // served rows to step t+lag-1
+  for (int64_t x = blk * (int64_t)NG + threadIdx.x / G4; x < nx; x += (int64_t)nblk * NG) {
     if (x < WC) {  // apply: the leader position of a row of step k
       const int32_t* rec = aplan + ((int64_t)k * WC + x) * world;
       const int32_t r0 = rec[0];
@@ -113,30 +117,33 @@ static __device__ __forceinline__ void owner_step_body(
       }
       if (sub == 0) Q.stamp[row] = t;
       const int32_t* dep = gdep + ((int64_t)k * WC + x) * world;
-      for (int q = 0; q < world; ++q) {  // step k+1's requests of this row: the new value
+      for (int q = 0; q < world; ++q) {  // step k+lag's requests of this row: the new value
         const int32_t i2 = dep[q];
         if (i2 < 0) continue;
         float* o = static_cast<float*>(dst.dst[q]) + (int64_t)i2 * ld + 4 * sub;
 #pragma unroll
-        for (int s = 0; s < S; ++s) dist_st4(o + 4 * G4 * s, nv[s]);
+        for (int s = 0; s < S; ++s)
+          dist_st4(o + 4 * G4 * s, lag > 1 ? make_float4(nv[s].x * f_dep, nv[s].y * f_dep, nv[s].z * f_dep,
+                                                         nv[s].w * f_dep)
+                                           : nv[s]);
       }
-    } else {  // gather: a position of step k+1 whose row step k does not apply
+    } else {  // gather: a position of step k+lag whose row step k does not apply
       const int64_t y = x - WC;
-      if (!gfree[(int64_t)(k + 1) * WC + y]) continue;
+      if (!gfree[(int64_t)(k + lag) * WC + y]) continue;
       const int q = (int)(y / cap), idx = (int)(y % cap);
-      const int32_t row = ids_recv[((int64_t)q * n + k + 1) * cap + idx];
+      const int32_t row = ids_recv[((int64_t)q * n + k + lag) * cap + idx];
       const float* w = Q.W + (int64_t)row * ld + 4 * sub;
       float4 v[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) v[s] = dist_ld4(w + 4 * G4 * s);
-      const float f = decay_pow(hp.log2a, t - Q.stamp[row]);  // brought to step (t + 1) - 1
+      const float f = decay_pow(hp.log2a, t + lag - 1 - Q.stamp[row]);  // brought to step (t + lag) - 1
       float* o = static_cast<float*>(dst.dst[q]) + (int64_t)idx * ld + 4 * sub;
 #pragma unroll
       for (int s = 0; s < S; ++s)
         dist_st4(o + 4 * G4 * s, make_float4(v[s].x * f, v[s].y * f, v[s].z * f, v[s].w * f));
     }
   }
-  if (mark) board_mark(mark, blk, t + 1);
+  if (mark && k + lag < n) board_mark(mark, blk, t + lag);  // (nothing gathered: no mark)
 }
 
 }  // namespace bprmf

@@ -334,7 +334,7 @@ hipError_t max_vals(const int32_t* vals, int world, int32_t* out, hipStream_t s)
 hipError_t dist_own_max(BatchBuf bb, int64_t n, int world, int32_t* cap, hipStream_t s);
 hipError_t dist_pack_ids(BatchBuf bb, int64_t n, int world, int cap, int32_t* ids_send,
                          hipStream_t s);
-hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int32_t* aplan,
+hipError_t dist_owner_plan(const int32_t* ids_recv, int64_t n, int world, int cap, int lag, int32_t* aplan,
                            int32_t* gdep, int32_t* gfree, hipStream_t s);
 // ---- the fused sharded step over the IPC transport (step.hip; two launches per step) ----
 // K2 whose per-slot gradients go straight to the owners: slot s of owner p = s / S lands at
@@ -365,9 +365,14 @@ struct OwnerArgs {
   const int32_t* wait_flags = nullptr;
   PushArgs dst;
   int32_t* mark = nullptr;  // completion board of the owner workgroups, >= kBoardMax words
+  // stale-1 (lag 2): front k applies step k-1 and gathers step k+1 (rows of the table after step
+  // k-1); the chunk's first front gathers steps 0 (dst) and 1 (dst1, the other parity)
+  int lag = 1;
+  PushArgs dst1;
 };
-// owner phase of step `step` of the chunk (0: gather step 0; else apply step-1 and gather step)
-// in the first workgroups, K1 of `step` (sharded, waiting for every rank's row flags) in the rest
+// owner phase of step `step` of the chunk (0: gather step 0; else apply step-1 and gather step,
+// or step+1 for lag 2) in the first workgroups, K1 of `step` (sharded, waiting for every rank's
+// row flags) in the rest
 hipError_t dist_front(const Geom& g, const OwnerArgs& o, BatchView bv, int B, Table P, Table Q,
                       const Hyper& hp, const int32_t* tbase, int step, float* contrib, float* ugrad,
                       float* xloss, const float* item_rows, const PeerWait& pw, hipStream_t s);

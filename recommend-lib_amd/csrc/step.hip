@@ -747,17 +747,23 @@ __global__ __launch_bounds__(kBlock) void k_dist_front(OwnerArgs o, BatchView bv
                                                        const float* __restrict__ item_rows,
                                                        PeerWait pw, int ob, int B) {
   if ((int)blockIdx.x < ob) {
-    if (step == 0)
+    if (step == 0) {
       owner_gather_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.n, o.world, o.cap, 0, hp, ld, tbase,
                                o.dst, o.mark);
-    else
+      if (o.lag > 1 && o.n > 1)  // stale-1: step 1's rows from the same table, other parity
+        owner_gather_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.n, o.world, o.cap, 1, hp, ld, tbase,
+                                 o.dst1, o.mark);
+    } else {
       owner_step_body<G4, S>(blockIdx.x, ob, Q, o.ids_recv, o.aplan, o.gdep, o.gfree, o.n, o.world,
                              o.cap, step - 1, hp, ld, tbase, o.grads_recv, o.self, o.self_grads,
-                             o.wait_flags, pw.err, o.dst, o.mark);
+                             o.wait_flags, pw.err, o.dst, o.mark, o.lag);
+    }
     return;
   }
   if ((int)blockIdx.x == ob) {  // the owner workgroups' finisher: every rank's row flag for us
-    board_finish(o.mark, ob, *tbase + step + 1, o.dst.flag, o.world, pw.err);
+    // the last step whose rows this launch gathered (stale-1: one ahead; none at the chunk's end)
+    const int rs = o.lag == 1 ? step : step == 0 ? (o.n > 1 ? 1 : 0) : step + 1;
+    if (rs < o.n) board_finish(o.mark, ob, *tbase + rs + 1, o.dst.flag, o.world, pw.err);
     return;
   }
   const PeerWait all{pw.flags, pw.world, -1, pw.err};  // every rank's rows, this one's included

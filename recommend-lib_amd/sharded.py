@@ -280,8 +280,9 @@ class ShardedBPRMF:
 
     semantics="stale1" (opt-in, not the reference step): the exact sharded step with
     the item rows one step stale (oracle/bpr_oracle.py sharded_stale1_serial): each step's
-    gradient exchange and the owners' apply run beside the next step's compute.  Runner only
-    (attach_runner "rccl" or "loopback")."""
+    gradient exchange and the owners' apply run beside the next step's compute.  Runner only:
+    attach_runner "rccl" or "loopback" (a second stream), or "ipc" with one rank per GPU (the
+    device-flag form, inside the next step's launch)."""
 
     def __init__(self, user_num, item_num, factor_num=32, lr=0.01, wd=0.001, batch_size=4096,
                  num_ng=4, init_std=0.01, seed=0, device=0, group=None, comm=None, backend=None,

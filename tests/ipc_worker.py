@@ -24,6 +24,8 @@ def main():
     local = mode == "local"  # semantics "local": the item table replicated, merged by all-reduce
     kw = dict(semantics="local", local_steps=int(spec["period"]), dp_steps=int(spec["dp"]),
               dp_overlap=bool(spec["overlap"])) if local else {}
+    if mode == "stale1":  # the stale-1 step's device-flag form (IPC transport)
+        kw = dict(semantics="stale1")
     m = sh.ShardedBPRMF(U, I, D, lr=float(spec["lr"]), wd=float(spec["wd"]), batch_size=B,
                         seed=int(spec["seed"]), device=0, **kw)
     if local:
@@ -33,7 +35,7 @@ def main():
         batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]
         st = m.train_replay(batches)
         st2 = m.train_replay(batches)
-    elif mode == "replay":
+    elif mode in ("replay", "stale1"):
         m.set_weights(sh.shard_rows(spec["P0"], rank, world), sh.shard_rows(spec["Q0"], rank, world))
         m.attach_runner("ipc")
         batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]

@@ -143,6 +143,62 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse):
         assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_ipc_stale1_device_flags_match_oracle_and_two_stream_form(rl, tmp_path, world):
+    """semantics "stale1" over the IPC transport: the device-flag form (dist.cpp
+    enqueue_stale1_ipc: front k = the owners' apply of step k-1 and gather of step k+1 beside
+    K1(k), back k = K2(k) pushing its gradients; two landing parities, no cross-stream events),
+    forced on the shared GPU (BPRMF_DIST_FUSE=1).  Against the spec
+    (oracle/bpr_oracle.py:sharded_stale1_serial; each call is one runner chunk) at the stale1
+    tolerance, and bit for bit against the two-stream form over the in-process loopback
+    transport."""
+    U, I, D, GB, steps = 301, 157, 64, 512, 6
+    g = np.random.default_rng(41 + world)
+    u = g.integers(0, U, (steps, GB)).astype(np.int32)
+    i = g.integers(0, I, (steps, GB)).astype(np.int32)
+    j = g.integers(0, I, (steps, GB)).astype(np.int32)
+    i[:, :40] = 7  # a hot item, touched by every step
+    j[:, 40:45] = i[:, 40:45]  # i == j
+    spec = dict(U=U, I=I, D=D, B=GB, lr=0.05, wd=0.01, seed=3, u=u, i=i, j=j,
+                P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
+                Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
+    res = _run_workers(tmp_path, spec, "stale1", world, extra_env={"BPRMF_DIST_FUSE": "1"})
+    sh = rl.sharded
+    P = sh.unshard_rows([r["P"] for r in res], U)
+    Q = sh.unshard_rows([r["Q"] for r in res], I)
+    batches = [(u[k], i[k], j[k]) for k in range(steps)]
+    Pr, Qr = spec["P0"].copy(), spec["Q0"].copy()
+    losses = np.concatenate([O.sharded_stale1_serial(Pr, Qr, batches, 0.05, 0.01, steps)
+                             for _ in range(2)])
+    np.testing.assert_allclose(P, Pr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Q, Qr, rtol=1e-5, atol=1e-6)
+    assert sum(float(r["loss"]) for r in res) == pytest.approx(losses.sum(), rel=1e-5)
+    # the two-stream form (rccl / loopback transports) computes the same rows in the same order
+    grp = sh.ThreadGroup(world)
+    out, errs = [None] * world, []
+
+    def run(r):
+        try:
+            m = sh.ShardedBPRMF(U, I, D, lr=0.05, wd=0.01, batch_size=GB, seed=3, device=0,
+                                comm=sh.ThreadComm(grp, r), semantics="stale1")
+            m.set_weights(sh.shard_rows(spec["P0"], r, world), sh.shard_rows(spec["Q0"], r, world))
+            m.attach_runner("loopback", key=8900 + world)
+            m.train_replay(batches)
+            m.train_replay(batches)
+            out[r] = m.get_weights()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            grp.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    if errs:
+        raise errs[0]
+    for r in range(world):
+        assert np.array_equal(res[r]["P"], out[r][0]) and np.array_equal(res[r]["Q"], out[r][1])
+
+
 def test_ipc_sampler_training_equals_loopback(rl, golden, tmp_path):
     f = golden("bpr_ml100k_replay.npz")
     pos = f["positives"].astype(np.int64)

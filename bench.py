@@ -365,10 +365,11 @@ def main():
                 step_us, what = us["step_graph"], ("k_hogwild<LOCAL> (in-kernel sampling + gather + dots "
                                                    "+ sigmoid + SGD scatter, hot items in per-XCD replicas) "
                                                    "+ k_local_merge every period")
-            elif "step_graph" in us and a.semantics == "stale1":  # two streams per rank
-                step_us, what = us["step_graph"], ("stale1 sharded step, per rank: K1 + K2 on the compute "
-                                                   "stream beside the owner stream's gradient exchange, "
-                                                   "apply, gather and row exchange of the step before")
+            elif "step_graph" in us and a.semantics == "stale1":
+                step_us, what = us["step_graph"], ("stale1 sharded step, per rank: K1 beside the owners' "
+                                                   "apply of the step before and gather of the step after "
+                                                   "(ipc: one launch, device flags) or beside the owner "
+                                                   "stream's exchanges (rccl: two streams), then K2")
             elif "step_graph" in us and sharded:  # events around each chunk's steps (per rank)
                 step_us, what = us["step_graph"], ("sharded step, per rank: owner gather + row exchange + "
                                                    "user_step + item_step + grad exchange + owner apply")

@@ -245,6 +245,13 @@ struct IpcTransport final : Transport {
     if (e && *e) return e[0] != '0';
     return world > 1 && !shared_device;
   }
+  // stale-1's device-flag form: as fused(), at world 1 too (no single-GPU step to dispatch to)
+  bool device_flags() const {
+    if (!opened || self_exchange) return false;
+    const char* e = getenv("BPRMF_DIST_FUSE");
+    if (e && *e) return e[0] != '0';
+    return !shared_device;
+  }
   float* landing(int kind) const { return static_cast<float*>(local[kind]); }
   void* peer_landing(int kind, int p) const { return remote[kind][p]; }
   int32_t* peer_flag(int kind, int p) const {
@@ -805,7 +812,8 @@ static int enqueue_steps(bprmf_handle* h, int64_t n, int cap, const int32_t* ids
   if (h->semantics == BPRMF_SEM_STALE1) {
     auto* ipc = dynamic_cast<IpcTransport*>(h->dist->tr);
     if (!ipc) return enqueue_stale1(h, n, cap, ids_recv, aplan);
-    if (!ipc->fused())
+    // the device-flag form needs one rank per GPU: its kernels wait inside the launches
+    if (!ipc->device_flags())
       return fail(BPRMF_E_UNSUPPORTED, "stale1 semantics over the IPC transport run the device-flag form, "
                                        "which needs one rank per GPU (or BPRMF_DIST_FUSE=1); attach the "
                                        "rccl or loopback transport");

@@ -29,6 +29,9 @@ from . import _lib
 # ------------------------------------------------------------------------------------------------
 # communicators
 # ------------------------------------------------------------------------------------------------
+
+IPC_BUS_ID_OFF = 5 * 64  # csrc/dist.cpp: kIpcHandles hipIpcMemHandle_t (64 B), then the bus id
+
 class TorchComm:
     """torch.distributed (backend "nccl" = RCCL on ROCm, or "gloo" for CPU tests)."""
 
@@ -371,10 +374,8 @@ class ShardedBPRMF:
             self.b.runner_rccl(uid)
         elif transport == "ipc":
             self.b.runner_ipc(lambda blob: self.comm.all_gather_bytes(blob, self.device))
-        elif transport == "auto" and self.semantics in ("local", "stale1"):
-            # local: the item merge is an all-reduce; stale1: the owner stream's exchanges are
-            # host-ordered RCCL send/recv (the IPC transport's kernels wait on their own flags)
-            return self.attach_runner("rccl")
+        elif transport == "auto" and self.semantics == "local":
+            return self.attach_runner("rccl")  # the item merge is an all-reduce
         elif transport == "auto":  # ipc where every rank can map its peers, else rccl
             # Every rank joins every collective whatever failed locally: a status byte travels
             # with the handles, so a rank whose export failed cannot leave its peers waiting in
@@ -386,6 +387,12 @@ class ShardedBPRMF:
                 self.transport_error = str(e)
                 ok = 0
             got = self.comm.all_gather_bytes(bytes([ok]) + blob, self.device)
+            # stale1 over IPC is the device-flag form: one rank per GPU (every blob carries its
+            # device's PCI bus id after the five handles); ranks sharing a GPU take rccl
+            if self.semantics == "stale1" and all(g[0] == 1 for g in got):
+                bus = [bytes(g[1 + IPC_BUS_ID_OFF:1 + IPC_BUS_ID_OFF + 64]) for g in got]
+                if len(set(bus)) < len(bus):
+                    return self.attach_runner("rccl")
             if all(g[0] == 1 for g in got):
                 try:
                     self.b.ipc_init(b"".join(g[1:] for g in got))

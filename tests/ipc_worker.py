@@ -24,7 +24,7 @@ def main():
     local = mode == "local"  # semantics "local": the item table replicated, merged by all-reduce
     kw = dict(semantics="local", local_steps=int(spec["period"]), dp_steps=int(spec["dp"]),
               dp_overlap=bool(spec["overlap"])) if local else {}
-    if mode == "stale1":  # the stale-1 step's device-flag form (IPC transport)
+    if mode in ("stale1", "stale1_auto"):  # the stale-1 step's device-flag form (IPC transport)
         kw = dict(semantics="stale1")
     m = sh.ShardedBPRMF(U, I, D, lr=float(spec["lr"]), wd=float(spec["wd"]), batch_size=B,
                         seed=int(spec["seed"]), device=0, **kw)
@@ -35,9 +35,9 @@ def main():
         batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]
         st = m.train_replay(batches)
         st2 = m.train_replay(batches)
-    elif mode in ("replay", "stale1"):
+    elif mode in ("replay", "stale1", "stale1_auto"):
         m.set_weights(sh.shard_rows(spec["P0"], rank, world), sh.shard_rows(spec["Q0"], rank, world))
-        m.attach_runner("ipc")
+        m.attach_runner("auto" if mode == "stale1_auto" else "ipc")
         batches = [(spec["u"][k], spec["i"][k], spec["j"][k]) for k in range(spec["u"].shape[0])]
         st = m.train_replay(batches)
         st2 = m.train_replay(batches)  # replays the captured step graph
@@ -48,7 +48,8 @@ def main():
         st2 = m.train_steps(1, 0, 5)
     torch.cuda.synchronize()
     P, Q = m.get_weights()
-    np.savez(out, P=P, Q=Q, loss=st["loss"] + st2["loss"], triplets=st["triplets"] + st2["triplets"])
+    np.savez(out, P=P, Q=Q, loss=st["loss"] + st2["loss"], triplets=st["triplets"] + st2["triplets"],
+             runner=str(m.runner))
     dist.barrier()
     dist.destroy_process_group()
 

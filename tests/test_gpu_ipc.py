@@ -143,12 +143,13 @@ def test_ipc_replay_equals_dense_oracle_and_loopback(rl, tmp_path, world, fuse):
         assert np.array_equal(res[r]["P"], lb[r][0]) and np.array_equal(res[r]["Q"], lb[r][1])
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_ipc_stale1_device_flags_match_oracle_and_two_stream_form(rl, tmp_path, world):
+@pytest.mark.parametrize("world,fuse", [(1, "1"), (2, "1"), (3, "1"), (1, "auto")])
+def test_ipc_stale1_device_flags_match_oracle_and_two_stream_form(rl, tmp_path, world, fuse):
     """semantics "stale1" over the IPC transport: the device-flag form (dist.cpp
     enqueue_stale1_ipc: front k = the owners' apply of step k-1 and gather of step k+1 beside
     K1(k), back k = K2(k) pushing its gradients; two landing parities, no cross-stream events),
-    forced on the shared GPU (BPRMF_DIST_FUSE=1).  Against the spec
+    forced on the shared GPU (BPRMF_DIST_FUSE=1); "auto": attach_runner("auto") at one rank per
+    GPU picks it by itself.  Against the spec
     (oracle/bpr_oracle.py:sharded_stale1_serial; each call is one runner chunk) at the stale1
     tolerance, and bit for bit against the two-stream form over the in-process loopback
     transport."""
@@ -162,7 +163,11 @@ def test_ipc_stale1_device_flags_match_oracle_and_two_stream_form(rl, tmp_path, 
     spec = dict(U=U, I=I, D=D, B=GB, lr=0.05, wd=0.01, seed=3, u=u, i=i, j=j,
                 P0=(0.05 * g.standard_normal((U, D))).astype(np.float32),
                 Q0=(0.05 * g.standard_normal((I, D))).astype(np.float32))
-    res = _run_workers(tmp_path, spec, "stale1", world, extra_env={"BPRMF_DIST_FUSE": "1"})
+    if fuse == "auto":
+        res = _run_workers(tmp_path, spec, "stale1_auto", world)
+        assert all(str(r["runner"]) == "ipc" for r in res)
+    else:
+        res = _run_workers(tmp_path, spec, "stale1", world, extra_env={"BPRMF_DIST_FUSE": fuse})
     sh = rl.sharded
     P = sh.unshard_rows([r["P"] for r in res], U)
     Q = sh.unshard_rows([r["Q"] for r in res], I)

@@ -130,12 +130,20 @@ static __device__ __forceinline__ void sample_ids(const Dims& D, const int32_t* 
 // k in [w K/ks, (w+1) K/ks) straight from the embedding rows (the first half from Pm[u], the
 // second from Qm[i]), the parts summed in wave order through LDS.  The y = 0 workgroups also
 // store the tower input rows (X0) for the weight gradient.
-__global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
+__global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Grads G, Acts A,
                                                    const int32_t* __restrict__ us,
-                                                   const int32_t* __restrict__ is, int n) {
+                                                   const int32_t* __restrict__ is, int n, int32_t t) {
   __shared__ f32x4 s_acc[3][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15;
   const int s0 = blockIdx.x * kSamples, E = D.E, K = 2 * E, N = D.nout[0], n0 = 16 * blockIdx.y;
+  if (G.touch_u && blockIdx.y == 0 && tid < kSamples) {  // the rows this step's row Adam will move
+    int32_t u, i;
+    sample_ids(D, us, is, s0 + tid, n, u, i);
+    if (u >= 0) {
+      G.touch_u[u] = t;
+      G.touch_i[i] = t;
+    }
+  }
   const int ks = E % 8 == 0 ? 4 : 2, kq = K / ks;  // parts of K, each a multiple of 4 floats
   if (A.X0 && blockIdx.y == 0) {
     const int q = K / 4;
@@ -171,7 +179,15 @@ __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Acts A,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Acts A,
+static __device__ __forceinline__ void catch_row(const RowSides& R, int64_t x, int side, const CatchArgs& c,
+                                                 int32_t skip);
+
+// The workgroups past the batch's groups catch up the NEXT step's rows (rn samples of Rn) to this
+// step t: the zero-gradient step t of a row this step does not gather (touch != t) is due anyway,
+// and nothing reads such a row before the next step, so the next step's k_ncf_rows finds it
+// current.  They run on the CUs the 16-workgroup middle layers leave idle.
+__global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Acts A, RowSides Rn, int rn,
+                                                  CatchArgs cn,
                                                   const int32_t* __restrict__ us,
                                                   const int32_t* __restrict__ is,
                                                   const float* __restrict__ ys, int n, int32_t t,
@@ -179,6 +195,12 @@ __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Act
                                                   int32_t* __restrict__ err,
                                                   float* __restrict__ zout) {
   extern __shared__ float sm[];
+  const int groups = (n + kSamples - 1) / kSamples;
+  if ((int)blockIdx.x >= groups) {
+    const int x = (int)blockIdx.x - groups;
+    if (x < 2 * rn) catch_row(Rn, x >> 1, x & 1, cn, cn.target);
+    return;
+  }
   const Lds Lp = lds_plan(D);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = 16;
@@ -294,7 +316,7 @@ __global__ __launch_bounds__(1024) void k_ncf_mid(Dims D, Params P, Grads G, Act
       atomicAdd(G.Qg + (int64_t)i * d + k, gk * sm[Lp.eu + s * (d + 4) + k]);
     }
   }
-  if (tid < kSamples && su[tid] >= 0) {  // the rows this step's row Adam will move
+  if (!mlp && tid < kSamples && su[tid] >= 0) {  // (with a tower, k_ncf_front stamps them)
     G.touch_u[su[tid]] = t;
     G.touch_i[si[tid]] = t;
   }
@@ -605,26 +627,30 @@ static hipError_t allow_lds(K* kernel, size_t bytes) {
 
 static hipError_t front_mid(const Dims& D, const Params& P, const Grads& G, const Acts& A,
                             const int32_t* u, const int32_t* i, const float* y, int n, int32_t t, double* loss,
-                            int32_t* err, float* z, hipStream_t s) {
+                            int32_t* err, float* z, const RowSides* Rn, int rn, const CatchArgs* cn,
+                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned groups = (unsigned)((n + kSamples - 1) / kSamples);
   if (D.model != kGMF)
-    k_ncf_front<<<dim3(groups, (unsigned)((D.nout[0] + 15) / 16)), 256, 0, s>>>(D, P, A, u, i, n);
+    k_ncf_front<<<dim3(groups, (unsigned)((D.nout[0] + 15) / 16)), 256, 0, s>>>(D, P, G, A, u, i, n, t);
+  // the next step's catch-up beside the middle layers (needs the touch stamps k_ncf_front wrote)
+  if (!Rn || !cn || D.model == kGMF || cn->target <= 0) rn = 0;
   const size_t mb = sizeof(float) * (size_t)lds_plan(D).total;
   if (hipError_t e = allow_lds(k_ncf_mid, mb)) return e;
-  k_ncf_mid<<<groups, 1024, mb, s>>>(D, P, G, A, u, i, y, n, t, loss, err, z);
+  k_ncf_mid<<<groups + 2 * (unsigned)rn, 1024, mb, s>>>(D, P, G, A, rn ? *Rn : RowSides{}, rn,
+                                                          rn ? *cn : CatchArgs{}, u, i, y, n, t, loss, err, z);
   return hipGetLastError();
 }
 
 hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
                   const int32_t* i, const float* y, int n, int32_t t, double* loss, int32_t* err,
-                  hipStream_t s) {
-  return front_mid(D, P, G, A, u, i, y, n, t, loss, err, nullptr, s);
+                  const RowSides* next, int next_n, const CatchArgs* next_c, hipStream_t s) {
+  return front_mid(D, P, G, A, u, i, y, n, t, loss, err, nullptr, next, next_n, next_c, s);
 }
 
 hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
                    int n, float* z, int32_t* err, hipStream_t s) {
-  return front_mid(D, P, Grads{}, A, u, i, nullptr, n, 0, nullptr, err, z, s);
+  return front_mid(D, P, Grads{}, A, u, i, nullptr, n, 0, nullptr, err, z, nullptr, 0, nullptr, s);
 }
 
 hipError_t back(const Dims& D, const Params& P, const Grads& G, const NcfJob* jobs, int njobs,

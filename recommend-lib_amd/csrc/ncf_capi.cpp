@@ -350,8 +350,10 @@ static int ncf_check_err(ncf_handle* h) {
   return 0;
 }
 
-// one Adam step over device samples u/i/y[0..n)
-static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const float* y, int n) {
+// one Adam step over device samples u/i/y[0..n); nu/ni[0..nn): the next step's samples when they
+// are already in device memory (their rows are then caught up beside this step's middle layers)
+static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const float* y, int n,
+                    const int32_t* nu = nullptr, const int32_t* ni = nullptr, int nn = 0) {
   if (h->t == INT32_MAX) return fail(BPRMF_E_STATE, "step counter overflow");
   const int32_t t = ++h->t;
   const RowSides R = row_sides(h, u, i);
@@ -371,7 +373,10 @@ static int ncf_step(ncf_handle* h, const int32_t* u, const int32_t* i, const flo
   a.bc2_sqrt = (float)std::sqrt(1.0 - std::pow(b2, (double)t));
   {
     NcfProf ps(h, 1);
-    HIPCHK(fwdbwd(h->D, h->P, h->G, h->A, u, i, y, n, t, h->d_loss, h->d_err, h->stream));
+    const RowSides Rn = row_sides(h, nu, ni);
+    const CatchArgs cn = catch_args(h, t);
+    HIPCHK(fwdbwd(h->D, h->P, h->G, h->A, u, i, y, n, t, h->d_loss, h->d_err, nu ? &Rn : nullptr, nu ? nn : 0,
+                  &cn, h->stream));
     HIPCHK(back(h->D, h->P, h->G, h->d_jobs, h->njobs, u, i, n, h->F, h->Fo, h->WTo, h->Fm, h->Fv, a,
                 h->stream));
   }
@@ -704,8 +709,13 @@ int ncf_train_samples(ncf_handle* h, const int32_t* u, const int32_t* i, const f
     HIPCHK(hipMemcpyAsync(h->d_u, u + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_i, i + off, 4 * m, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d_y, y + off, 4 * m, hipMemcpyHostToDevice, h->stream));
-    for (int64_t s = 0; s < m; s += B, ++steps)
-      if (int r = ncf_step(h, h->d_u + s, h->d_i + s, h->d_y + s, (int)std::min(B, m - s))) return r;
+    for (int64_t s = 0; s < m; s += B, ++steps) {
+      const int64_t s2 = s + B;  // the next step's samples, when they are in this chunk
+      if (int r = ncf_step(h, h->d_u + s, h->d_i + s, h->d_y + s, (int)std::min(B, m - s),
+                           s2 < m ? h->d_u + s2 : nullptr, s2 < m ? h->d_i + s2 : nullptr,
+                           (int)std::min(B, std::max<int64_t>(0, m - s2))))
+        return r;
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
   }
   return ncf_end(h, st, n, steps);
@@ -730,8 +740,13 @@ int ncf_train_steps(ncf_handle* h, uint32_t epoch, int64_t first_step, int64_t n
       NcfProf ps(h, 0);
       HIPCHK(ncf::sample(ncf_sampler(h), epoch, off, m, h->d_u, h->d_i, h->d_y, h->d_err, h->stream));
     }
-    for (int64_t s = 0; s < m; s += B, ++steps)
-      if (int r = ncf_step(h, h->d_u + s, h->d_i + s, h->d_y + s, (int)std::min(B, m - s))) return r;
+    for (int64_t s = 0; s < m; s += B, ++steps) {
+      const int64_t s2 = s + B;  // the next step's samples, when they are in this chunk
+      if (int r = ncf_step(h, h->d_u + s, h->d_i + s, h->d_y + s, (int)std::min(B, m - s),
+                           s2 < m ? h->d_u + s2 : nullptr, s2 < m ? h->d_i + s2 : nullptr,
+                           (int)std::min(B, std::max<int64_t>(0, m - s2))))
+        return r;
+    }
   }
   return ncf_end(h, st, end - beg, steps);
 }

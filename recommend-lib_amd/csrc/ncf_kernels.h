@@ -91,9 +91,10 @@ struct AdamArgs {
 
 size_t fwdbwd_lds_bytes(const Dims& D);
 // k_ncf_front + k_ncf_mid (training: activations and gradients into A, loss, embedding GMF grads)
+// next (optional): the next step's samples, caught up to step t beside the middle layers
 hipError_t fwdbwd(const Dims& D, const Params& P, const Grads& G, const Acts& A, const int32_t* u,
                   const int32_t* i, const float* y, int n, int32_t t, double* loss, int32_t* err,
-                  hipStream_t s);
+                  const RowSides* next, int next_n, const CatchArgs* next_c, hipStream_t s);
 hipError_t forward(const Dims& D, const Params& P, const Acts& A, const int32_t* u, const int32_t* i,
                    int n, float* z, int32_t* err, hipStream_t s);
 // k_ncf_back: the step's jobs; the tower / predict weights from Fcur (and P) to Fnext / WTnext

@@ -70,7 +70,8 @@ int ncf_predict(ncf_handle* h, const int32_t* u, const int32_t* i, int64_t n, fl
 /* embedding rows Adam steps every step from now on: rows with a nonzero moment (ever touched).
  * (Their zero-gradient steps are applied lazily, in closed form, before anything reads them.) */
 int ncf_active_rows(ncf_handle* h, int64_t* users, int64_t* items);
-/* live timing: kinds 0 sample, 1 forward/backward, 2 Adam, 3 catch-up of the rows read (bprmf_kprof) */
+/* live timing (bprmf_kprof): kinds 0 sample, 1 forward/backward with the tower's Adam, 2 a call's
+ * last row Adam, 3 the row launch (the previous step's row Adam + this step's catch-up) */
 int ncf_profile(ncf_handle* h, int32_t enable);
 int ncf_profile_read(ncf_handle* h, bprmf_kprof* out);
 

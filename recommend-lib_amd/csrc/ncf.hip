@@ -74,8 +74,9 @@ size_t fwdbwd_lds_bytes(const Dims& D) { return sizeof(float) * (size_t)lds_plan
 // f32 MFMA, lane group g = l >> 4 takes k = 16t + 4g .. +3 (kc % 4 == 0); lane l supplies
 // row l & 15 of X from xr (0 where !xok).  The W rows come from L2/HBM: eight k-steps of loads
 // are issued before their 32 MFMAs, so one latency is paid per eight steps, not per step.
+// xs (optional): this lane's row of X is also stored there as it is loaded
 static __device__ __forceinline__ f32x4 tile_xwt(const float* xr, bool xok, const float* W, int ldw,
-                                                 int kc, int n0, int nmax, int lane) {
+                                                 int kc, int n0, int nmax, int lane, float* xs = nullptr) {
   constexpr int U = 8;
   const int r = lane & 15, g = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -92,6 +93,7 @@ static __device__ __forceinline__ f32x4 tile_xwt(const float* xr, bool xok, cons
     for (int q = 0; q < U; ++q) {
       const int k = 16 * (t0 + q) + 4 * g;
       a[q] = (xok && k < kc) ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (xs && k < kc) *reinterpret_cast<float4*>(xs + k) = a[q];
     }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
@@ -145,17 +147,6 @@ __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Grads G, Ac
     }
   }
   const int ks = E % 8 == 0 ? 4 : 2, kq = K / ks;  // parts of K, each a multiple of 4 floats
-  if (A.X0 && blockIdx.y == 0) {
-    const int q = K / 4;
-    for (int x = tid; x < kSamples * q; x += blockDim.x) {
-      const int s = x / q, c = 4 * (x % q);
-      int32_t u, i;
-      sample_ids(D, us, is, s0 + s, n, u, i);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (u >= 0) v = c < E ? ld4(P.Pm + (int64_t)u * E + c) : ld4(P.Qm + (int64_t)i * E + (c - E));
-      if (s0 + s < n) *reinterpret_cast<float4*>(A.X0 + (int64_t)(s0 + s) * K + c) = v;
-    }
-  }
   const int nn = n0 + r;
   const float bias = wave == 0 && nn < N ? P.b[0][nn] : 0.f;  // issued before the MFMAs
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -164,7 +155,9 @@ __global__ __launch_bounds__(256) void k_ncf_front(Dims D, Params P, Grads G, Ac
     sample_ids(D, us, is, s0 + r, n, u, i);
     const int kb = wave * kq;  // this part's first k; < E: the user's row
     const float* xr = kb < E ? P.Pm + (int64_t)max(u, 0) * E + kb : P.Qm + (int64_t)max(i, 0) * E + (kb - E);
-    acc = tile_xwt(xr, u >= 0, P.W[0] + kb, K, kq, n0, N, lane);
+    // the y = 0 workgroups store the rows they load as X0 (zero for a sample without ids)
+    float* xs = A.X0 && blockIdx.y == 0 ? A.X0 + (int64_t)(s0 + r) * K + kb : nullptr;
+    acc = tile_xwt(xr, u >= 0, P.W[0] + kb, K, kq, n0, N, lane, xs);
   }
   if (wave > 0) s_acc[wave - 1][lane] = acc;
   __syncthreads();
@@ -515,6 +508,19 @@ __global__ __launch_bounds__(256) void k_ncf_back(Dims D, Params P, Grads G, con
   const float* pa = J.A + J.m0 + r;
   const float* pb = vec ? J.B : J.B + J.k0 + r;
   const int ldb = vec ? 1 : J.ldb;
+  // this lane's output elements and their Adam operands, loaded ahead of the contraction
+  const int kk = J.k0 + r;
+  const bool out = vec ? r == 0 : kk < J.K;  // a vector job's 16 columns are equal: lane r = 0
+  int jj[4];
+  float p0[4], m0[4], v0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int mm = J.m0 + 4 * g + q;
+    jj[q] = out && mm < J.M ? (vec ? J.flat + mm : J.flat + mm * J.K + kk) : -1;
+    p0[q] = jj[q] >= 0 ? Fcur[jj[q]] : 0.f;
+    m0[q] = jj[q] >= 0 ? M[jj[q]] : 0.f;
+    v0[q] = jj[q] >= 0 ? V[jj[q]] : 0.f;
+  }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   constexpr int U = 32;  // samples 4U per round of loads
   for (int s4 = 0; s4 < n; s4 += 4 * U) {
@@ -528,20 +534,16 @@ __global__ __launch_bounds__(256) void k_ncf_back(Dims D, Params P, Grads G, con
 #pragma unroll
     for (int e = 0; e < U; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
   }
-  if (vec && r != 0) return;  // a vector job's 16 columns are equal
-  const int kk = J.k0 + r;
-  if (!vec && kk >= J.K) return;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int mm = J.m0 + 4 * g + q;
-    if (mm >= J.M) continue;
-    const int j = vec ? J.flat + mm : J.flat + mm * J.K + kk;
-    float p = Fcur[j], m = M[j], v = V[j];
+    const int j = jj[q];
+    if (j < 0) continue;
+    float p = p0[q], m = m0[q], v = v0[q];
     adam1(p, m, v, acc[q], a);
     Fnext[j] = p;
     M[j] = m;
     V[j] = v;
-    if (J.layer >= 0) WTnext[J.wt + (int64_t)kk * J.M + mm] = p;
+    if (J.layer >= 0) WTnext[J.wt + (int64_t)kk * J.M + (J.m0 + 4 * g + q)] = p;
   }
 }
 

@@ -109,6 +109,37 @@ def test_lazy_embedding_adam_matches_dense_over_long_gaps(rl):
     m.close()
 
 
+def test_lazy_adam_within_multi_step_calls_matches_dense(rl):
+    """The same long-gap stream as above, replayed as two calls of many steps: inside a call the
+    next step's rows are caught up beside the middle layers (k_ncf_mid's extra workgroups) and a
+    step's row Adam runs in the next step's row launch (k_ncf_rows), both paths a one-step call
+    never takes.  Against the oracle's dense Adam at 1e-6."""
+    U, I, d, L, B = 40, 48, 8, 2, 8
+    g = np.random.default_rng(29)
+    m = rl.NCF(U, I, d, L, batch_size=B, seed=5)
+    params = m.state_dict()
+    opt = N.Adam(params)
+    us, is_, ys = [], [], []
+    for k in range(260):
+        u = g.integers(0, U // 4, B)
+        i = g.integers(0, I // 4, B)
+        if k in (2, 250):
+            u[: B // 2] = g.integers(3 * U // 4, U, B // 2)
+            i[: B // 2] = g.integers(3 * I // 4, I, B // 2)
+        u[B - 1], i[B - 1] = u[0], i[0]  # a repeated row inside the step
+        y = (g.random(B) < 0.3).astype(np.float32)
+        grads, _ = N.grads(params, "NeuMF-end", L, u, i, y)
+        params = opt.step(params, grads)
+        us.append(u), is_.append(i), ys.append(y)
+    for lo, hi in ((0, 150), (150, 260)):
+        st = m.train_samples(np.concatenate(us[lo:hi]), np.concatenate(is_[lo:hi]), np.concatenate(ys[lo:hi]))
+        assert st["steps"] == hi - lo
+    got = m.state_dict()
+    for n in m.names:
+        np.testing.assert_allclose(got[n], params[n], rtol=0, atol=1e-6, err_msg=n)
+    m.close()
+
+
 def test_sampler_matches_oracle_and_ncfdata_semantics(rl, golden):
     f = golden("bpr_ml100k_replay.npz")
     pos = f["positives"].astype(np.int64)
